@@ -1,0 +1,196 @@
+#!/usr/bin/env python
+"""Headline benchmark: ResNet-50 bf16 data-parallel training throughput (images/s, whole job).
+
+BASELINE.json metric: "images/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X; scaling
+efficiency", config "ResNet-50 bf16 DDP on 8×MI355X, synthetic ImageNet-shaped input".
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched
+by ``torch.distributed.run`` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in the env), one rank per
+GPU over RCCL. W untimed steps, then exactly K timed steps bracketed by barrier +
+synchronize on both sides; the MAX elapsed over ranks is reported; rank 0 prints ONE JSON
+line. Weak scaling: the per-GPU batch is fixed as N grows.
+
+Each step is a full training step: H2D-free synthetic batch (already on device), forward,
+cross-entropy, backward with bucketed RCCL all-reduce overlapped with backward (xddp
+Reducer), fused SGD (momentum 0.9, wd 1e-4, fp32 master weights) — nothing skipped.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch-size", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--impl", choices=["xddp", "torch"], default="xddp",
+                    help="xddp = this framework; torch = torch.nn.parallel.DDP reference stack (comparison only)")
+    ap.add_argument("--norm", choices=["xddp", "torch"], default="torch", help="BatchNorm implementation")
+    ap.add_argument("--bucket-cap-mb", type=float, default=None)
+    ap.add_argument("--comm-dtype", default="none", help="gradient comm dtype (none = param dtype)")
+    ap.add_argument("--grad-as-bucket-view", type=int, default=1)
+    ap.add_argument("--channels-last", type=int, default=1)
+    ap.add_argument("--no-sync-accum", type=int, default=1, help="micro-batches per step (no_sync accumulation)")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def build_model(args, device):
+    from distributeddataparallel_amd import models
+
+    norm_layer = None
+    if args.norm == "xddp":
+        from distributeddataparallel_amd.ops.batch_norm import FusedBatchNorm2d
+
+        norm_layer = FusedBatchNorm2d
+    if args.model.startswith("resnet"):
+        m = getattr(models, args.model)(norm_layer=norm_layer)
+    else:
+        raise SystemExit(f"unknown model {args.model}")
+    m = m.to(device=device, dtype=torch.bfloat16)
+    if args.channels_last:
+        m = m.to(memory_format=torch.channels_last)
+    return m
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched via torch.distributed.run (one rank per GPU)")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        from distributeddataparallel_amd.utils.spawn import free_port
+
+        os.environ["MASTER_PORT"] = str(free_port())
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    torch.backends.cudnn.benchmark = bool(int(os.environ.get("XDDP_CUDNN_BENCHMARK", "0")))
+
+    if args.impl == "xddp":
+        import distributeddataparallel_amd as xddp
+        from distributeddataparallel_amd import distributed as dist
+        from distributeddataparallel_amd.optim import FusedSGD
+
+        dist.init_process_group("rccl", device_id=local_rank)
+    else:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=device)
+
+    torch.manual_seed(0)
+    model = build_model(args, device)
+    if args.impl == "xddp":
+        comm_dtype = None if args.comm_dtype == "none" else getattr(torch, args.comm_dtype)
+        ddp = xddp.DDP(model, device_ids=[local_rank], bucket_cap_mb=args.bucket_cap_mb,
+                       gradient_as_bucket_view=bool(args.grad_as_bucket_view), comm_dtype=comm_dtype)
+        opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, master_weights=True)
+        zero_kw = dict(set_to_none=not args.grad_as_bucket_view)
+    else:
+        ddp = torch.nn.parallel.DistributedDataParallel(
+            model, device_ids=[local_rank], bucket_cap_mb=args.bucket_cap_mb or 25,
+            gradient_as_bucket_view=bool(args.grad_as_bucket_view))
+        opt = torch.optim.SGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+        zero_kw = dict(set_to_none=not args.grad_as_bucket_view)
+
+    B, S = args.batch_size, args.image_size
+    mf = torch.channels_last if args.channels_last else torch.contiguous_format
+    g = torch.Generator(device=device).manual_seed(1234 + rank)
+    x = torch.randn(B, 3, S, S, device=device, generator=g).to(torch.bfloat16).contiguous(memory_format=mf)
+    y = torch.randint(0, 1000, (B,), device=device, generator=g)
+    micro = max(1, args.no_sync_accum)
+    xs, ys = x.chunk(micro), y.chunk(micro)
+
+    def step():
+        opt.zero_grad(**zero_kw)
+        for i in range(micro):
+            if i < micro - 1:
+                with ddp.no_sync():
+                    F.cross_entropy(ddp(xs[i]).float(), ys[i]).backward()
+            else:
+                loss = F.cross_entropy(ddp(xs[i]).float(), ys[i])
+                loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    et = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    if args.impl == "xddp":
+        dist.all_reduce(et, op=dist.ReduceOp.MAX)
+    else:
+        dist.all_reduce(et, op=dist.ReduceOp.MAX)
+    elapsed = float(et.item())
+    final_loss = float(loss.float().item())
+    ms = elapsed / args.steps * 1e3
+    total_imgs = B * world * args.steps
+    value = total_imgs / elapsed
+    if rank == 0:
+        out = {
+            "metric": "images/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X; scaling efficiency",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random ImageNet-shaped 3x224x224 bf16 inputs, random labels; random-init weights)",
+            "config": {
+                "model": args.model,
+                "global_batch": B * world,
+                "per_gpu_batch": B,
+                "seq_len": None,
+                "image_size": S,
+                "parallelism": f"dp{world}",
+                "impl": args.impl,
+                "norm": args.norm,
+                "optimizer": "SGD(momentum=0.9, wd=1e-4) fp32 master weights",
+                "channels_last": bool(args.channels_last),
+                "comm_dtype": args.comm_dtype,
+                "gradient_as_bucket_view": bool(args.grad_as_bucket_view),
+                "micro_batches": micro,
+            },
+            "final_loss": round(final_loss, 4),
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

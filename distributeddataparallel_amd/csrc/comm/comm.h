@@ -1,0 +1,138 @@
+// Communicator abstraction for xddp.
+//
+// Two native backends implement it:
+//   * RcclComm — RCCL over xGMI on a dedicated high-priority HIP stream, hipEvent-based Work,
+//                group coalescing, watchdog thread (timeout + async-error → ncclCommAbort).
+//   * TcpComm  — CPU ring collectives over a TCP full mesh, executed in FIFO order on a
+//                worker thread (the GPU-free multi-process test backend; gloo's role).
+// Every collective is recorded in a bounded ring buffer ("flight recorder", T20) that
+// Python can dump for desync/timeout triage.
+#pragma once
+
+#include <ATen/ATen.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <exception>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "store/tcp_store.h"
+
+namespace xddp {
+
+class Work {
+ public:
+  virtual ~Work() = default;
+  // Non-blocking completion query.
+  virtual bool is_completed() = 0;
+  // GPU: make the caller's current stream wait for the collective (no host block).
+  // CPU: block until done. Re-throws a collective error.
+  virtual void wait() = 0;
+  // Block the host until the collective has finished on the device.
+  virtual void synchronize() { wait(); }
+  virtual std::vector<at::Tensor> result() { return outputs; }
+  std::vector<at::Tensor> outputs;
+  int64_t seq = -1;
+};
+
+struct FlightEntry {
+  int64_t seq;
+  std::string op;
+  int64_t numel;
+  std::string dtype;
+  int64_t t_enqueue_ns;
+  int64_t t_done_ns;  // 0 while in flight
+  std::string state;  // "scheduled" | "completed" | "failed" | "timeout"
+};
+
+class FlightRecorder {
+ public:
+  explicit FlightRecorder(size_t cap = 2048) : cap_(cap) {}
+  int64_t record(const std::string& op, int64_t numel, at::ScalarType dt) {
+    std::lock_guard<std::mutex> g(mu_);
+    int64_t s = next_++;
+    if (ring_.size() == cap_) ring_.pop_front();
+    ring_.push_back(FlightEntry{s, op, numel, std::string(c10::toString(dt)), now_ns(), 0, "scheduled"});
+    return s;
+  }
+  void finish(int64_t seq, const char* state) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto it = ring_.rbegin(); it != ring_.rend(); ++it) {
+      if (it->seq == seq) {
+        it->t_done_ns = now_ns();
+        it->state = state;
+        return;
+      }
+    }
+  }
+  std::vector<FlightEntry> dump() {
+    std::lock_guard<std::mutex> g(mu_);
+    return std::vector<FlightEntry>(ring_.begin(), ring_.end());
+  }
+  int64_t count() const { return next_; }
+
+ private:
+  size_t cap_;
+  std::mutex mu_;
+  std::deque<FlightEntry> ring_;
+  std::atomic<int64_t> next_{0};
+};
+
+class Comm : public std::enable_shared_from_this<Comm> {
+ public:
+  Comm(int rank, int size) : rank_(rank), size_(size) {}
+  virtual ~Comm() = default;
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+  virtual std::string backend() const = 0;
+
+  virtual std::shared_ptr<Work> allreduce(at::Tensor t, RedOp op, double premul = 1.0) = 0;
+  virtual std::shared_ptr<Work> broadcast(at::Tensor t, int root) = 0;
+  // out.numel() == size * in.numel(); rank r's input lands at out[r*n:(r+1)*n].
+  virtual std::shared_ptr<Work> allgather(at::Tensor out, at::Tensor in) = 0;
+  // in.numel() == size * out.numel()
+  virtual std::shared_ptr<Work> reduce_scatter(at::Tensor out, at::Tensor in, RedOp op) = 0;
+  // equal splits: in/out numel divisible by size
+  virtual std::shared_ptr<Work> alltoall(at::Tensor out, at::Tensor in) = 0;
+  virtual std::shared_ptr<Work> send(at::Tensor t, int dst) = 0;
+  virtual std::shared_ptr<Work> recv(at::Tensor t, int src) = 0;
+  virtual std::shared_ptr<Work> barrier() = 0;
+  // Coalescing window (RCCL group); CPU backend runs ops in order anyway.
+  virtual void group_start() {}
+  virtual void group_end() {}
+  virtual void abort() {}
+  virtual void shutdown() {}
+
+  FlightRecorder& flight() { return flight_; }
+  // Debug: TORCH_DISTRIBUTED_DEBUG=DETAIL-style fingerprint check before each collective.
+  bool debug_fingerprint = false;
+
+ protected:
+  int rank_, size_;
+  FlightRecorder flight_;
+};
+
+// CPU backend ---------------------------------------------------------------------------
+std::shared_ptr<Comm> make_tcp_comm(std::shared_ptr<Store> store, int rank, int size,
+                                    std::chrono::milliseconds timeout);
+// `host` = address peers use to reach this rank's listening socket.
+std::shared_ptr<Comm> make_tcp_comm_host(std::shared_ptr<Store> store, int rank, int size,
+                                         std::chrono::milliseconds timeout, const std::string& host);
+
+// RCCL backend --------------------------------------------------------------------------
+std::shared_ptr<Comm> make_rccl_comm(std::shared_ptr<Store> store, int rank, int size, int device,
+                                     std::chrono::milliseconds timeout, bool high_priority_stream);
+
+// Extra RCCL-only entry points (no-ops / errors for other backends).
+std::string rccl_version();
+// Stream the RCCL comm runs on (raw handle as int64) — for tests/profiling.
+int64_t rccl_stream_handle(const std::shared_ptr<Comm>& c);
+
+}  // namespace xddp

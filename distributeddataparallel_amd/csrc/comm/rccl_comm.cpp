@@ -1,0 +1,397 @@
+// RCCL communicator over xGMI.
+//
+// Design (MI355X-first, not a ProcessGroupNCCL translation):
+//  * one communicator per process/GPU, created eagerly at init (no lazy first-collective
+//    stall inside the DDP constructor), unique id exchanged through the xddp store;
+//  * all collectives go on ONE dedicated high-priority HIP stream obtained from torch's
+//    stream pool, so backward kernels keep the CUs and the caching allocator knows the
+//    stream (recordStream on every buffer handed to RCCL);
+//  * Work completion = a timing-free hipEvent recorded after the RCCL call; wait() makes the
+//    caller's current stream wait on it (no host block);
+//  * ncclGroupStart/End coalescing for bucket bursts;
+//  * a watchdog thread polls in-flight events + ncclCommGetAsyncError and aborts the
+//    communicator on timeout/error so a hung peer surfaces as an exception, not a hang.
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <iostream>
+#include <list>
+#include <thread>
+
+#include "comm/comm.h"
+
+#define XDDP_NCCL_CHECK(expr)                                                                  \
+  do {                                                                                         \
+    ncclResult_t _r = (expr);                                                                  \
+    TORCH_CHECK(_r == ncclSuccess, "RCCL error: ", ncclGetErrorString(_r), " (" #expr ")");    \
+  } while (0)
+
+namespace xddp {
+
+namespace {
+
+ncclDataType_t to_nccl(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return ncclFloat32;
+    case at::kHalf: return ncclFloat16;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    case at::kByte: return ncclUint8;
+    case at::kChar: return ncclInt8;
+    case at::kBool: return ncclUint8;
+    case at::kFloat8_e4m3fn: return ncclFloat8e4m3;
+    case at::kFloat8_e5m2: return ncclFloat8e5m2;
+    default: TORCH_CHECK(false, "xddp rccl: unsupported dtype ", t);
+  }
+}
+
+ncclRedOp_t to_nccl(RedOp op, at::ScalarType t) {
+  if (t == at::kBool) {
+    if (op == RedOp::SUM || op == RedOp::MAX || op == RedOp::BOR) return ncclMax;
+    if (op == RedOp::PRODUCT || op == RedOp::MIN || op == RedOp::BAND) return ncclMin;
+  }
+  switch (op) {
+    case RedOp::SUM: return ncclSum;
+    case RedOp::AVG: return ncclAvg;
+    case RedOp::PRODUCT: return ncclProd;
+    case RedOp::MIN: return ncclMin;
+    case RedOp::MAX: return ncclMax;
+    default: TORCH_CHECK(false, "xddp rccl: unsupported reduce op ", static_cast<int>(op));
+  }
+}
+
+class EventPool {
+ public:
+  hipEvent_t get() {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!free_.empty()) {
+      auto e = free_.back();
+      free_.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    XDDP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+  }
+  void put(hipEvent_t e) {
+    std::lock_guard<std::mutex> g(mu_);
+    free_.push_back(e);
+  }
+
+ private:
+  std::mutex mu_;
+  std::vector<hipEvent_t> free_;
+};
+
+}  // namespace
+
+class RcclComm;
+
+class RcclWork : public Work {
+ public:
+  RcclWork(std::shared_ptr<EventPool> pool, int device, std::shared_ptr<std::atomic<int>> err)
+      : pool_(std::move(pool)), device_(device), err_(std::move(err)) {
+    ev = pool_->get();
+    t_start = now_ns();
+  }
+  ~RcclWork() override { pool_->put(ev); }
+  bool is_completed() override {
+    check_error();
+    return hipEventQuery(ev) == hipSuccess;
+  }
+  void wait() override {
+    check_error();
+    auto cur = c10::hip::getCurrentHIPStream(device_);
+    XDDP_HIP_CHECK(hipStreamWaitEvent(cur.stream(), ev, 0));
+  }
+  void synchronize() override {
+    check_error();
+    XDDP_HIP_CHECK(hipEventSynchronize(ev));
+    check_error();
+  }
+  void check_error() {
+    int e = err_->load();
+    TORCH_CHECK(e == 0, "xddp rccl: communicator is in error state (",
+                e == 1 ? "collective timed out; watchdog aborted the communicator" : "asynchronous RCCL error",
+                ")");
+  }
+  hipEvent_t ev;
+  int64_t t_start;
+
+ private:
+  std::shared_ptr<EventPool> pool_;
+  int device_;
+  std::shared_ptr<std::atomic<int>> err_;
+};
+
+class RcclComm : public Comm {
+ public:
+  RcclComm(std::shared_ptr<Store> store, int rank, int size, int device, std::chrono::milliseconds timeout,
+           bool high_priority)
+      : Comm(rank, size),
+        device_(device),
+        timeout_(timeout),
+        stream_(c10::hip::getStreamFromPool(high_priority, static_cast<c10::DeviceIndex>(device))),
+        pool_(std::make_shared<EventPool>()),
+        err_(std::make_shared<std::atomic<int>>(0)) {
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
+    ncclUniqueId id;
+    if (rank == 0) {
+      XDDP_NCCL_CHECK(ncclGetUniqueId(&id));
+      store->set("rccl/uid", std::string(reinterpret_cast<const char*>(&id), sizeof(id)));
+    } else {
+      std::string s = store->get("rccl/uid");
+      TORCH_CHECK(s.size() == sizeof(id), "xddp rccl: bad unique id size");
+      std::memcpy(&id, s.data(), sizeof(id));
+    }
+    XDDP_NCCL_CHECK(ncclCommInitRank(&comm_, size, id, rank));
+    watchdog_ = std::thread([this] { watchdog_loop(); });
+  }
+
+  ~RcclComm() override {
+    stop_watchdog();
+    // Deliberately no ncclCommDestroy here: at interpreter exit the HIP runtime may already
+    // be torn down. destroy_process_group() calls shutdown() explicitly.
+  }
+
+  std::string backend() const override { return "rccl"; }
+
+  std::shared_ptr<Work> allreduce(at::Tensor t, RedOp op, double premul) override {
+    check_tensor(t);
+    return launch("allreduce", t, {t}, [&](hipStream_t s) {
+      if (op == RedOp::PREMUL_SUM) {
+        TORCH_CHECK(at::isFloatingType(t.scalar_type()), "PREMUL_SUM needs a floating-point tensor");
+        // the host-immediate scalar must be in the tensor's dtype
+        ncclRedOp_t rop;
+        double d = premul;
+        float f = static_cast<float>(premul);
+        uint16_t half_bits = t.scalar_type() == at::kHalf ? at::Half(f).x : at::BFloat16(f).x;
+        void* sp = t.scalar_type() == at::kDouble  ? static_cast<void*>(&d)
+                   : t.scalar_type() == at::kFloat ? static_cast<void*>(&f)
+                                                   : static_cast<void*>(&half_bits);
+        XDDP_NCCL_CHECK(ncclRedOpCreatePreMulSum(&rop, sp, to_nccl(t.scalar_type()), ncclScalarHostImmediate, comm_));
+        XDDP_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), rop, comm_, s));
+        XDDP_NCCL_CHECK(ncclRedOpDestroy(rop, comm_));
+      } else {
+        XDDP_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()),
+                                      to_nccl(op, t.scalar_type()), comm_, s));
+      }
+    });
+  }
+
+  std::shared_ptr<Work> broadcast(at::Tensor t, int root) override {
+    check_tensor(t);
+    return launch("broadcast", t, {t}, [&](hipStream_t s) {
+      XDDP_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, s));
+    });
+  }
+
+  std::shared_ptr<Work> allgather(at::Tensor out, at::Tensor in) override {
+    check_contig(out);
+    check_contig(in);
+    TORCH_CHECK(out.numel() == in.numel() * size_, "allgather: output must hold size*input elements");
+    return launch("allgather", in, {out, in}, [&](hipStream_t s) {
+      XDDP_NCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), to_nccl(in.scalar_type()), comm_, s));
+    });
+  }
+
+  std::shared_ptr<Work> reduce_scatter(at::Tensor out, at::Tensor in, RedOp op) override {
+    check_contig(out);
+    check_contig(in);
+    TORCH_CHECK(in.numel() == out.numel() * size_, "reduce_scatter: input must hold size*output elements");
+    return launch("reduce_scatter", in, {out, in}, [&](hipStream_t s) {
+      XDDP_NCCL_CHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), to_nccl(in.scalar_type()),
+                                        to_nccl(op, in.scalar_type()), comm_, s));
+    });
+  }
+
+  std::shared_ptr<Work> alltoall(at::Tensor out, at::Tensor in) override {
+    check_contig(out);
+    check_contig(in);
+    TORCH_CHECK(in.numel() == out.numel() && in.numel() % size_ == 0, "alltoall: equal splits required");
+    return launch("alltoall", in, {out, in}, [&](hipStream_t s) {
+      XDDP_NCCL_CHECK(ncclAllToAll(in.data_ptr(), out.data_ptr(), in.numel() / size_, to_nccl(in.scalar_type()),
+                                   comm_, s));
+    });
+  }
+
+  std::shared_ptr<Work> send(at::Tensor t, int dst) override {
+    check_contig(t);
+    return launch("send", t, {t}, [&](hipStream_t s) {
+      XDDP_NCCL_CHECK(ncclSend(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), dst, comm_, s));
+    });
+  }
+
+  std::shared_ptr<Work> recv(at::Tensor t, int src) override {
+    check_contig(t);
+    return launch("recv", t, {t}, [&](hipStream_t s) {
+      XDDP_NCCL_CHECK(ncclRecv(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), src, comm_, s));
+    });
+  }
+
+  std::shared_ptr<Work> barrier() override {
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
+    if (!barrier_buf_.defined())
+      barrier_buf_ = at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, device_));
+    auto w = allreduce(barrier_buf_, RedOp::SUM, 1.0);
+    w->synchronize();
+    return w;
+  }
+
+  void group_start() override {
+    XDDP_NCCL_CHECK(ncclGroupStart());
+    in_group_++;
+  }
+  void group_end() override {
+    XDDP_NCCL_CHECK(ncclGroupEnd());
+    if (--in_group_ == 0) {
+      for (auto& w : group_works_) finish_launch(w);
+      group_works_.clear();
+    }
+  }
+
+  void abort() override {
+    std::lock_guard<std::mutex> g(comm_mu_);
+    if (comm_ && !aborted_) {
+      ncclCommAbort(comm_);
+      aborted_ = true;
+    }
+  }
+
+  void shutdown() override {
+    stop_watchdog();
+    std::lock_guard<std::mutex> g(comm_mu_);
+    if (comm_ && !aborted_ && !destroyed_) {
+      c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
+      XDDP_HIP_CHECK(hipStreamSynchronize(stream_.stream()));
+      ncclCommDestroy(comm_);
+      destroyed_ = true;
+    }
+  }
+
+  hipStream_t stream() const { return stream_.stream(); }
+
+ private:
+  void check_tensor(const at::Tensor& t) {
+    TORCH_CHECK(t.is_cuda(), "xddp rccl backend: tensor must be on a GPU");
+    TORCH_CHECK(t.device().index() == device_, "xddp rccl backend: tensor on device ", t.device().index(),
+                " but communicator is bound to device ", device_);
+    TORCH_CHECK(t.is_non_overlapping_and_dense(), "xddp rccl backend: tensor must be dense");
+  }
+  void check_contig(const at::Tensor& t) {
+    check_tensor(t);
+    TORCH_CHECK(t.is_contiguous(), "xddp rccl backend: tensor must be contiguous");
+  }
+
+  template <typename F>
+  std::shared_ptr<Work> launch(const char* name, const at::Tensor& meta, std::vector<at::Tensor> keep, F&& body) {
+    TORCH_CHECK(err_->load() == 0, "xddp rccl: communicator is in error state; re-create the process group");
+    TORCH_CHECK(!destroyed_, "xddp rccl: communicator was shut down");
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
+    auto cur = c10::hip::getCurrentHIPStream(device_);
+    hipEvent_t pre = pool_->get();
+    XDDP_HIP_CHECK(hipEventRecord(pre, cur.stream()));
+    XDDP_HIP_CHECK(hipStreamWaitEvent(stream_.stream(), pre, 0));
+    pool_->put(pre);
+    auto w = std::make_shared<RcclWork>(pool_, device_, err_);
+    w->seq = flight_.record(name, meta.numel(), meta.scalar_type());
+    body(stream_.stream());
+    for (auto& t : keep) {
+      if (t.defined() && t.is_cuda())
+        c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_);
+    }
+    w->outputs = std::move(keep);
+    if (in_group_ > 0) group_works_.push_back(w);
+    else finish_launch(w);
+    return w;
+  }
+
+  void finish_launch(const std::shared_ptr<RcclWork>& w) {
+    XDDP_HIP_CHECK(hipEventRecord(w->ev, stream_.stream()));
+    std::lock_guard<std::mutex> g(wd_mu_);
+    inflight_.push_back(w);
+  }
+
+  void watchdog_loop() {
+    while (!wd_stop_) {
+      {
+        std::unique_lock<std::mutex> g(wd_mu_);
+        wd_cv_.wait_for(g, std::chrono::milliseconds(100), [&] { return wd_stop_.load(); });
+        if (wd_stop_) break;
+        const int64_t now = now_ns();
+        for (auto it = inflight_.begin(); it != inflight_.end();) {
+          hipError_t q = hipEventQuery((*it)->ev);
+          if (q == hipSuccess) {
+            flight_.finish((*it)->seq, "completed");
+            it = inflight_.erase(it);
+          } else if (now - (*it)->t_start > static_cast<int64_t>(timeout_.count()) * 1000000LL) {
+            flight_.finish((*it)->seq, "timeout");
+            std::cerr << "[xddp rank " << rank_ << "] watchdog: collective seq " << (*it)->seq
+                      << " exceeded timeout of " << timeout_.count() << " ms; aborting communicator\n";
+            err_->store(1);
+            it = inflight_.erase(it);
+          } else {
+            ++it;
+          }
+        }
+      }
+      if (err_->load() == 0 && comm_ && !aborted_ && !destroyed_) {
+        ncclResult_t ae = ncclSuccess;
+        if (ncclCommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+          std::cerr << "[xddp rank " << rank_ << "] watchdog: async RCCL error " << ncclGetErrorString(ae) << "\n";
+          err_->store(2);
+        }
+      }
+      if (err_->load() != 0) abort();
+    }
+  }
+
+  void stop_watchdog() {
+    wd_stop_ = true;
+    wd_cv_.notify_all();
+    if (watchdog_.joinable()) watchdog_.join();
+  }
+
+  int device_;
+  std::chrono::milliseconds timeout_;
+  c10::hip::HIPStream stream_;
+  std::shared_ptr<EventPool> pool_;
+  std::shared_ptr<std::atomic<int>> err_;
+  ncclComm_t comm_ = nullptr;
+  std::mutex comm_mu_;
+  bool aborted_ = false;
+  bool destroyed_ = false;
+  int in_group_ = 0;
+  std::vector<std::shared_ptr<RcclWork>> group_works_;
+  at::Tensor barrier_buf_;
+  std::thread watchdog_;
+  std::atomic<bool> wd_stop_{false};
+  std::mutex wd_mu_;
+  std::condition_variable wd_cv_;
+  std::list<std::shared_ptr<RcclWork>> inflight_;
+};
+
+std::shared_ptr<Comm> make_rccl_comm(std::shared_ptr<Store> store, int rank, int size, int device,
+                                     std::chrono::milliseconds timeout, bool high_priority_stream) {
+  return std::make_shared<RcclComm>(std::move(store), rank, size, device, timeout, high_priority_stream);
+}
+
+std::string rccl_version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return std::to_string(v / 10000) + "." + std::to_string((v % 10000) / 100) + "." + std::to_string(v % 100);
+}
+
+int64_t rccl_stream_handle(const std::shared_ptr<Comm>& c) {
+  auto r = std::dynamic_pointer_cast<RcclComm>(c);
+  TORCH_CHECK(r, "not an RCCL communicator");
+  return reinterpret_cast<int64_t>(r->stream());
+}
+
+}  // namespace xddp

@@ -1,0 +1,182 @@
+// Device-side helpers for CDNA4 (gfx950): 16-byte vector loads/stores with in-register
+// dtype conversion (bf16 via v_cvt_pk_bf16_f32), 64-lane wave reductions.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace xddp {
+namespace dev {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+// Storage tags (bit-compatible with at::BFloat16 / at::Half).
+struct bf16_t {
+  uint16_t x;
+};
+struct f16_t {
+  uint16_t x;
+};
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  f32x2 v = {a, b};
+  bf16x2 r = __builtin_convertvector(v, bf16x2);  // v_cvt_pk_bf16_f32 (RNE) on gfx950
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint16_t f32_to_bf16(float a) { return (uint16_t)(pack_bf16x2(a, 0.f) & 0xffffu); }
+__device__ __forceinline__ float f16_to_f32(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+__device__ __forceinline__ uint32_t pack_f16x2(float a, float b) {
+  f32x2 v = {a, b};
+  f16x2 r = __builtin_convertvector(v, f16x2);
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint16_t f32_to_f16(float a) { return __builtin_bit_cast(uint16_t, (_Float16)a); }
+
+// ---- scalar access in compute type ------------------------------------------------
+template <typename T, typename C>
+struct Elem;
+template <typename C>
+struct Elem<float, C> {
+  static __device__ __forceinline__ C ld(const float* p, int64_t i) { return (C)p[i]; }
+  static __device__ __forceinline__ void st(float* p, int64_t i, C v) { p[i] = (float)v; }
+};
+template <typename C>
+struct Elem<double, C> {
+  static __device__ __forceinline__ C ld(const double* p, int64_t i) { return (C)p[i]; }
+  static __device__ __forceinline__ void st(double* p, int64_t i, C v) { p[i] = (double)v; }
+};
+template <typename C>
+struct Elem<bf16_t, C> {
+  static __device__ __forceinline__ C ld(const bf16_t* p, int64_t i) { return (C)bf16_to_f32(p[i].x); }
+  static __device__ __forceinline__ void st(bf16_t* p, int64_t i, C v) { p[i].x = f32_to_bf16((float)v); }
+};
+template <typename C>
+struct Elem<f16_t, C> {
+  static __device__ __forceinline__ C ld(const f16_t* p, int64_t i) { return (C)f16_to_f32(p[i].x); }
+  static __device__ __forceinline__ void st(f16_t* p, int64_t i, C v) { p[i].x = f32_to_f16((float)v); }
+};
+
+// ---- 8-wide vector access (16 B per instruction where the dtype allows) ------------
+template <typename T>
+struct Vec8;
+template <>
+struct Vec8<float> {
+  static constexpr int kAlign = 16;
+  template <typename C>
+  static __device__ __forceinline__ void ld(const float* p, C (&v)[8]) {
+    f32x4 a = *reinterpret_cast<const f32x4*>(p);
+    f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  template <typename C>
+  static __device__ __forceinline__ void st(float* p, const C (&v)[8]) {
+    f32x4 a = {(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+    f32x4 b = {(float)v[4], (float)v[5], (float)v[6], (float)v[7]};
+    *reinterpret_cast<f32x4*>(p) = a;
+    *reinterpret_cast<f32x4*>(p + 4) = b;
+  }
+};
+template <>
+struct Vec8<double> {
+  static constexpr int kAlign = 16;
+  template <typename C>
+  static __device__ __forceinline__ void ld(const double* p, C (&v)[8]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f64x2 a = *reinterpret_cast<const f64x2*>(p + 2 * j);
+      v[2 * j] = (C)a.x;
+      v[2 * j + 1] = (C)a.y;
+    }
+  }
+  template <typename C>
+  static __device__ __forceinline__ void st(double* p, const C (&v)[8]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f64x2 a = {(double)v[2 * j], (double)v[2 * j + 1]};
+      *reinterpret_cast<f64x2*>(p + 2 * j) = a;
+    }
+  }
+};
+template <>
+struct Vec8<bf16_t> {
+  static constexpr int kAlign = 16;
+  template <typename C>
+  static __device__ __forceinline__ void ld(const bf16_t* p, C (&v)[8]) {
+    u32x4 a = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = (C)__uint_as_float(a[j] << 16);
+      v[2 * j + 1] = (C)__uint_as_float(a[j] & 0xffff0000u);
+    }
+  }
+  template <typename C>
+  static __device__ __forceinline__ void st(bf16_t* p, const C (&v)[8]) {
+    u32x4 a;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = pack_bf16x2((float)v[2 * j], (float)v[2 * j + 1]);
+    *reinterpret_cast<u32x4*>(p) = a;
+  }
+};
+template <>
+struct Vec8<f16_t> {
+  static constexpr int kAlign = 16;
+  template <typename C>
+  static __device__ __forceinline__ void ld(const f16_t* p, C (&v)[8]) {
+    u32x4 a = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = (C)f16_to_f32((uint16_t)(a[j] & 0xffffu));
+      v[2 * j + 1] = (C)f16_to_f32((uint16_t)(a[j] >> 16));
+    }
+  }
+  template <typename C>
+  static __device__ __forceinline__ void st(f16_t* p, const C (&v)[8]) {
+    u32x4 a;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = pack_f16x2((float)v[2 * j], (float)v[2 * j + 1]);
+    *reinterpret_cast<u32x4*>(p) = a;
+  }
+};
+
+// ---- reductions over a 64-lane wavefront ------------------------------------------
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum; `scratch` must hold blockDim.x/64 entries. Result valid in all threads.
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  T r = 0;
+  for (int i = 0; i < nw; ++i) r += scratch[i];
+  __syncthreads();
+  return r;
+}
+
+// XCD-aware remap (bijective for any grid): consecutive logical tiles land on one XCD's L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+}  // namespace dev
+}  // namespace xddp

@@ -1,0 +1,536 @@
+"""Collective front-end: process groups over the native xddp communicators.
+
+API parity with the reference stack's ``torch.distributed`` surface that DDP users touch
+(SURVEY.md §2.2 T4): ``init_process_group`` / ``destroy_process_group`` / ``get_rank`` /
+``get_world_size`` / ``all_reduce`` / ``broadcast`` / ``all_gather`` / ``reduce_scatter`` /
+``all_to_all`` / ``send`` / ``recv`` / ``barrier`` / ``new_group`` and ``ReduceOp``.
+
+Backends (both native C++, see ``csrc/comm``):
+  * ``"rccl"`` (alias ``"nccl"``) — RCCL over xGMI, one process per GPU;
+  * ``"cpu"``  (alias ``"gloo"``) — TCP ring collectives, used for GPU-free multi-process runs.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+import sys
+from datetime import timedelta
+from typing import List, Optional, Sequence
+
+import torch
+
+from .._native import load
+from .rendezvous import advertise_host, rendezvous
+
+__all__ = [
+    "ReduceOp", "Backend", "ProcessGroup", "Work", "GroupMember", "init_process_group", "destroy_process_group",
+    "is_initialized", "get_rank", "get_world_size", "get_backend", "new_group", "all_reduce", "broadcast",
+    "all_gather", "all_gather_into_tensor", "reduce_scatter_tensor", "all_to_all_single", "send", "recv",
+    "barrier", "monitored_barrier", "broadcast_object_list", "all_gather_object", "get_default_group",
+    "coalescing", "is_available", "get_local_rank",
+]
+
+DEFAULT_TIMEOUT = timedelta(minutes=30)
+DEFAULT_RCCL_TIMEOUT = timedelta(minutes=10)
+
+
+def is_available() -> bool:
+    return True
+
+
+class ReduceOp:
+    """Reduction ops (values match the native ``RedOp`` enum)."""
+
+    SUM = "SUM"
+    AVG = "AVG"
+    PRODUCT = "PRODUCT"
+    MIN = "MIN"
+    MAX = "MAX"
+    BAND = "BAND"
+    BOR = "BOR"
+    BXOR = "BXOR"
+    PREMUL_SUM = "PREMUL_SUM"
+
+
+def _redop(op):
+    C = load()
+    if isinstance(op, C.RedOp):
+        return op
+    if op is None:
+        return C.RedOp.SUM
+    name = op if isinstance(op, str) else getattr(op, "name", str(op)).split(".")[-1]
+    return getattr(C.RedOp, name.upper())
+
+
+class Backend:
+    RCCL = "rccl"
+    NCCL = "rccl"  # on ROCm, "nccl" *is* RCCL
+    CPU = "cpu"
+    GLOO = "cpu"
+
+    @staticmethod
+    def normalize(name: Optional[str]) -> str:
+        if name is None:
+            return "rccl" if torch.cuda.is_available() else "cpu"
+        n = name.lower()
+        if n in ("nccl", "rccl", "cuda", "hip"):
+            return "rccl"
+        if n in ("gloo", "cpu", "tcp"):
+            return "cpu"
+        raise ValueError(f"unknown backend {name!r}")
+
+
+class Work:
+    """Async handle for one collective (wraps the native Work)."""
+
+    def __init__(self, native, outputs=None, post=None):
+        self._w = native
+        self._outputs = outputs
+        self._post = post
+        self._fut = None
+        self._done_post = False
+
+    def wait(self, timeout=None):
+        if self._w is not None:
+            self._w.wait()
+        if self._post is not None and not self._done_post:
+            self._done_post = True
+            self._post()
+        return True
+
+    def is_completed(self) -> bool:
+        return self._w is None or self._w.is_completed()
+
+    def is_success(self) -> bool:
+        return self.is_completed()
+
+    def synchronize(self):
+        if self._w is not None:
+            self._w.synchronize()
+        if self._post is not None and not self._done_post:
+            self._done_post = True
+            self._post()
+
+    def result(self):
+        return self._outputs if self._outputs is not None else (self._w.result() if self._w is not None else [])
+
+    def get_future(self) -> torch.futures.Future:
+        """A future completed once the collective is ordered before the caller's stream.
+
+        GPU: the caller's current stream waits on the collective's event, so consumers that
+        run on that stream (e.g. a ``.then`` callback launching kernels) are correctly
+        ordered, exactly like the reference stack's NCCL futures.
+        """
+        if self._fut is None:
+            self.wait()
+            self._fut = torch.futures.Future()
+            res = self.result()
+            self._fut.set_result(res)
+        return self._fut
+
+
+class _GroupMemberSentinel:
+    def __repr__(self):
+        return "NON_GROUP_MEMBER"
+
+
+class GroupMember:
+    WORLD = None
+    NON_GROUP_MEMBER = _GroupMemberSentinel()
+
+
+class ProcessGroup:
+    """A set of ranks sharing one native communicator."""
+
+    def __init__(self, comm, store, rank: int, size: int, backend: str, global_ranks: List[int], device,
+                 name: str, timeout: timedelta):
+        self.comm = comm
+        self.store = store
+        self._rank = rank
+        self._size = size
+        self._backend = backend
+        self.global_ranks = list(global_ranks)
+        self.device = device
+        self.group_name = name
+        self.timeout = timeout
+        self._coalescing = 0
+
+    # torch.distributed.ProcessGroup-style accessors
+    def rank(self) -> int:
+        return self._rank
+
+    def size(self) -> int:
+        return self._size
+
+    def name(self) -> str:
+        return self._backend
+
+    @property
+    def backend(self) -> str:
+        return self._backend
+
+    def __repr__(self):
+        return f"ProcessGroup({self._backend}, rank={self._rank}, size={self._size}, name={self.group_name})"
+
+    # -------- collectives (return Work) --------
+    def _prep(self, t: torch.Tensor) -> torch.Tensor:
+        if self._backend == "cpu" and t.device.type != "cpu":
+            raise RuntimeError("the cpu backend only handles CPU tensors")
+        return t
+
+    def allreduce(self, tensor, op=ReduceOp.SUM, premul: float = 1.0) -> Work:
+        t = self._prep(tensor)
+        return Work(self.comm.allreduce(t, _redop(op), float(premul)), [tensor])
+
+    def broadcast(self, tensor, src: int = 0) -> Work:
+        return Work(self.comm.broadcast(self._prep(tensor), int(src)), [tensor])
+
+    def allgather_into_tensor(self, output, input) -> Work:
+        return Work(self.comm.allgather(output, input), [output])
+
+    def reduce_scatter_tensor(self, output, input, op=ReduceOp.SUM) -> Work:
+        return Work(self.comm.reduce_scatter(output, input, _redop(op)), [output])
+
+    def alltoall_base(self, output, input) -> Work:
+        return Work(self.comm.alltoall(output, input), [output])
+
+    def send(self, tensor, dst: int) -> Work:
+        return Work(self.comm.send(tensor, int(dst)), [tensor])
+
+    def recv(self, tensor, src: int) -> Work:
+        return Work(self.comm.recv(tensor, int(src)), [tensor])
+
+    def barrier(self) -> Work:
+        return Work(self.comm.barrier(), [])
+
+    def flight_records(self):
+        return self.comm.flight_records()
+
+    def shutdown(self):
+        self.comm.shutdown()
+
+    def abort(self):
+        self.comm.abort()
+
+
+class _World:
+    def __init__(self):
+        self.default_pg: Optional[ProcessGroup] = None
+        self.groups: dict = {}
+        self.group_count = 0
+        self.store = None
+
+
+_world = _World()
+
+
+def _excepthook_prefix(rank: int):
+    prev = sys.excepthook
+
+    def hook(tp, val, tb):
+        sys.stderr.write(f"[rank{rank}]: ")
+        prev(tp, val, tb)
+
+    sys.excepthook = hook
+
+
+def _device_for(backend: str, device_id):
+    if backend != "rccl":
+        return torch.device("cpu")
+    if device_id is None:
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        n = torch.cuda.device_count()
+        device_id = local % max(n, 1)
+    if isinstance(device_id, torch.device):
+        device_id = device_id.index if device_id.index is not None else 0
+    torch.cuda.set_device(int(device_id))
+    return torch.device("cuda", int(device_id))
+
+
+def _make_comm(backend: str, store, rank: int, size: int, device, timeout: timedelta, master_addr: str):
+    C = load()
+    if backend == "rccl":
+        hp = os.environ.get("XDDP_COMM_HIGH_PRIORITY", "1") != "0"
+        return C.make_rccl_comm(store, rank, size, device.index, timeout.total_seconds(), hp)
+    return C.make_cpu_comm(store, rank, size, timeout.total_seconds(), advertise_host(master_addr))
+
+
+def init_process_group(backend: Optional[str] = None, init_method: Optional[str] = None,
+                       timeout: Optional[timedelta] = None, world_size: int = -1, rank: int = -1,
+                       store=None, group_name: str = "", device_id=None) -> ProcessGroup:
+    """Create the default process group (reference: ``dist.init_process_group``).
+
+    Unlike the reference stack the communicator is created eagerly and bound to
+    ``device_id`` (default ``LOCAL_RANK``), fixing quirk Q2 (no ``set_device``).
+    """
+    if _world.default_pg is not None:
+        raise RuntimeError("trying to initialize the default process group twice")
+    C = load()
+    be = Backend.normalize(backend)
+    if timeout is None:
+        timeout = DEFAULT_RCCL_TIMEOUT if be == "rccl" else DEFAULT_TIMEOUT
+    master_addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    if store is None:
+        store, rank, world_size, master_addr = rendezvous(init_method, rank, world_size, timeout)
+    else:
+        if rank < 0 or world_size <= 0:
+            raise ValueError("rank and world_size are required when passing a store")
+    device = _device_for(be, device_id)
+    pstore = C.PrefixStore("default_pg", store)
+    comm = _make_comm(be, pstore, rank, world_size, device, timeout, master_addr)
+    pg = ProcessGroup(comm, pstore, rank, world_size, be, list(range(world_size)), device,
+                      group_name or "default_pg", timeout)
+    _world.default_pg = pg
+    _world.store = store
+    _world.groups[pg.group_name] = pg
+    GroupMember.WORLD = pg
+    _excepthook_prefix(rank)
+    if os.environ.get("XDDP_INIT_BARRIER", "1") == "1" and world_size > 1:
+        # store-based barrier: every rank's communicator is up before returning
+        n = store.add("xddp/init_barrier", 1)
+        if n == world_size:
+            store.set("xddp/init_done", "1")
+        store.wait(["xddp/init_done"], timeout.total_seconds())
+    return pg
+
+
+def is_initialized() -> bool:
+    return _world.default_pg is not None
+
+
+def get_default_group() -> ProcessGroup:
+    if _world.default_pg is None:
+        raise RuntimeError("Default process group has not been initialized, please call init_process_group")
+    return _world.default_pg
+
+
+def _resolve(group) -> ProcessGroup:
+    if group is None or group is GroupMember.WORLD:
+        return get_default_group()
+    if group is GroupMember.NON_GROUP_MEMBER:
+        raise RuntimeError("this rank is not part of the group")
+    return group
+
+
+def destroy_process_group(group=None):
+    """Shut down communicators (sub-groups first, then the default group)."""
+    if group is None or group is GroupMember.WORLD:
+        for name in sorted(_world.groups.keys(), reverse=True):
+            pg = _world.groups[name]
+            if pg is not _world.default_pg:
+                try:
+                    pg.shutdown()
+                except Exception:
+                    pass
+        if _world.default_pg is not None:
+            try:
+                _world.default_pg.shutdown()
+            except Exception:
+                pass
+        _world.groups.clear()
+        _world.default_pg = None
+        _world.group_count = 0
+        _world.store = None
+        GroupMember.WORLD = None
+    else:
+        pg = _resolve(group)
+        pg.shutdown()
+        _world.groups.pop(pg.group_name, None)
+
+
+def get_rank(group=None) -> int:
+    if group is None and _world.default_pg is None:
+        return 0
+    if group is GroupMember.NON_GROUP_MEMBER:
+        return -1
+    return _resolve(group).rank()
+
+
+def get_world_size(group=None) -> int:
+    if group is None and _world.default_pg is None:
+        return 1
+    if group is GroupMember.NON_GROUP_MEMBER:
+        return -1
+    return _resolve(group).size()
+
+
+def get_local_rank() -> int:
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def get_backend(group=None) -> str:
+    return _resolve(group).backend
+
+
+def new_group(ranks: Optional[Sequence[int]] = None, timeout: Optional[timedelta] = None, backend=None):
+    """Create a sub-group. Must be called by every rank of the default group (same order)."""
+    C = load()
+    world = get_default_group()
+    ranks = sorted(range(world.size()) if ranks is None else ranks)
+    _world.group_count += 1
+    name = f"group_{_world.group_count}"
+    be = Backend.normalize(backend) if backend is not None else world.backend
+    if world.rank() not in ranks:
+        return GroupMember.NON_GROUP_MEMBER
+    timeout = timeout or world.timeout
+    sub_rank = ranks.index(world.rank())
+    store = C.PrefixStore(name, _world.store)
+    comm = _make_comm(be, store, sub_rank, len(ranks), world.device if be == "rccl" else torch.device("cpu"),
+                      timeout, os.environ.get("MASTER_ADDR", "127.0.0.1"))
+    pg = ProcessGroup(comm, store, sub_rank, len(ranks), be, ranks, world.device, name, timeout)
+    _world.groups[name] = pg
+    return pg
+
+
+def get_process_group_ranks(group) -> List[int]:
+    return list(_resolve(group).global_ranks)
+
+
+def _group_rank(pg: ProcessGroup, global_rank: int) -> int:
+    if pg is _world.default_pg:
+        return global_rank
+    return pg.global_ranks.index(global_rank)
+
+
+# ---------------------------------------------------------------------------------------
+# functional collectives
+# ---------------------------------------------------------------------------------------
+def _ret(work: Work, async_op: bool):
+    if async_op:
+        return work
+    work.wait()
+    return None
+
+
+def all_reduce(tensor, op=ReduceOp.SUM, group=None, async_op=False):
+    return _ret(_resolve(group).allreduce(tensor, op), async_op)
+
+
+def broadcast(tensor, src=0, group=None, async_op=False):
+    pg = _resolve(group)
+    return _ret(pg.broadcast(tensor, _group_rank(pg, src)), async_op)
+
+
+def all_gather_into_tensor(output_tensor, input_tensor, group=None, async_op=False):
+    return _ret(_resolve(group).allgather_into_tensor(output_tensor, input_tensor), async_op)
+
+
+def all_gather(tensor_list, tensor, group=None, async_op=False):
+    pg = _resolve(group)
+    flat = torch.empty((pg.size(),) + tuple(tensor.shape), dtype=tensor.dtype, device=tensor.device)
+    src = tensor.contiguous()
+
+    def post():
+        for i, t in enumerate(tensor_list):
+            t.copy_(flat[i])
+
+    w = pg.allgather_into_tensor(flat, src)
+    w._post = post
+    w._outputs = tensor_list
+    return _ret(w, async_op)
+
+
+def reduce_scatter_tensor(output, input, op=ReduceOp.SUM, group=None, async_op=False):
+    return _ret(_resolve(group).reduce_scatter_tensor(output, input, op), async_op)
+
+
+def all_to_all_single(output, input, output_split_sizes=None, input_split_sizes=None, group=None, async_op=False):
+    if output_split_sizes is not None or input_split_sizes is not None:
+        raise NotImplementedError("uneven all_to_all splits are not supported yet")
+    return _ret(_resolve(group).alltoall_base(output, input), async_op)
+
+
+def send(tensor, dst, group=None):
+    pg = _resolve(group)
+    pg.send(tensor, _group_rank(pg, dst)).wait()
+
+
+def recv(tensor, src, group=None):
+    pg = _resolve(group)
+    pg.recv(tensor, _group_rank(pg, src)).wait()
+    return src
+
+
+def isend(tensor, dst, group=None) -> Work:
+    pg = _resolve(group)
+    return pg.send(tensor, _group_rank(pg, dst))
+
+
+def irecv(tensor, src, group=None) -> Work:
+    pg = _resolve(group)
+    return pg.recv(tensor, _group_rank(pg, src))
+
+
+def barrier(group=None, async_op=False, device_ids=None):
+    return _ret(_resolve(group).barrier(), async_op)
+
+
+def monitored_barrier(group=None, timeout=None, wait_all_ranks=False):
+    """Store-based barrier that names the ranks that failed to arrive (CPU-side)."""
+    pg = _resolve(group)
+    timeout = timeout or pg.timeout
+    store = pg.store
+    gen = store.add("monitored_barrier/gen", 0) // max(pg.size(), 1)
+    key = f"monitored_barrier/{gen}"
+    store.add(key, 1)
+    store.add("monitored_barrier/gen", 1)
+    import time
+
+    deadline = time.time() + timeout.total_seconds()
+    while store.add(key, 0) < pg.size():
+        if time.time() > deadline:
+            raise RuntimeError(f"monitored_barrier timed out: {store.add(key, 0)}/{pg.size()} ranks arrived")
+        time.sleep(0.005)
+
+
+@contextlib.contextmanager
+def coalescing(group=None):
+    """Coalesce the collectives issued inside into one RCCL group launch."""
+    pg = _resolve(group)
+    pg.comm.group_start()
+    try:
+        yield
+    finally:
+        pg.comm.group_end()
+
+
+def broadcast_object_list(object_list, src=0, group=None, device=None):
+    import pickle
+
+    pg = _resolve(group)
+    dev = pg.device if pg.backend == "rccl" else torch.device("cpu")
+    if pg.rank() == _group_rank(pg, src):
+        payload = pickle.dumps(list(object_list))
+        n = torch.tensor([len(payload)], dtype=torch.long, device=dev)
+    else:
+        payload = b""
+        n = torch.zeros(1, dtype=torch.long, device=dev)
+    broadcast(n, src, group)
+    size = int(n.item())
+    buf = (torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev) if payload
+           else torch.zeros(size, dtype=torch.uint8, device=dev))
+    broadcast(buf, src, group)
+    if pg.rank() != _group_rank(pg, src):
+        # our own pickles, produced by the src rank of this job
+        objs = pickle.loads(bytes(buf.cpu().numpy()))
+        for i, o in enumerate(objs):
+            object_list[i] = o
+
+
+def all_gather_object(object_list, obj, group=None):
+    import pickle
+
+    pg = _resolve(group)
+    dev = pg.device if pg.backend == "rccl" else torch.device("cpu")
+    payload = pickle.dumps(obj)
+    n = torch.tensor([len(payload)], dtype=torch.long, device=dev)
+    sizes = torch.zeros(pg.size(), dtype=torch.long, device=dev)
+    all_gather_into_tensor(sizes, n, group)
+    mx = int(sizes.max().item())
+    buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
+    buf[: len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev)
+    out = torch.zeros(pg.size() * mx, dtype=torch.uint8, device=dev)
+    all_gather_into_tensor(out, buf, group)
+    out = out.cpu().view(pg.size(), mx)
+    for i in range(pg.size()):
+        object_list[i] = pickle.loads(bytes(out[i, : int(sizes[i])].numpy()))

@@ -1,0 +1,188 @@
+"""ResNet family (torchvision-identical structure, random init).
+
+The reference trains ``torchvision.models.resnet18`` with its ``fc`` replaced by
+``Linear(512, 10)`` (``ref:dpp.py:11-18``); BASELINE.json's headline config is ResNet-50.
+torchvision is not installed here, so the architectures are rebuilt layer-for-layer
+(parameter counts match torchvision: ResNet-50 = 25,557,032; ResNet-18/10-class =
+11,181,642 — SURVEY.md Appendix A). ``norm_layer`` lets the bench swap in xddp's fused
+HIP BatchNorm(+ReLU) without changing the parameter/buffer layout or state_dict keys.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Type, Union
+
+import torch
+import torch.nn as nn
+
+__all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50", "resnet101", "resnet152",
+           "SimpleCNN"]
+
+
+def conv3x3(i, o, stride=1, groups=1, dilation=1):
+    return nn.Conv2d(i, o, 3, stride=stride, padding=dilation, groups=groups, bias=False, dilation=dilation)
+
+
+def conv1x1(i, o, stride=1):
+    return nn.Conv2d(i, o, 1, stride=stride, bias=False)
+
+
+def _bn_relu(norm_layer, c):
+    """Return (bn, act). A fused norm layer (``fuses_relu``) absorbs the ReLU."""
+    bn = norm_layer(c)
+    if getattr(bn, "fuses_relu", False):
+        bn.relu = True
+        return bn, nn.Identity()
+    return bn, nn.ReLU(inplace=True)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64, dilation=1,
+                 norm_layer=None):
+        super().__init__()
+        norm_layer = norm_layer or nn.BatchNorm2d
+        self.conv1 = conv3x3(inplanes, planes, stride)
+        self.bn1, self.act1 = _bn_relu(norm_layer, planes)
+        self.conv2 = conv3x3(planes, planes)
+        self.bn2 = norm_layer(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+        self._fused_add = getattr(self.bn2, "supports_add_relu", False)
+
+    def forward(self, x):
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.act1(self.bn1(self.conv1(x)))
+        out = self.conv2(out)
+        if self._fused_add:
+            return self.bn2(out, residual=identity, relu=True)
+        out = self.bn2(out)
+        out += identity
+        return self.relu(out)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64, dilation=1,
+                 norm_layer=None):
+        super().__init__()
+        norm_layer = norm_layer or nn.BatchNorm2d
+        width = int(planes * (base_width / 64.0)) * groups
+        self.conv1 = conv1x1(inplanes, width)
+        self.bn1, self.act1 = _bn_relu(norm_layer, width)
+        self.conv2 = conv3x3(width, width, stride, groups, dilation)
+        self.bn2, self.act2 = _bn_relu(norm_layer, width)
+        self.conv3 = conv1x1(width, planes * self.expansion)
+        self.bn3 = norm_layer(planes * self.expansion)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+        self._fused_add = getattr(self.bn3, "supports_add_relu", False)
+
+    def forward(self, x):
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.act1(self.bn1(self.conv1(x)))
+        out = self.act2(self.bn2(self.conv2(out)))
+        out = self.conv3(out)
+        if self._fused_add:
+            return self.bn3(out, residual=identity, relu=True)
+        out = self.bn3(out)
+        out += identity
+        return self.relu(out)
+
+
+class ResNet(nn.Module):
+    def __init__(self, block: Type[Union[BasicBlock, Bottleneck]], layers: List[int], num_classes: int = 1000,
+                 zero_init_residual: bool = False, groups: int = 1, width_per_group: int = 64,
+                 norm_layer: Optional[Callable[..., nn.Module]] = None):
+        super().__init__()
+        norm_layer = norm_layer or nn.BatchNorm2d
+        self._norm_layer = norm_layer
+        self.inplanes = 64
+        self.dilation = 1
+        self.groups = groups
+        self.base_width = width_per_group
+        self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1, self.relu = _bn_relu(norm_layer, self.inplanes)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif hasattr(m, "weight") and hasattr(m, "running_mean") and m.weight is not None:
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.constant_(m.bn3.weight, 0)
+                elif isinstance(m, BasicBlock):
+                    nn.init.constant_(m.bn2.weight, 0)
+
+    def _make_layer(self, block, planes, blocks, stride=1):
+        norm_layer = self._norm_layer
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
+                                       norm_layer(planes * block.expansion))
+        layers = [block(self.inplanes, planes, stride, downsample, self.groups, self.base_width, self.dilation,
+                        norm_layer)]
+        self.inplanes = planes * block.expansion
+        for _ in range(1, blocks):
+            layers.append(block(self.inplanes, planes, groups=self.groups, base_width=self.base_width,
+                                dilation=self.dilation, norm_layer=norm_layer))
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.relu(self.bn1(self.conv1(x)))
+        x = self.maxpool(x)
+        x = self.layer1(x)
+        x = self.layer2(x)
+        x = self.layer3(x)
+        x = self.layer4(x)
+        x = self.avgpool(x)
+        x = torch.flatten(x, 1)
+        return self.fc(x)
+
+
+def resnet18(**kw):
+    return ResNet(BasicBlock, [2, 2, 2, 2], **kw)
+
+
+def resnet34(**kw):
+    return ResNet(BasicBlock, [3, 4, 6, 3], **kw)
+
+
+def resnet50(**kw):
+    return ResNet(Bottleneck, [3, 4, 6, 3], **kw)
+
+
+def resnet101(**kw):
+    return ResNet(Bottleneck, [3, 4, 23, 3], **kw)
+
+
+def resnet152(**kw):
+    return ResNet(Bottleneck, [3, 8, 36, 3], **kw)
+
+
+class SimpleCNN(nn.Module):
+    """The reference's model wrapper (``ref:dpp.py:11-18``): ResNet-18 with a 10-class head.
+
+    Random init instead of ImageNet weights (no network; quirk Q3). state_dict keys match the
+    reference (``model.conv1.weight`` ... ; ``module.model.*`` once wrapped in DDP).
+    """
+
+    def __init__(self, num_classes: int = 10, norm_layer=None):
+        super().__init__()
+        self.model = resnet18(norm_layer=norm_layer)
+        self.model.fc = nn.Linear(512, num_classes)
+
+    def forward(self, x):
+        return self.model(x)

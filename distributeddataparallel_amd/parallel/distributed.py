@@ -1,0 +1,411 @@
+"""``DistributedDataParallel`` — the user-facing DDP wrapper over the native xddp Reducer.
+
+API and behaviour follow the reference stack's wrapper (SURVEY.md §2.2 T6a–T6m,
+``torch/nn/parallel/distributed.py:328-2434``, used by ``ref:dpp.py:39``):
+
+* constructor signature (``device_ids``, ``broadcast_buffers``, ``bucket_cap_mb``,
+  ``find_unused_parameters``, ``gradient_as_bucket_view``, ``static_graph``, ...);
+* init-time parameter verification + rank-0 broadcast of params and buffers;
+* iteration 0 uses one bucket (or [1 MiB, cap] with ``find_unused_parameters``), then the
+  buckets are rebuilt once in gradient-ready order;
+* per-forward buffer broadcast, ``no_sync()``, ``join()``, comm hooks, static graph,
+  ``module.``-prefixed ``state_dict`` (the wrapped net lives in ``self.module``).
+
+MI355X additions (opt-in knobs, defaults keep reference semantics):
+
+* ``comm_dtype`` — communicate gradients in bf16/fp16 with a fused cast inside the bucket
+  pack kernel (the builtin ``BF16_COMPRESS`` hook without a Python round trip);
+* ``bucket_cap_mb`` defaults can be overridden per job via ``XDDP_BUCKET_CAP_MB``.
+"""
+from __future__ import annotations
+
+import copy
+import logging
+import os
+import sys
+import weakref
+from contextlib import contextmanager
+from enum import Enum, auto
+from typing import Any, Callable, List, Optional
+
+import torch
+import torch.nn as nn
+from torch.autograd.profiler import record_function
+
+from .. import distributed as xdist
+from .._native import load
+from .join import Join, Joinable, JoinHook
+
+logger = logging.getLogger(__name__)
+
+DEFAULT_FIRST_BUCKET_BYTES = 1024 * 1024
+DEFAULT_BUCKET_CAP_MB = 25
+BROADCAST_BUCKET_BYTES = 250 * 1024 * 1024
+
+__all__ = ["DistributedDataParallel", "BuiltinCommHookType"]
+
+
+class BuiltinCommHookType(Enum):
+    ALLREDUCE = auto()
+    FP16_COMPRESS = auto()
+    BF16_COMPRESS = auto()
+
+
+def _find_tensors(obj) -> List[torch.Tensor]:
+    if isinstance(obj, torch.Tensor):
+        return [obj]
+    if isinstance(obj, (list, tuple)):
+        return [t for o in obj for t in _find_tensors(o)]
+    if isinstance(obj, dict):
+        return [t for o in obj.values() for t in _find_tensors(o)]
+    if hasattr(obj, "__dataclass_fields__"):
+        return [t for f in obj.__dataclass_fields__ for t in _find_tensors(getattr(obj, f))]
+    return []
+
+
+def _to_device(obj, device, non_blocking=True):
+    if isinstance(obj, torch.Tensor):
+        return obj if obj.device == device else obj.to(device, non_blocking=non_blocking)
+    if isinstance(obj, tuple) and hasattr(obj, "_fields"):
+        return type(obj)(*(_to_device(o, device, non_blocking) for o in obj))
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_device(o, device, non_blocking) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _to_device(v, device, non_blocking) for k, v in obj.items()}
+    return obj
+
+
+class _DDPJoinHook(JoinHook):
+    """Shadows one DDP iteration's collectives on a rank that ran out of inputs."""
+
+    def __init__(self, ddp: "DistributedDataParallel", divide_by_initial_world_size: bool):
+        self.ddp = ddp
+        self.ddp._divide_by_initial_world_size = divide_by_initial_world_size
+
+    def main_hook(self):
+        ddp = self.ddp
+        ddp.reducer.rebuild_buckets()
+        ddp._check_and_sync_module_buffers()
+        # zero gradient all-reduce per bucket (same order/sizes as the non-joined ranks)
+        for z in ddp.reducer.zeros_like_buckets():
+            ddp.process_group.allreduce(z, xdist.ReduceOp.SUM).wait()
+        if ddp.find_unused_parameters:
+            m = torch.zeros(len(ddp._module_parameters), dtype=torch.int32, device=ddp._comm_device)
+            ddp.process_group.allreduce(m, xdist.ReduceOp.SUM).wait()
+
+    def post_hook(self, is_last_joiner: bool):
+        self.ddp._sync_final_model(is_last_joiner)
+
+
+class DistributedDataParallel(nn.Module, Joinable):
+    def __init__(
+        self,
+        module: nn.Module,
+        device_ids: Optional[List[Any]] = None,
+        output_device=None,
+        dim: int = 0,
+        broadcast_buffers: bool = True,
+        init_sync: bool = True,
+        process_group=None,
+        bucket_cap_mb: Optional[float] = None,
+        find_unused_parameters: bool = False,
+        check_reduction: bool = False,
+        gradient_as_bucket_view: bool = False,
+        static_graph: bool = False,
+        delay_all_reduce_named_params=None,
+        param_to_hook_all_reduce=None,
+        mixed_precision=None,
+        device_mesh=None,
+        comm_dtype: Optional[torch.dtype] = None,
+        first_bucket_cap_mb: Optional[float] = None,
+    ):
+        super().__init__()
+        Joinable.__init__(self)
+        C = load()
+        if device_mesh is not None:
+            raise NotImplementedError("device_mesh is not supported; pass process_group")
+        if delay_all_reduce_named_params is not None or param_to_hook_all_reduce is not None:
+            raise NotImplementedError("delay_all_reduce_named_params is not supported")
+        self.process_group = process_group if process_group is not None else xdist.get_default_group()
+        self.module = module
+        self.dim = dim
+        self.broadcast_buffers = broadcast_buffers
+        self.find_unused_parameters = find_unused_parameters
+        self.gradient_as_bucket_view = gradient_as_bucket_view
+        self.require_backward_grad_sync = True
+        self.require_forward_param_sync = True
+        self.static_graph = False
+        self._divide_by_initial_world_size = True
+        self.mixed_precision = mixed_precision
+        if mixed_precision is not None:
+            raise NotImplementedError("native mixed_precision shadow params are not supported; use comm_dtype "
+                                      "or a bf16 model with a master-weight optimizer")
+
+        self._params_and_buffers_to_ignore = set(getattr(module, "_ddp_params_and_buffers_to_ignore", []))
+        named = [(n, p) for n, p in module.named_parameters() if n not in self._params_and_buffers_to_ignore]
+        seen = set()
+        self._module_parameters, self._param_names = [], []
+        for n, p in named:
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                self._module_parameters.append(p)
+                self._param_names.append(n)
+        if not self._module_parameters:
+            raise RuntimeError("DistributedDataParallel is not needed when a module doesn't have any parameter "
+                               "that requires a gradient.")
+        devices = {p.device for p in self._module_parameters}
+        if len(devices) > 1:
+            raise ValueError(f"DistributedDataParallel's input module must be on a single device, found {devices}")
+        self._param_device = next(iter(devices))
+        self.device_type = self._param_device.type
+        if device_ids is not None and len(device_ids) > 1:
+            raise ValueError("device_ids can only be None or contain a single element.")
+        if self.device_type == "cpu" or device_ids is None or len(device_ids) == 0:
+            self.device_ids = None
+            self.output_device = None
+        else:
+            self.device_ids = [torch.device("cuda", d) if isinstance(d, int) else torch.device(d) for d in device_ids]
+            self.output_device = self.device_ids[0] if output_device is None else torch.device(output_device)
+        if self.process_group.backend == "rccl" and self.device_type != "cuda":
+            raise ValueError("the rccl backend needs the module on a GPU")
+        if self.process_group.backend == "cpu" and self.device_type != "cpu":
+            raise ValueError("the cpu backend needs the module on the CPU")
+        self._comm_device = self._param_device
+
+        env_cap = os.environ.get("XDDP_BUCKET_CAP_MB")
+        if bucket_cap_mb is None:
+            bucket_cap_mb = float(env_cap) if env_cap else DEFAULT_BUCKET_CAP_MB
+        self.bucket_bytes_cap = int(bucket_cap_mb * 1024 * 1024)
+        self.first_bucket_bytes_cap = int(first_bucket_cap_mb * 1024 * 1024) if first_bucket_cap_mb else \
+            DEFAULT_FIRST_BUCKET_BYTES
+        self.broadcast_bucket_size = BROADCAST_BUCKET_BYTES
+        self._comm_dtype = comm_dtype
+
+        self._buffers_list = [b for n, b in module.named_buffers() if n not in self._params_and_buffers_to_ignore]
+        if init_sync:
+            C.verify_params_across_processes(self.process_group.comm, self._module_parameters)
+            self._sync_module_states(src=0)
+
+        self._build_reducer()
+        self._comm_hooks = []
+        self._logging_sample_rate = 100
+        if static_graph:
+            self._set_static_graph()
+
+    # ----------------------------------------------------------------------------- setup
+    def _build_reducer(self):
+        C = load()
+        params = self._module_parameters
+        if self.find_unused_parameters:
+            limits = [self.first_bucket_bytes_cap, self.bucket_bytes_cap]
+        else:
+            limits = [sys.maxsize]
+        idx, lims = C.compute_bucket_assignment_by_size(params, limits)
+        idx, lims = list(reversed(idx)), list(reversed(lims))
+        cd = "" if self._comm_dtype is None else str(self._comm_dtype).replace("torch.", "")
+        self.reducer = C.Reducer(
+            params, idx, lims, self.process_group.comm,
+            find_unused_parameters=self.find_unused_parameters,
+            gradient_as_bucket_view=self.gradient_as_bucket_view,
+            static_graph=False,
+            bucket_bytes_cap=self.bucket_bytes_cap,
+            first_bucket_bytes_cap=self.first_bucket_bytes_cap,
+            comm_dtype=cd,
+            param_names=self._param_names,
+        )
+
+    def _sync_module_states(self, src: int = 0):
+        C = load()
+        tensors = [p.detach() for p in self.module.parameters()] + [b for b in self._buffers_list]
+        tensors = [t for t in tensors if t.numel() > 0]
+        if tensors:
+            with torch.no_grad():
+                C.broadcast_coalesced(self.process_group.comm, tensors, self.broadcast_bucket_size, src)
+
+    # ----------------------------------------------------------------------------- forward
+    def _pre_forward(self, *inputs, **kwargs):
+        if torch.is_grad_enabled() and self.require_backward_grad_sync:
+            self.reducer.prepare_for_forward()
+        work = Join.notify_join_context(self)
+        if work is not None and not self._divide_by_initial_world_size:
+            work.wait()
+            self.reducer.set_gradient_divide_factor(float(work._ones.item()))
+        if torch.is_grad_enabled() and self.reducer.rebuild_buckets():
+            logger.info("xddp: rebuilt buckets: %s", self.reducer.bucket_sizes_bytes())
+        if self._check_sync_bufs_pre_fwd():
+            self._sync_buffers()
+        if self.device_ids:
+            inputs = _to_device(inputs, self.device_ids[0])
+            kwargs = _to_device(kwargs, self.device_ids[0])
+        return inputs, kwargs
+
+    def _post_forward(self, output):
+        if torch.is_grad_enabled() and self.require_backward_grad_sync:
+            self.require_forward_param_sync = True
+            outs = _find_tensors(output) if (self.find_unused_parameters and not self.static_graph) else []
+            self.reducer.prepare_for_backward(outs)
+        else:
+            self.require_forward_param_sync = False
+        return output
+
+    def forward(self, *inputs, **kwargs):
+        with record_function("DistributedDataParallel.forward"):
+            inputs, kwargs = self._pre_forward(*inputs, **kwargs)
+            output = self.module(*inputs, **kwargs)
+            return self._post_forward(output)
+
+    # ----------------------------------------------------------------------------- buffers
+    def will_sync_module_buffers(self) -> bool:
+        return self.require_forward_param_sync and self.broadcast_buffers and len(self._buffers_list) > 0
+
+    def _check_sync_bufs_pre_fwd(self) -> bool:
+        return self.will_sync_module_buffers()
+
+    def _find_common_rank(self, input_rank: int, rank_cond: bool) -> int:
+        t = torch.tensor([input_rank if rank_cond else -1], device=self._comm_device)
+        self.process_group.allreduce(t, xdist.ReduceOp.MAX).wait()
+        r = int(t.item())
+        if r == -1:
+            raise ValueError("BUG! Expected rank_cond to be true for at least one process.")
+        return r
+
+    def _sync_buffers(self, src: int = 0):
+        with torch.no_grad():
+            if self._join_config.enable:
+                src = self._find_common_rank(self.process_group.rank(), True)
+            C = load()
+            bufs = [b for b in self._buffers_list if b.numel() > 0]
+            if bufs:
+                C.broadcast_coalesced(self.process_group.comm, bufs, self.broadcast_bucket_size, src)
+
+    def _check_and_sync_module_buffers(self):
+        if self.will_sync_module_buffers():
+            src = self._find_common_rank(self.process_group.rank(), False)
+            C = load()
+            bufs = [b for b in self._buffers_list if b.numel() > 0]
+            if bufs:
+                C.broadcast_coalesced(self.process_group.comm, bufs, self.broadcast_bucket_size, src)
+
+    def _sync_final_model(self, is_last_joiner: bool):
+        src = self._find_common_rank(self.process_group.rank(), is_last_joiner)
+        self._sync_module_states(src=src)
+
+    # ----------------------------------------------------------------------------- no_sync / join
+    @contextmanager
+    def no_sync(self):
+        """Accumulate grads locally; the first backward after the context reduces them."""
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+
+    def join(self, divide_by_initial_world_size: bool = True, enable: bool = True,
+             throw_on_early_termination: bool = False):
+        return Join([self], enable, throw_on_early_termination,
+                    divide_by_initial_world_size=divide_by_initial_world_size)
+
+    def join_hook(self, **kwargs):
+        return _DDPJoinHook(self, kwargs.get("divide_by_initial_world_size", True))
+
+    @property
+    def join_device(self):
+        return self._comm_device
+
+    @property
+    def join_process_group(self):
+        return self.process_group
+
+    # ----------------------------------------------------------------------------- hooks
+    def register_comm_hook(self, state: object, hook: Callable):
+        """Register ``hook(state, bucket) -> Future[Tensor]`` (reference: ``:1953-2032``)."""
+        if not callable(hook):
+            raise TypeError("comm hook must be callable")
+        self._comm_hooks.append((state, hook))
+        self.reducer.register_comm_hook(state, hook)
+
+    def _register_builtin_comm_hook(self, comm_hook_type):
+        """Native builtin hooks: ALLREDUCE (default) or FP16/BF16 compression (fused casts)."""
+        if comm_hook_type in (BuiltinCommHookType.FP16_COMPRESS, "FP16_COMPRESS"):
+            self.reducer.set_comm_dtype("float16")
+        elif comm_hook_type in (BuiltinCommHookType.BF16_COMPRESS, "BF16_COMPRESS"):
+            self.reducer.set_comm_dtype("bfloat16")
+        elif comm_hook_type in (BuiltinCommHookType.ALLREDUCE, "ALLREDUCE"):
+            pass
+        else:
+            raise ValueError(f"unknown builtin comm hook {comm_hook_type}")
+
+    def _register_fused_optim(self, optim_cls, *args, optim_params=None, **kwargs):
+        from .comm_hooks.optimizer_overlap_hooks import _OptimizerHookState, _hook_then_optimizer
+        from .comm_hooks.default_hooks import allreduce_hook
+
+        state = _OptimizerHookState(optim_cls, self._module_parameters if optim_params is None else optim_params,
+                                    *args, **kwargs)
+        self.register_comm_hook(self.process_group, _hook_then_optimizer(allreduce_hook, state))
+
+    # ----------------------------------------------------------------------------- misc
+    def _set_static_graph(self):
+        if self.static_graph:
+            return
+        self.static_graph = True
+        self.reducer.set_static_graph()
+
+    def _get_ddp_logging_data(self) -> dict:
+        d = dict(self.reducer.construction_data())
+        for k, v in self.reducer.runtime_stats().items():
+            d[k] = int(v) if float(v).is_integer() else v
+        d["module_name"] = type(self.module).__name__
+        d["device_ids"] = "" if not self.device_ids else ", ".join(str(x.index) for x in self.device_ids)
+        d["broadcast_buffers"] = int(self.broadcast_buffers)
+        d["is_multi_device_module"] = 0
+        d["num_parameter_tensors"] = len(self._module_parameters)
+        d["total_parameter_size_bytes"] = sum(p.numel() * p.element_size() for p in self._module_parameters)
+        d["dtypes"] = ", ".join(sorted({str(p.dtype).replace("torch.", "") for p in self._module_parameters}))
+        d["comm_hook"] = "" if not self._comm_hooks else getattr(self._comm_hooks[0][1], "__qualname__", "hook")
+        return d
+
+    def _set_ddp_runtime_logging_sample_rate(self, sample_rate: int):
+        if sample_rate < 1:
+            raise ValueError("DDP runtime logging sample rate should be equal or greater than 1")
+        self.reducer.set_runtime_logging_sample_rate(sample_rate)
+
+    def _get_ddp_bucket_indices(self):
+        return self.reducer.bucket_indices()
+
+    def _remove_autograd_hooks(self):
+        self.reducer.remove_autograd_hooks()
+
+    def _check_reducer_finalized(self):
+        self.reducer.check_finalized()
+
+    def _update_process_group(self, new_process_group):
+        """Continue training on a new (shrunk/expanded) group without rebuilding the wrapper."""
+        self.process_group = new_process_group
+        self.reducer.set_comm(new_process_group.comm)
+
+    def __getstate__(self):
+        self._check_default_group()
+        attrs = copy.copy(self.__dict__)
+        del attrs["process_group"]
+        del attrs["reducer"]
+        attrs["_comm_hooks"] = []
+        return attrs
+
+    def __setstate__(self, state):
+        self.process_group = xdist.get_default_group()
+        super().__setstate__(state)
+        self.__dict__.setdefault("require_forward_param_sync", True)
+        self.__dict__.setdefault("require_backward_grad_sync", True)
+        self._build_reducer()
+        if self.static_graph:
+            self.static_graph = False
+            self._set_static_graph()
+
+    def _check_default_group(self):
+        if self.process_group is not xdist.get_default_group():
+            raise RuntimeError("DDP pickling/unpickling are only supported when using DDP with the default process "
+                               "group.")
+
+
+DDP = DistributedDataParallel

@@ -1,0 +1,24 @@
+"""Multi-process test harness (MultiProcessTestCase analogue): run a module-level
+function in W spawned ranks on the CPU backend and surface the first failure."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _entry(rank, fn, world, backend, args):
+    sys.path.insert(0, REPO)
+    from distributeddataparallel_amd import distributed as xdist
+
+    xdist.init_process_group(backend, rank=rank, world_size=world)
+    try:
+        fn(rank, world, *args)
+    finally:
+        xdist.destroy_process_group()
+
+
+def run_ranks(fn, world=2, backend="cpu", args=()):
+    from distributeddataparallel_amd.utils.spawn import free_port, spawn
+
+    env = {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port()), "OMP_NUM_THREADS": "1"}
+    spawn(_entry, args=(fn, world, backend, args), nprocs=world, env=env)
