@@ -77,6 +77,9 @@ def main():
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched via torch.distributed.run (one rank per GPU)")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("RANK", str(rank))
+    os.environ.setdefault("WORLD_SIZE", str(world))
+    os.environ.setdefault("LOCAL_RANK", str(local_rank))
     if "MASTER_PORT" not in os.environ:
         from distributeddataparallel_amd.utils.spawn import free_port
 
@@ -103,13 +106,13 @@ def main():
         ddp = xddp.DDP(model, device_ids=[local_rank], bucket_cap_mb=args.bucket_cap_mb,
                        gradient_as_bucket_view=bool(args.grad_as_bucket_view), comm_dtype=comm_dtype)
         opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, master_weights=True)
-        zero_kw = dict(set_to_none=not args.grad_as_bucket_view)
+        zero_kw = dict(set_to_none=True)
     else:
         ddp = torch.nn.parallel.DistributedDataParallel(
             model, device_ids=[local_rank], bucket_cap_mb=args.bucket_cap_mb or 25,
             gradient_as_bucket_view=bool(args.grad_as_bucket_view))
         opt = torch.optim.SGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
-        zero_kw = dict(set_to_none=not args.grad_as_bucket_view)
+        zero_kw = dict(set_to_none=True)
 
     B, S = args.batch_size, args.image_size
     mf = torch.channels_last if args.channels_last else torch.contiguous_format

@@ -164,6 +164,7 @@ class RcclComm : public Comm {
 
   std::shared_ptr<Work> allreduce(at::Tensor t, RedOp op, double premul) override {
     check_tensor(t);
+    if (size_ == 1 && op != RedOp::PREMUL_SUM) return local_noop("allreduce", t);  // identity on one rank
     return launch("allreduce", t, {t}, [&](hipStream_t s) {
       if (op == RedOp::PREMUL_SUM) {
         TORCH_CHECK(at::isFloatingType(t.scalar_type()), "PREMUL_SUM needs a floating-point tensor");
@@ -187,6 +188,7 @@ class RcclComm : public Comm {
 
   std::shared_ptr<Work> broadcast(at::Tensor t, int root) override {
     check_tensor(t);
+    if (size_ == 1) return local_noop("broadcast", t);
     return launch("broadcast", t, {t}, [&](hipStream_t s) {
       XDDP_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, s));
     });
@@ -239,7 +241,9 @@ class RcclComm : public Comm {
     c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
     if (!barrier_buf_.defined())
       barrier_buf_ = at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, device_));
-    auto w = allreduce(barrier_buf_, RedOp::SUM, 1.0);
+    auto w = launch("barrier", barrier_buf_, {barrier_buf_}, [&](hipStream_t s) {
+      XDDP_NCCL_CHECK(ncclAllReduce(barrier_buf_.data_ptr(), barrier_buf_.data_ptr(), 1, ncclInt32, ncclSum, comm_, s));
+    });
     w->synchronize();
     return w;
   }
@@ -309,6 +313,17 @@ class RcclComm : public Comm {
     w->outputs = std::move(keep);
     if (in_group_ > 0) group_works_.push_back(w);
     else finish_launch(w);
+    return w;
+  }
+
+  // One-rank collectives that are identities: no RCCL launch, a Work that is already ordered.
+  std::shared_ptr<Work> local_noop(const char* name, const at::Tensor& t) {
+    TORCH_CHECK(err_->load() == 0, "xddp rccl: communicator is in error state");
+    auto w = std::make_shared<RcclWork>(pool_, device_, err_);
+    w->seq = flight_.record(name, t.numel(), t.scalar_type());
+    XDDP_HIP_CHECK(hipEventRecord(w->ev, c10::hip::getCurrentHIPStream(device_).stream()));
+    flight_.finish(w->seq, "completed");
+    w->outputs = {t};
     return w;
   }
 

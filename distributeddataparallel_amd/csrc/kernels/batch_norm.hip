@@ -1,0 +1,462 @@
+// BatchNorm for channels_last (NHWC) activations on gfx950, with fused epilogues.
+//
+// Reference hot path (SURVEY.md §2.6 K3–K6): per BN layer the eager stack runs
+// native_batch_norm (MIOpen) + num_batches_tracked.add_ + relu_ (+ residual add) forward and
+// batch_norm_backward + threshold_backward (+ add) backward: 4–6 full passes over the
+// activation. Here:
+//   forward : stats pass (read x) → tiny per-channel finalize (mean, invstd, running-stat EMA,
+//             num_batches_tracked += 1, scale/shift) → apply pass (read x [+res], write y)
+//             with BN·γ+β, + residual, ReLU fused;
+//   backward: reduce pass (read dy, x, y) → finalize (dγ, dβ and the three dx coefficients)
+//             → elementwise pass writing dx (and d(residual) when the add was fused).
+// Layout: rows = N·H·W, each row has C contiguous channels. A lane owns 8 consecutive
+// channels (16-byte bf16 loads); the block tiles TX lanes across channels × TY lanes down rows.
+// Per-thread partial sums are converted to (n, mean, M2) and merged with Chan's formula
+// (in LDS, then across row-blocks) so large N·H·W does not cancel catastrophically.
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include "common.h"
+#include "kernels/dev_utils.h"
+
+namespace xddp {
+namespace kernels {
+
+using dev::bf16_t;
+using dev::f16_t;
+using dev::Elem;
+using dev::Vec8;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+struct Geo {
+  int tx, ty;       // lanes across channel-vectors, lanes down rows
+  int cblocks;      // grid.x
+  int rblocks;      // grid.y
+  int64_t rows_per; // rows per row-block
+};
+
+Geo make_geo(int64_t M, int C) {
+  Geo g;
+  const int cvec = C / 8;
+  g.tx = std::min(cvec, 32);
+  while (cvec % g.tx) g.tx--;  // tx divides the channel-vector count
+  g.ty = kBlock / g.tx;
+  g.cblocks = cvec / g.tx;
+  // aim for ~2048 blocks total, each row-block >= ty rows
+  int64_t want = std::max<int64_t>(1, 2048 / g.cblocks);
+  int64_t maxr = std::max<int64_t>(1, (M + g.ty - 1) / g.ty);
+  g.rblocks = (int)std::min<int64_t>(std::min<int64_t>(want, maxr), 65535);
+  g.rows_per = (M + g.rblocks - 1) / g.rblocks;
+  g.rblocks = (int)((M + g.rows_per - 1) / g.rows_per);
+  return g;
+}
+
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
+  const float nn = n + nb;
+  if (nb == 0.f) return;
+  if (n == 0.f) {
+    n = nb; mean = meanb; m2 = m2b;
+    return;
+  }
+  const float d = meanb - mean;
+  const float f = nb / nn;
+  mean += d * f;
+  m2 += m2b + d * d * n * f;
+  n = nn;
+}
+
+// ---------------------------------------------------------------- forward stats
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ x, int64_t M, int C, int64_t rows_per,
+                                                          float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
+  const int c0 = (blockIdx.x * TX + tx) * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per;
+  const int64_t r1 = min(M, r0 + rows_per);
+  float s[8] = {0}, ss[8] = {0};
+  int cnt = 0;
+  for (int64_t r = r0 + ty; r < r1; r += TY) {
+    float v[8];
+    Vec8<T>::ld(x + r * C + c0, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] += v[j];
+      ss[j] = fmaf(v[j], v[j], ss[j]);
+    }
+    cnt++;
+  }
+  // thread partials -> (n, mean, m2) in LDS: layout [ty][tx][8][3]
+  float* my = lds + ((ty * TX + tx) * 8) * 3;
+  const float n = (float)cnt;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float mean = cnt ? s[j] / n : 0.f;
+    my[j * 3 + 0] = n;
+    my[j * 3 + 1] = mean;
+    my[j * 3 + 2] = cnt ? fmaxf(ss[j] - s[j] * mean, 0.f) : 0.f;
+  }
+  __syncthreads();
+  // tree-merge across ty
+  for (int stride = TY / 2; stride > 0; stride >>= 1) {
+    if (ty < stride) {
+      float* o = lds + (((ty + stride) * TX + tx) * 8) * 3;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) chan_merge(my[j * 3], my[j * 3 + 1], my[j * 3 + 2], o[j * 3], o[j * 3 + 1], o[j * 3 + 2]);
+    }
+    __syncthreads();
+  }
+  if (ty == 0) {
+    float* dst = part + ((int64_t)blockIdx.y * C + c0) * 3;
+#pragma unroll
+    for (int j = 0; j < 24; ++j) dst[j] = my[j];
+  }
+}
+
+// One thread per channel: merge row-block partials; EMA running stats; scale/shift.
+template <typename W>
+__global__ __launch_bounds__(kBlock) void bn_stats_finalize_kernel(
+    const float* __restrict__ part, int rblocks, int C, int64_t M, const W* __restrict__ weight,
+    const W* __restrict__ bias, W* running_mean, W* running_var, const int64_t* nbt, float momentum, bool cma,
+    float eps,
+    float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int b = 0; b < rblocks; ++b) {
+    const float* p = part + ((int64_t)b * C + c) * 3;
+    chan_merge(n, mean, m2, p[0], p[1], p[2]);
+  }
+  const float var = m2 / fmaxf(n, 1.f);
+  const float inv = rsqrtf(var + eps);
+  mean_out[c] = mean;
+  invstd_out[c] = inv;
+  const float g = weight ? Elem<W, float>::ld(weight, c) : 1.f;
+  const float bb = bias ? Elem<W, float>::ld(bias, c) : 0.f;
+  scale[c] = g * inv;
+  shift[c] = bb - mean * g * inv;
+  if (running_mean) {
+    float mom = momentum;
+    if (cma && nbt) mom = 1.f / (float)(nbt[0] + 1);  // nbt is incremented later, by the apply kernel
+    const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
+    Elem<W, float>::st(running_mean, c, (1.f - mom) * Elem<W, float>::ld(running_mean, c) + mom * mean);
+    Elem<W, float>::st(running_var, c, (1.f - mom) * Elem<W, float>::ld(running_var, c) + mom * unbiased);
+  }
+}
+
+// eval mode: scale/shift from running stats
+template <typename W>
+__global__ void bn_eval_coef_kernel(int C, const W* weight, const W* bias, const W* rm, const W* rv, float eps,
+                                    float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = rsqrtf(Elem<W, float>::ld(rv, c) + eps);
+  const float g = weight ? Elem<W, float>::ld(weight, c) : 1.f;
+  const float b = bias ? Elem<W, float>::ld(bias, c) : 0.f;
+  scale[c] = g * inv;
+  shift[c] = b - Elem<W, float>::ld(rm, c) * g * inv;
+}
+
+// ---------------------------------------------------------------- apply
+template <typename T, bool RES, bool RELU>
+__global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                          T* __restrict__ y, int64_t nvec, int C,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, int64_t* nbt_inc) {
+  if (nbt_inc && blockIdx.x == 0 && threadIdx.x == 0) nbt_inc[0] += 1;  // num_batches_tracked.add_(1), fused
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int64_t e = v * 8;
+    const int c0 = (int)(e % C);
+    float a[8], r[8];
+    Vec8<T>::ld(x + e, a);
+    if (RES) Vec8<T>::ld(res + e, r);
+    const dev::f32x4 s0 = *reinterpret_cast<const dev::f32x4*>(scale + c0);
+    const dev::f32x4 s1 = *reinterpret_cast<const dev::f32x4*>(scale + c0 + 4);
+    const dev::f32x4 h0 = *reinterpret_cast<const dev::f32x4*>(shift + c0);
+    const dev::f32x4 h1 = *reinterpret_cast<const dev::f32x4*>(shift + c0 + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float o = fmaf(a[j], sc[j], sh[j]);
+      if (RES) o += r[j];
+      if (RELU) o = fmaxf(o, 0.f);
+      a[j] = o;
+    }
+    Vec8<T>::st(y + e, a);
+  }
+}
+
+// ---------------------------------------------------------------- backward reduce
+// part layout [rblocks][C][2] = (sum dy_eff, sum dy_eff*(x-mean))
+template <typename T, bool RELU>
+__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                               const T* __restrict__ y, int64_t M, int C,
+                                                               int64_t rows_per, const float* __restrict__ mean,
+                                                               float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
+  const int c0 = (blockIdx.x * TX + tx) * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per;
+  const int64_t r1 = min(M, r0 + rows_per);
+  float mu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) mu[j] = mean[c0 + j];
+  float sd[8] = {0}, sdx[8] = {0};
+  for (int64_t r = r0 + ty; r < r1; r += TY) {
+    float g[8], a[8];
+    Vec8<T>::ld(dy + r * C + c0, g);
+    Vec8<T>::ld(x + r * C + c0, a);
+    if (RELU) {
+      float o[8];
+      Vec8<T>::ld(y + r * C + c0, o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = o[j] > 0.f ? g[j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sd[j] += g[j];
+      sdx[j] = fmaf(g[j], a[j] - mu[j], sdx[j]);
+    }
+  }
+  float* my = lds + ((ty * TX + tx) * 8) * 2;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    my[j * 2] = sd[j];
+    my[j * 2 + 1] = sdx[j];
+  }
+  __syncthreads();
+  for (int stride = TY / 2; stride > 0; stride >>= 1) {
+    if (ty < stride) {
+      const float* o = lds + (((ty + stride) * TX + tx) * 8) * 2;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) my[j] += o[j];
+    }
+    __syncthreads();
+  }
+  if (ty == 0) {
+    float* dst = part + ((int64_t)blockIdx.y * C + c0) * 2;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dst[j] = my[j];
+  }
+}
+
+// per channel: dgamma, dbeta; dx = k1*dy_eff + k2*(x-mean) + k3
+template <typename W>
+__global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __restrict__ part, int rblocks, int C,
+                                                                 int64_t M, const W* __restrict__ weight,
+                                                                 const float* __restrict__ invstd, W* dweight,
+                                                                 W* dbias, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float sd = 0.f, sdx = 0.f;
+  for (int b = 0; b < rblocks; ++b) {
+    const float* p = part + ((int64_t)b * C + c) * 2;
+    sd += p[0];
+    sdx += p[1];
+  }
+  const float inv = invstd[c];
+  const float g = weight ? Elem<W, float>::ld(weight, c) : 1.f;
+  if (dweight) Elem<W, float>::st(dweight, c, sdx * inv);
+  if (dbias) Elem<W, float>::st(dbias, c, sd);
+  const float invM = 1.f / (float)M;
+  coef[c] = g * inv;                                   // k1
+  coef[C + c] = -g * inv * inv * inv * sdx * invM;     // k2
+  coef[2 * C + c] = -g * inv * sd * invM;              // k3
+}
+
+template <typename T, bool RELU, bool DRES>
+__global__ __launch_bounds__(kBlock) void bn_bwd_elem_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                             const T* __restrict__ y, T* __restrict__ dx,
+                                                             T* __restrict__ dres, int64_t nvec, int C,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ coef) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int64_t e = v * 8;
+    const int c0 = (int)(e % C);
+    float g[8], a[8];
+    Vec8<T>::ld(dy + e, g);
+    Vec8<T>::ld(x + e, a);
+    if (RELU) {
+      float o[8];
+      Vec8<T>::ld(y + e, o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = o[j] > 0.f ? g[j] : 0.f;
+    }
+    if (DRES) Vec8<T>::st(dres + e, g);
+    float out[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      out[j] = fmaf(coef[c], g[j], fmaf(coef[C + c], a[j] - mean[c], coef[2 * C + c]));
+    }
+    Vec8<T>::st(dx + e, out);
+  }
+}
+
+template <typename F>
+void dispatch_act(at::ScalarType st, F&& f) {
+  switch (st) {
+    case at::kBFloat16: f(bf16_t{}); break;
+    case at::kFloat: f(float{}); break;
+    case at::kHalf: f(f16_t{}); break;
+    default: TORCH_CHECK(false, "xddp batch_norm: unsupported activation dtype ", st);
+  }
+}
+
+template <typename F>
+void dispatch_w(at::ScalarType st, F&& f) {
+  switch (st) {
+    case at::kBFloat16: f(bf16_t{}); break;
+    case at::kFloat: f(float{}); break;
+    case at::kHalf: f(f16_t{}); break;
+    default: TORCH_CHECK(false, "xddp batch_norm: unsupported weight dtype ", st);
+  }
+}
+
+int elem_grid(int64_t nvec) { return (int)std::min<int64_t>((nvec + kBlock - 1) / kBlock, 256 * 16); }
+
+void check_nhwc(const at::Tensor& x) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4, "xddp batch_norm expects a 4-D device tensor");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "xddp batch_norm expects channels_last input");
+  TORCH_CHECK(x.size(1) % 8 == 0, "xddp batch_norm needs C % 8 == 0");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0, "xddp batch_norm needs 16-B aligned data");
+}
+
+template <typename W>
+W* opt_ptr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<W*>(t->data_ptr()) : nullptr;
+}
+
+}  // namespace
+
+// returns (y, mean, invstd)
+std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& weight,
+                                   const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& running_mean,
+                                   const c10::optional<at::Tensor>& running_var,
+                                   const c10::optional<at::Tensor>& num_batches_tracked, bool training,
+                                   double momentum, bool cumulative, double eps,
+                                   const c10::optional<at::Tensor>& residual, bool relu) {
+  check_nhwc(x);
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), Wd = x.size(3);
+  const int64_t M = N * H * Wd;
+  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  auto fopt = x.options().dtype(at::kFloat);
+  auto y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  auto ss = at::empty({2, C}, fopt);
+  const bool has_res = residual.has_value() && residual->defined();
+  if (has_res) {
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->scalar_type() == x.scalar_type() &&
+                    residual->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "fused residual must match x (shape, dtype, channels_last)");
+  }
+  const auto wdt = weight.has_value() && weight->defined() ? weight->scalar_type()
+                   : (running_mean.has_value() && running_mean->defined() ? running_mean->scalar_type() : at::kFloat);
+  dispatch_act(x.scalar_type(), [&](auto tag_t) {
+    using T = decltype(tag_t);
+    dispatch_w(wdt, [&](auto tag_w) {
+      using W = decltype(tag_w);
+      const int fin_grid = (int)((C + kBlock - 1) / kBlock);
+      if (training) {
+        TORCH_CHECK(M > 0, "batch_norm on empty input");
+        Geo g = make_geo(M, (int)C);
+        auto part = at::empty({(int64_t)g.rblocks, C, 3}, fopt);
+        const size_t lds = (size_t)kBlock * 8 * 3 * sizeof(float);
+        hipLaunchKernelGGL((bn_stats_kernel<T>), dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds, stream,
+                           reinterpret_cast<const T*>(x.data_ptr()), M, (int)C, g.rows_per, part.data_ptr<float>());
+        XDDP_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL((bn_stats_finalize_kernel<W>), dim3(fin_grid), dim3(kBlock), 0, stream,
+                           part.data_ptr<float>(), g.rblocks, (int)C, M, opt_ptr<const W>(weight),
+                           opt_ptr<const W>(bias), opt_ptr<W>(running_mean), opt_ptr<W>(running_var),
+                           (num_batches_tracked.has_value() && num_batches_tracked->defined())
+                               ? num_batches_tracked->data_ptr<int64_t>() : nullptr,
+                           (float)momentum, cumulative, (float)eps, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                           ss.data_ptr<float>(), ss.data_ptr<float>() + C);
+        XDDP_HIP_CHECK(hipGetLastError());
+      } else {
+        TORCH_CHECK(running_mean.has_value() && running_var.has_value(), "eval batch_norm needs running stats");
+        hipLaunchKernelGGL((bn_eval_coef_kernel<W>), dim3(fin_grid), dim3(kBlock), 0, stream, (int)C,
+                           opt_ptr<const W>(weight), opt_ptr<const W>(bias), opt_ptr<const W>(running_mean),
+                           opt_ptr<const W>(running_var), (float)eps, ss.data_ptr<float>(), ss.data_ptr<float>() + C);
+        XDDP_HIP_CHECK(hipGetLastError());
+      }
+      const int64_t nvec = M * C / 8;
+      const T* res = has_res ? reinterpret_cast<const T*>(residual->data_ptr()) : nullptr;
+      int64_t* nbt_inc = (training && num_batches_tracked.has_value() && num_batches_tracked->defined())
+                             ? num_batches_tracked->data_ptr<int64_t>() : nullptr;
+      auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
+                           reinterpret_cast<const T*>(x.data_ptr()), res, reinterpret_cast<T*>(y.data_ptr()), nvec,
+                           (int)C, ss.data_ptr<float>(), ss.data_ptr<float>() + C, nbt_inc);
+      };
+      if (has_res) { if (relu) launch(bn_apply_kernel<T, true, true>); else launch(bn_apply_kernel<T, true, false>); }
+      else { if (relu) launch(bn_apply_kernel<T, false, true>); else launch(bn_apply_kernel<T, false, false>); }
+      XDDP_HIP_CHECK(hipGetLastError());
+    });
+  });
+  return {y, mean, invstd};
+}
+
+// returns (dx, dweight, dbias, dresidual)
+std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x, const c10::optional<at::Tensor>& y,
+                                    const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
+                                    const at::Tensor& invstd, bool relu, bool need_dres, bool need_dweight) {
+  check_nhwc(x);
+  auto dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "dy must match x");
+  if (relu) TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the forward output");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), Wd = x.size(3);
+  const int64_t M = N * H * Wd;
+  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  auto fopt = x.options().dtype(at::kFloat);
+  auto dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  at::Tensor dres = need_dres ? at::empty_like(x, at::MemoryFormat::ChannelsLast) : at::Tensor();
+  const bool has_w = weight.has_value() && weight->defined();
+  const auto wdt = has_w ? weight->scalar_type() : at::kFloat;
+  at::Tensor dw = (has_w && need_dweight) ? at::empty({C}, weight->options()) : at::Tensor();
+  at::Tensor db = (has_w && need_dweight) ? at::empty({C}, weight->options()) : at::Tensor();
+  auto coef = at::empty({3, C}, fopt);
+  Geo g = make_geo(M, (int)C);
+  auto part = at::empty({(int64_t)g.rblocks, C, 2}, fopt);
+  dispatch_act(x.scalar_type(), [&](auto tag_t) {
+    using T = decltype(tag_t);
+    dispatch_w(wdt, [&](auto tag_w) {
+      using W = decltype(tag_w);
+      const T* yp = relu ? reinterpret_cast<const T*>(y->data_ptr()) : nullptr;
+      const size_t lds = (size_t)kBlock * 8 * 2 * sizeof(float);
+      auto red = relu ? bn_bwd_reduce_kernel<T, true> : bn_bwd_reduce_kernel<T, false>;
+      hipLaunchKernelGGL(red, dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds, stream,
+                         reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(x.data_ptr()), yp, M,
+                         (int)C, g.rows_per, mean.data_ptr<float>(), part.data_ptr<float>());
+      XDDP_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
+                         part.data_ptr<float>(), g.rblocks, (int)C, M,
+                         has_w ? reinterpret_cast<const W*>(weight->data_ptr()) : nullptr, invstd.data_ptr<float>(),
+                         dw.defined() ? reinterpret_cast<W*>(dw.data_ptr()) : nullptr,
+                         db.defined() ? reinterpret_cast<W*>(db.data_ptr()) : nullptr, coef.data_ptr<float>());
+      XDDP_HIP_CHECK(hipGetLastError());
+      const int64_t nvec = M * C / 8;
+      auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
+                           reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(x.data_ptr()), yp,
+                           reinterpret_cast<T*>(dx.data_ptr()),
+                           need_dres ? reinterpret_cast<T*>(dres.data_ptr()) : nullptr, nvec, (int)C,
+                           mean.data_ptr<float>(), coef.data_ptr<float>());
+      };
+      if (relu) { if (need_dres) launch(bn_bwd_elem_kernel<T, true, true>); else launch(bn_bwd_elem_kernel<T, true, false>); }
+      else { if (need_dres) launch(bn_bwd_elem_kernel<T, false, true>); else launch(bn_bwd_elem_kernel<T, false, false>); }
+      XDDP_HIP_CHECK(hipGetLastError());
+    });
+  });
+  return {dx, dw, db, dres};
+}
+
+}  // namespace kernels
+}  // namespace xddp

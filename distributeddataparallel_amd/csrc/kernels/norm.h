@@ -1,10 +1,28 @@
-// Normalization kernels (BatchNorm NHWC, LayerNorm, RMSNorm) for gfx950.
+// Normalization kernels (BatchNorm NHWC with fused residual/ReLU, LayerNorm, RMSNorm) for gfx950.
 #pragma once
 
+#include <ATen/ATen.h>
 #include <pybind11/pybind11.h>
+
+#include <vector>
 
 namespace xddp {
 namespace kernels {
+
+std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& weight,
+                                   const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& running_mean,
+                                   const c10::optional<at::Tensor>& running_var,
+                                   const c10::optional<at::Tensor>& num_batches_tracked, bool training,
+                                   double momentum, bool cumulative, double eps,
+                                   const c10::optional<at::Tensor>& residual, bool relu);
+std::vector<at::Tensor> bn_backward(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& y,
+                                    const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
+                                    const at::Tensor& invstd, bool relu, bool need_dres, bool need_dweight);
+std::vector<at::Tensor> ln_forward(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
+                                   const c10::optional<at::Tensor>& beta, double eps, bool rms);
+std::vector<at::Tensor> ln_backward(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
+                                    const c10::optional<at::Tensor>& mean, const at::Tensor& rstd, bool rms,
+                                    bool need_dgamma, bool need_dbeta);
 
 void bind_norm_kernels(pybind11::module_& m);
 

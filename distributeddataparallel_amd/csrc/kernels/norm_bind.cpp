@@ -1,0 +1,22 @@
+#include <torch/extension.h>
+
+#include "kernels/norm.h"
+
+namespace py = pybind11;
+
+namespace xddp {
+namespace kernels {
+
+void bind_norm_kernels(py::module_& m) {
+  m.def("bn_forward", &bn_forward, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
+        py::arg("running_var"), py::arg("num_batches_tracked"), py::arg("training"), py::arg("momentum"),
+        py::arg("cumulative"), py::arg("eps"), py::arg("residual"), py::arg("relu"));
+  m.def("bn_backward", &bn_backward, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("weight"), py::arg("mean"),
+        py::arg("invstd"), py::arg("relu"), py::arg("need_dres"), py::arg("need_dweight"));
+  m.def("ln_forward", &ln_forward, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("rms"));
+  m.def("ln_backward", &ln_backward, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
+        py::arg("rms"), py::arg("need_dgamma"), py::arg("need_dbeta"));
+}
+
+}  // namespace kernels
+}  // namespace xddp

@@ -1,0 +1,103 @@
+"""Fused BatchNorm2d (+ residual add + ReLU) on xddp's NHWC HIP kernels.
+
+Drop-in for ``nn.BatchNorm2d``: same parameters, buffers and state_dict keys (it *is* a
+``BatchNorm2d`` subclass, so DDP buffer sync, ``convert_sync_batchnorm`` and checkpoints
+see the standard layout). ``forward(x, residual=None, relu=False)`` fuses the
+bottleneck/basic-block epilogue ``relu(bn(x) + residual)`` into one pass forward and one
+backward (SURVEY.md §2.6 K3–K6, K9). Inputs that the kernels do not cover (NCHW layout,
+C % 8 != 0, CPU, eval-mode autograd) take the equivalent PyTorch path.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .._native import load
+
+__all__ = ["FusedBatchNorm2d", "batch_norm_act"]
+
+
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, residual, relu):
+        C = load()
+        y, mean, invstd = C.bn_forward(x, weight, bias, running_mean, running_var, nbt, True, momentum, cma, eps,
+                                       residual, relu)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = load()
+        x, y, weight, mean, invstd = ctx.saved_tensors
+        need_dw = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        dx, dw, db, dres = C.bn_backward(dy, x, y, weight, mean, invstd, ctx.relu,
+                                         ctx.has_res and ctx.needs_input_grad[9], need_dw)
+        return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
+                None, None, None, None, None, None, dres if ctx.has_res else None, None)
+
+
+def _kernel_ok(x: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dim() == 4 and x.size(1) % 8 == 0 and x.numel() > 0
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
+            and x.data_ptr() % 16 == 0)
+
+
+def batch_norm_act(x, running_mean, running_var, weight=None, bias=None, training=True, momentum=0.1, eps=1e-5,
+                   num_batches_tracked=None, residual: Optional[torch.Tensor] = None, relu: bool = False):
+    """Functional fused BN(+add)(+ReLU). ``momentum=None`` means cumulative moving average."""
+    use_kernel = _kernel_ok(x) and (residual is None or (residual.shape == x.shape and residual.dtype == x.dtype and
+                                                         residual.is_contiguous(memory_format=torch.channels_last)))
+    if use_kernel and training:
+        cma = momentum is None
+        return _BNAct.apply(x, weight, bias, running_mean, running_var, num_batches_tracked,
+                            0.0 if cma else float(momentum), cma, float(eps), residual, relu)
+    if use_kernel and not training and not (torch.is_grad_enabled() and (
+            x.requires_grad or (weight is not None and weight.requires_grad))):
+        C = load()
+        y, _, _ = C.bn_forward(x, weight, bias, running_mean, running_var, None, False, 0.0, False, float(eps),
+                               residual, relu)
+        return y
+    # reference path
+    if training and num_batches_tracked is not None:
+        num_batches_tracked.add_(1)
+        if momentum is None:
+            momentum = 1.0 / float(num_batches_tracked)
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum if momentum is not None else 0.0,
+                     eps)
+    if residual is not None:
+        y = y + residual
+    if relu:
+        y = F.relu(y)
+    return y
+
+
+class FusedBatchNorm2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` with an NHWC HIP kernel and optional fused residual-add + ReLU."""
+
+    supports_add_relu = True
+    fuses_relu = True
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True, device=None,
+                 dtype=None):
+        super().__init__(num_features, eps, momentum, affine, track_running_stats, device, dtype)
+        self.relu = False
+
+    def forward(self, x, residual: Optional[torch.Tensor] = None, relu: Optional[bool] = None):
+        self._check_input_dim(x)
+        relu = self.relu if relu is None else relu
+        training = self.training or not self.track_running_stats
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        nbt = self.num_batches_tracked if (self.training and self.track_running_stats) else None
+        return batch_norm_act(x, rm, rv, self.weight, self.bias, training, self.momentum, self.eps, nbt, residual,
+                              relu)
+
+    def extra_repr(self):
+        return super().extra_repr() + (", relu=True" if self.relu else "")

@@ -66,19 +66,21 @@ def test_ddp_matches_local_training(pg, grad_as_view, comm_dtype):
     assert d["has_rebuilt_buckets"] == "1"
 
 
-def test_ddp_bf16_channels_last_fused_sgd(pg):
+@pytest.mark.parametrize("fused_bn", [False, True])
+def test_ddp_bf16_channels_last_fused_sgd(pg, fused_bn):
     from distributeddataparallel_amd.models import resnet50
+    from distributeddataparallel_amd.ops import FusedBatchNorm2d
     from distributeddataparallel_amd.optim import FusedSGD
 
     torch.manual_seed(0)
-    m = resnet50().cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+    m = resnet50(norm_layer=FusedBatchNorm2d if fused_bn else None).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
     ddp = xddp.DDP(m, device_ids=[0], gradient_as_bucket_view=True)
     opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, master_weights=True)
     x = torch.randn(8, 3, 64, 64, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (8,), device="cuda")
     losses = []
     for _ in range(3):
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad(set_to_none=True)
         loss = F.cross_entropy(ddp(x).float(), y)
         loss.backward()
         opt.step()
@@ -87,3 +89,23 @@ def test_ddp_bf16_channels_last_fused_sgd(pg):
     # grads alias bucket memory
     p0 = next(m.parameters())
     assert p0.grad is not None and p0.grad.data_ptr() != 0
+
+
+def test_resnet50_fused_bn_matches_torch_bn(pg):
+    """Same weights, same batch: fused-BN ResNet-50 forward/backward ≈ nn.BatchNorm2d ResNet-50 (fp32)."""
+    from distributeddataparallel_amd.models import resnet50
+    from distributeddataparallel_amd.ops import FusedBatchNorm2d
+
+    torch.manual_seed(0)
+    a = resnet50(norm_layer=FusedBatchNorm2d).cuda().to(memory_format=torch.channels_last)
+    b = resnet50().cuda().to(memory_format=torch.channels_last)
+    b.load_state_dict(a.state_dict())
+    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (4,), device="cuda")
+    la = F.cross_entropy(a(x), y)
+    lb = F.cross_entropy(b(x), y)
+    torch.testing.assert_close(la, lb, rtol=1e-3, atol=1e-3)
+    la.backward()
+    lb.backward()
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(p.grad, q.grad, rtol=2e-2, atol=2e-3, msg=n)

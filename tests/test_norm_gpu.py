@@ -1,0 +1,125 @@
+"""Fused BatchNorm(+add+ReLU) / LayerNorm / RMSNorm HIP kernels vs PyTorch fp32 references."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributeddataparallel_amd.ops import FusedBatchNorm2d, FusedLayerNorm, FusedRMSNorm
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _tol(dt):
+    return dict(rtol=2e-2, atol=2e-2) if dt != torch.float32 else dict(rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 256, 7, 7), (2, 32, 3, 5), (16, 2048, 1, 1)])
+@pytest.mark.parametrize("res,relu", [(False, False), (False, True), (True, True)])
+def test_batchnorm_train_fwd_bwd(dt, shape, res, relu):
+    torch.manual_seed(0)
+    C = shape[1]
+    bn = FusedBatchNorm2d(C).to(DEV, dt)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    ref = torch.nn.BatchNorm2d(C).to(DEV)  # fp32 reference
+    ref.load_state_dict({k: v.float() for k, v in bn.state_dict().items()})
+    x = (torch.randn(shape, device=DEV) * 2 + 0.5).to(dt).contiguous(memory_format=torch.channels_last)
+    r = torch.randn(shape, device=DEV).to(dt).contiguous(memory_format=torch.channels_last) if res else None
+    x1 = x.clone().requires_grad_()
+    r1 = r.clone().requires_grad_() if res else None
+    y = bn(x1, residual=r1, relu=relu)
+    x2 = x.float().clone().requires_grad_()
+    r2 = r.float().clone().requires_grad_() if res else None
+    y2 = ref(x2)
+    if res:
+        y2 = y2 + r2
+    if relu:
+        y2 = F.relu(y2)
+    torch.testing.assert_close(y.float(), y2, **_tol(dt))
+    torch.testing.assert_close(bn.running_mean.float(), ref.running_mean, **_tol(dt))
+    torch.testing.assert_close(bn.running_var.float(), ref.running_var, **_tol(dt))
+    assert int(bn.num_batches_tracked) == 1
+    g = torch.randn(shape, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    y.backward(g)
+    y2.backward(g.float())
+    torch.testing.assert_close(x1.grad.float(), x2.grad, **_tol(dt))
+    torch.testing.assert_close(bn.weight.grad.float(), ref.weight.grad, rtol=3e-2, atol=3e-2 * shape[0] ** 0.5)
+    torch.testing.assert_close(bn.bias.grad.float(), ref.bias.grad, rtol=3e-2, atol=3e-2 * shape[0] ** 0.5)
+    if res:
+        torch.testing.assert_close(r1.grad.float(), r2.grad, **_tol(dt))
+
+
+def test_batchnorm_eval_and_cma():
+    torch.manual_seed(0)
+    bn = FusedBatchNorm2d(64, momentum=None).to(DEV)
+    ref = torch.nn.BatchNorm2d(64, momentum=None).to(DEV)
+    for _ in range(3):
+        x = torch.randn(4, 64, 8, 8, device=DEV).contiguous(memory_format=torch.channels_last)
+        bn(x)
+        ref(x)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-5, atol=1e-5)
+    assert int(bn.num_batches_tracked) == 3
+    bn.eval()
+    ref.eval()
+    x = torch.randn(4, 64, 8, 8, device=DEV).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        torch.testing.assert_close(bn(x, relu=True), F.relu(ref(x)), rtol=1e-5, atol=1e-5)
+
+
+def test_batchnorm_large_mean_offset_stable():
+    """Chan-merged stats must not cancel when |mean| >> std over many rows."""
+    bn = FusedBatchNorm2d(16).to(DEV)
+    x = (torch.randn(64, 16, 56, 56, device=DEV) * 0.01 + 100.0).contiguous(memory_format=torch.channels_last)
+    y = bn(x)
+    ref = F.batch_norm(x, None, None, training=True)
+    torch.testing.assert_close(y, ref, rtol=1e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(4, 7, 1024), (3, 4096), (5, 40), (2, 3, 8192)])
+def test_layernorm(dt, shape):
+    torch.manual_seed(0)
+    D = shape[-1]
+    ln = FusedLayerNorm(D).to(DEV, dt)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.5, 0.5)
+    x = (torch.randn(shape, device=DEV) * 3 + 1).to(dt)
+    x1 = x.clone().requires_grad_()
+    y = ln(x1)
+    w = ln.weight.detach().float().requires_grad_()
+    b = ln.bias.detach().float().requires_grad_()
+    x2 = x.float().requires_grad_()
+    y2 = F.layer_norm(x2, (D,), w, b, 1e-5)
+    torch.testing.assert_close(y.float(), y2, **_tol(dt))
+    g = torch.randn(shape, device=DEV).to(dt)
+    y.backward(g)
+    y2.backward(g.float())
+    torch.testing.assert_close(x1.grad.float(), x2.grad, **_tol(dt))
+    rows = x.numel() // D
+    torch.testing.assert_close(ln.weight.grad.float(), w.grad, rtol=3e-2, atol=3e-2 * rows ** 0.5)
+    torch.testing.assert_close(ln.bias.grad.float(), b.grad, rtol=3e-2, atol=3e-2 * rows ** 0.5)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_rmsnorm(dt):
+    torch.manual_seed(0)
+    D = 4096
+    rn = FusedRMSNorm(D).to(DEV, dt)
+    with torch.no_grad():
+        rn.weight.uniform_(0.5, 1.5)
+    x = torch.randn(6, 5, D, device=DEV).to(dt)
+    x1 = x.clone().requires_grad_()
+    y = rn(x1)
+    w = rn.weight.detach().float().requires_grad_()
+    x2 = x.float().requires_grad_()
+    y2 = x2 * torch.rsqrt(x2.pow(2).mean(-1, keepdim=True) + 1e-6) * w
+    torch.testing.assert_close(y.float(), y2, **_tol(dt))
+    g = torch.randn_like(x2).to(dt)
+    y.backward(g)
+    y2.backward(g.float())
+    torch.testing.assert_close(x1.grad.float(), x2.grad, **_tol(dt))
+    torch.testing.assert_close(rn.weight.grad.float(), w.grad, rtol=3e-2, atol=0.3)
