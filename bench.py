@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--impl", choices=["xddp", "torch"], default="xddp",
                     help="xddp = this framework; torch = torch.nn.parallel.DDP reference stack (comparison only)")
-    ap.add_argument("--norm", choices=["xddp", "torch"], default="torch", help="BatchNorm implementation")
+    ap.add_argument("--norm", choices=["xddp", "torch"], default="xddp", help="BatchNorm implementation")
     ap.add_argument("--bucket-cap-mb", type=float, default=None)
     ap.add_argument("--comm-dtype", default="none", help="gradient comm dtype (none = param dtype)")
     ap.add_argument("--grad-as-bucket-view", type=int, default=1)

@@ -46,8 +46,8 @@ Geo make_geo(int64_t M, int C) {
   while (cvec % g.tx) g.tx--;  // tx divides the channel-vector count
   g.ty = kBlock / g.tx;
   g.cblocks = cvec / g.tx;
-  // aim for ~2048 blocks total, each row-block >= ty rows
-  int64_t want = std::max<int64_t>(1, 2048 / g.cblocks);
+  // aim for ~1024 blocks total (8 waves/CU-worth), each row-block >= ty rows
+  int64_t want = std::max<int64_t>(1, 1024 / g.cblocks);
   int64_t maxr = std::max<int64_t>(1, (M + g.ty - 1) / g.ty);
   g.rblocks = (int)std::min<int64_t>(std::min<int64_t>(want, maxr), 65535);
   g.rows_per = (M + g.rblocks - 1) / g.rblocks;
@@ -78,15 +78,24 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
   const int c0 = (blockIdx.x * TX + tx) * 8;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per;
   const int64_t r1 = min(M, r0 + rows_per);
-  float s[8] = {0}, ss[8] = {0};
+  // shifted sums: K = the thread's first sample per channel, so sum/sumsq of (x-K) do not
+  // cancel when |mean| >> std (guide §5.4 rule 26: the large-offset case has its own test)
+  float s[8] = {0}, ss[8] = {0}, k[8] = {0};
   int cnt = 0;
-  for (int64_t r = r0 + ty; r < r1; r += TY) {
+  int64_t r = r0 + ty;
+  if (r < r1) {
+    Vec8<T>::ld(x + r * C + c0, k);
+    cnt = 1;
+    r += TY;
+  }
+  for (; r < r1; r += TY) {
     float v[8];
     Vec8<T>::ld(x + r * C + c0, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      s[j] += v[j];
-      ss[j] = fmaf(v[j], v[j], ss[j]);
+      const float d = v[j] - k[j];
+      s[j] += d;
+      ss[j] = fmaf(d, d, ss[j]);
     }
     cnt++;
   }
@@ -95,10 +104,10 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
   const float n = (float)cnt;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float mean = cnt ? s[j] / n : 0.f;
+    const float dm = cnt ? s[j] / n : 0.f;
     my[j * 3 + 0] = n;
-    my[j * 3 + 1] = mean;
-    my[j * 3 + 2] = cnt ? fmaxf(ss[j] - s[j] * mean, 0.f) : 0.f;
+    my[j * 3 + 1] = k[j] + dm;
+    my[j * 3 + 2] = cnt ? fmaxf(ss[j] - s[j] * dm, 0.f) : 0.f;
   }
   __syncthreads();
   // tree-merge across ty
@@ -117,21 +126,45 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
   }
 }
 
-// One thread per channel: merge row-block partials; EMA running stats; scale/shift.
+// One block per 8-channel vector: 256 threads stride over the row-block partials (96-B
+// contiguous loads), Chan-merge in registers, then a tree merge in LDS; lane j<8 then
+// finalizes channel cv*8+j (mean, invstd, running-stat EMA, scale/shift).
 template <typename W>
 __global__ __launch_bounds__(kBlock) void bn_stats_finalize_kernel(
     const float* __restrict__ part, int rblocks, int C, int64_t M, const W* __restrict__ weight,
     const W* __restrict__ bias, W* running_mean, W* running_var, const int64_t* nbt, float momentum, bool cma,
-    float eps,
-    float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int b = 0; b < rblocks; ++b) {
-    const float* p = part + ((int64_t)b * C + c) * 3;
-    chan_merge(n, mean, m2, p[0], p[1], p[2]);
+    float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale,
+    float* __restrict__ shift) {
+  __shared__ float lds[kBlock * 24];
+  const int cv = blockIdx.x, t = threadIdx.x;
+  float n[8], mu[8], m2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) n[j] = mu[j] = m2[j] = 0.f;
+  for (int b = t; b < rblocks; b += kBlock) {
+    const float* p = part + ((int64_t)b * C + cv * 8) * 3;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) chan_merge(n[j], mu[j], m2[j], p[j * 3], p[j * 3 + 1], p[j * 3 + 2]);
   }
-  const float var = m2 / fmaxf(n, 1.f);
+  float* my = lds + t * 24;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    my[j * 3] = n[j];
+    my[j * 3 + 1] = mu[j];
+    my[j * 3 + 2] = m2[j];
+  }
+  __syncthreads();
+  for (int stride = kBlock / 2; stride > 0; stride >>= 1) {
+    if (t < stride) {
+      const float* o = lds + (t + stride) * 24;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) chan_merge(my[j * 3], my[j * 3 + 1], my[j * 3 + 2], o[j * 3], o[j * 3 + 1], o[j * 3 + 2]);
+    }
+    __syncthreads();
+  }
+  if (t >= 8) return;
+  const int c = cv * 8 + t;
+  const float cn = lds[t * 3], mean = lds[t * 3 + 1], cm2 = lds[t * 3 + 2];
+  const float var = cm2 / fmaxf(cn, 1.f);
   const float inv = rsqrtf(var + eps);
   mean_out[c] = mean;
   invstd_out[c] = inv;
@@ -246,20 +279,38 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
   }
 }
 
-// per channel: dgamma, dbeta; dx = k1*dy_eff + k2*(x-mean) + k3
+// per channel: dgamma, dbeta; dx = k1*dy_eff + k2*(x-mean) + k3. Same parallel shape as the
+// stats finalize: one block per 8-channel vector, threads stride over row-block partials.
 template <typename W>
 __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __restrict__ part, int rblocks, int C,
                                                                  int64_t M, const W* __restrict__ weight,
                                                                  const float* __restrict__ invstd, W* dweight,
                                                                  W* dbias, float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float sd = 0.f, sdx = 0.f;
-  for (int b = 0; b < rblocks; ++b) {
-    const float* p = part + ((int64_t)b * C + c) * 2;
-    sd += p[0];
-    sdx += p[1];
+  __shared__ float lds[kBlock * 16];
+  const int cv = blockIdx.x, t = threadIdx.x;
+  float acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  for (int b = t; b < rblocks; b += kBlock) {
+    const float* p = part + ((int64_t)b * C + cv * 8) * 2;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] += p[j];
   }
+  float* my = lds + t * 16;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) my[j] = acc[j];
+  __syncthreads();
+  for (int stride = kBlock / 2; stride > 0; stride >>= 1) {
+    if (t < stride) {
+      const float* o = lds + (t + stride) * 16;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) my[j] += o[j];
+    }
+    __syncthreads();
+  }
+  if (t >= 8) return;
+  const int c = cv * 8 + t;
+  const float sd = lds[t * 2], sdx = lds[t * 2 + 1];
   const float inv = invstd[c];
   const float g = weight ? Elem<W, float>::ld(weight, c) : 1.f;
   if (dweight) Elem<W, float>::st(dweight, c, sdx * inv);
@@ -372,7 +423,7 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
         hipLaunchKernelGGL((bn_stats_kernel<T>), dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds, stream,
                            reinterpret_cast<const T*>(x.data_ptr()), M, (int)C, g.rows_per, part.data_ptr<float>());
         XDDP_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL((bn_stats_finalize_kernel<W>), dim3(fin_grid), dim3(kBlock), 0, stream,
+        hipLaunchKernelGGL((bn_stats_finalize_kernel<W>), dim3(C / 8), dim3(kBlock), 0, stream,
                            part.data_ptr<float>(), g.rblocks, (int)C, M, opt_ptr<const W>(weight),
                            opt_ptr<const W>(bias), opt_ptr<W>(running_mean), opt_ptr<W>(running_var),
                            (num_batches_tracked.has_value() && num_batches_tracked->defined())
@@ -436,7 +487,7 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
                          reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(x.data_ptr()), yp, M,
                          (int)C, g.rows_per, mean.data_ptr<float>(), part.data_ptr<float>());
       XDDP_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
+      hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(kBlock), 0, stream,
                          part.data_ptr<float>(), g.rblocks, (int)C, M,
                          has_w ? reinterpret_cast<const W*>(weight->data_ptr()) : nullptr, invstd.data_ptr<float>(),
                          dw.defined() ? reinterpret_cast<W*>(dw.data_ptr()) : nullptr,

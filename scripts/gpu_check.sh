@@ -17,12 +17,13 @@ run() {  # run <name> <timeout> cmd...
 STEPS=${STEPS:-20}
 python -c "import torch; print(torch.cuda.get_device_name(0))"
 run pytest_gpu 600 python -m pytest tests -m gpu -x -q
-run bench_xddp 600 python bench.py --steps $STEPS --warmup 10 --json-out gpurun_out/bench_xddp.json
-run bench_torch 600 python bench.py --impl torch --steps $STEPS --warmup 10 --json-out gpurun_out/bench_torch.json
+run bench_xddp 600 python bench.py --norm xddp --steps $STEPS --warmup 10 --json-out gpurun_out/bench_xddp.json
+run bench_xddp_torchbn 600 python bench.py --norm torch --steps $STEPS --warmup 10 --json-out gpurun_out/bench_xddp_torchbn.json
+run bench_torch 600 python bench.py --impl torch --norm torch --steps $STEPS --warmup 10 --json-out gpurun_out/bench_torch.json
 if [ "${PROFILE:-1}" = "1" ]; then
   R=$PWD
   cd /tmp && export TMPDIR=/tmp
-  run_prof() { timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o prof --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 > "$R/gpurun_out/prof.log" 2>&1; }
+  run_prof() { timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o prof --output-format csv -- python3 "$R/bench.py" --norm xddp --steps 5 --warmup 5 > "$R/gpurun_out/prof.log" 2>&1; }
   run_prof; echo "prof rc=$?"
   cd "$R"
 fi

@@ -42,31 +42,37 @@ def test_rccl_collectives_w1(pg):
 @pytest.mark.parametrize("grad_as_view", [False, True])
 @pytest.mark.parametrize("comm_dtype", [None, torch.bfloat16])
 def test_ddp_matches_local_training(pg, grad_as_view, comm_dtype):
-    torch.manual_seed(0)
-    model = SimpleCNN().cuda()
-    ref = SimpleCNN().cuda()
-    ref.load_state_dict(model.state_dict())
-    ddp = xddp.DDP(model, device_ids=[0], gradient_as_bucket_view=grad_as_view, comm_dtype=comm_dtype)
-    o1 = torch.optim.SGD(ddp.parameters(), lr=0.01)
-    o2 = torch.optim.SGD(ref.parameters(), lr=0.01)
-    for it in range(4):
-        x = torch.randn(16, 3, 32, 32, device="cuda")
-        y = torch.randint(0, 10, (16,), device="cuda")
-        o1.zero_grad()
-        o2.zero_grad()
-        F.cross_entropy(ddp(x), y).backward()
-        F.cross_entropy(ref(x), y).backward()
-        for p, q in zip(model.parameters(), ref.parameters()):
-            tol = 1e-2 if comm_dtype is not None else 1e-5
-            torch.testing.assert_close(p.grad, q.grad, rtol=tol, atol=tol)
-        o1.step()
-        o2.step()
+    """W=1 DDP grads == plain-model grads (deterministic MIOpen; ref re-synced every step so
+    only the reducer's own numerics are measured: exact for fp32, bf16 rounding otherwise)."""
+    torch.backends.cudnn.deterministic = True
+    try:
+        torch.manual_seed(0)
+        model = SimpleCNN().cuda()
+        ref = SimpleCNN().cuda()
+        ddp = xddp.DDP(model, device_ids=[0], gradient_as_bucket_view=grad_as_view, comm_dtype=comm_dtype)
+        opt = torch.optim.SGD(ddp.parameters(), lr=0.01)
+        for it in range(4):
+            ref.load_state_dict(model.state_dict())
+            x = torch.randn(16, 3, 32, 32, device="cuda")
+            y = torch.randint(0, 10, (16,), device="cuda")
+            opt.zero_grad()
+            ref.zero_grad()
+            F.cross_entropy(ddp(x), y).backward()
+            F.cross_entropy(ref(x), y).backward()
+            for (n, p), q in zip(model.named_parameters(), ref.parameters()):
+                if comm_dtype is None:
+                    torch.testing.assert_close(p.grad, q.grad, rtol=0, atol=0, msg=f"it{it} {n}")
+                else:
+                    scale = q.grad.abs().max().item() + 1e-12
+                    assert (p.grad - q.grad).abs().max().item() <= 1e-2 * scale, (it, n)
+            opt.step()
+    finally:
+        torch.backends.cudnn.deterministic = False
     assert ddp.reducer.native_launches() > 0, "native bucket kernels did not run"
     d = ddp._get_ddp_logging_data()
     assert d["has_rebuilt_buckets"] == "1"
 
 
-@pytest.mark.parametrize("fused_bn", [False, True])
 def test_ddp_bf16_channels_last_fused_sgd(pg, fused_bn):
     from distributeddataparallel_amd.models import resnet50
     from distributeddataparallel_amd.ops import FusedBatchNorm2d
