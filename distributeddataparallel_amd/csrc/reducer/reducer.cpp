@@ -737,7 +737,21 @@ void verify_params_across_processes(const std::shared_ptr<Comm>& comm, const std
   } else {
     comm->broadcast(t, 0)->wait();
   }
-  if (!at::equal(t, mine)) {
+  // agree on the verdict so every rank raises (not only the ones that differ from rank 0)
+  const bool mismatch_local = !at::equal(t, mine);
+  auto flag = at::full({1}, mismatch_local ? 1 : 0, at::kInt);
+  if (dev.is_cuda()) {
+    auto d = flag.to(dev);
+    comm->allreduce(d, RedOp::MAX, 1.0)->wait();
+    flag = d.cpu();
+  } else {
+    comm->allreduce(flag, RedOp::MAX, 1.0)->wait();
+  }
+  if (flag.item<int>() != 0 && !mismatch_local) {
+    TORCH_CHECK(false, "DDP expects same model across all ranks, but another rank's parameter sizes/strides differ "
+                       "from rank 0 (this rank, ", comm->rank(), ", matches rank 0)");
+  }
+  if (mismatch_local) {
     // locate first mismatch for a helpful message
     const int64_t* a = mine.data_ptr<int64_t>();
     const int64_t* b = t.data_ptr<int64_t>();

@@ -20,5 +20,6 @@ def _entry(rank, fn, world, backend, args):
 def run_ranks(fn, world=2, backend="cpu", args=()):
     from distributeddataparallel_amd.utils.spawn import free_port, spawn
 
-    env = {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port()), "OMP_NUM_THREADS": "1"}
+    env = {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port()), "OMP_NUM_THREADS": "1",
+           "XDDP_TEST_TORCH_PORT": str(free_port())}
     spawn(_entry, args=(fn, world, backend, args), nprocs=world, env=env)
