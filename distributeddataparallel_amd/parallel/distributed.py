@@ -34,6 +34,7 @@ from torch.autograd.profiler import record_function
 
 from .. import distributed as xdist
 from .._native import load
+from ..utils import fault as _fault
 from .join import Join, Joinable, JoinHook
 
 logger = logging.getLogger(__name__)
@@ -224,6 +225,8 @@ class DistributedDataParallel(nn.Module, Joinable):
 
     # ----------------------------------------------------------------------------- forward
     def _pre_forward(self, *inputs, **kwargs):
+        self._forward_count = getattr(self, "_forward_count", 0) + 1
+        _fault.maybe_fail(self.process_group.rank(), self._forward_count)
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             self.reducer.prepare_for_forward()
         work = Join.notify_join_context(self)
