@@ -1,0 +1,229 @@
+"""PowerSGD gradient compression hook (reference: ``ddp_comm_hooks/powerSGD_hook.py:121-862``,
+Vogels et al. 2019), re-implemented on xddp collectives.
+
+Per bucket, every gradient of rank >= 2 larger than the low-rank payload is viewed as an
+``n x m`` matrix M (after adding the error-feedback residual) and approximated by ``P Qᵀ``
+with one power-iteration step:  P = M Q  → all-reduce(P) → orthogonalize(P) → Q = Mᵀ P →
+all-reduce(Q) → M ≈ P Qᵀ. Rank-1 tensors (biases, norms) and tensors where compression
+does not save bytes are all-reduced uncompressed in one flat buffer. Before
+``start_powerSGD_iter`` the hook is a plain all-reduce (vanilla warm start).
+"""
+from __future__ import annotations
+
+import math
+from collections import defaultdict
+from typing import Dict
+
+import torch
+
+from ... import distributed as xdist
+from .default_hooks import _allreduce_fut
+
+
+def _orthogonalize(matrices: torch.Tensor, epsilon: float = 0.0):
+    """In-place Gram-Schmidt over the columns of each matrix in a [B, n, r] batch."""
+    num_cols = matrices.shape[2]
+    for i in range(num_cols):
+        col = matrices[:, :, i: i + 1]
+        if epsilon == 0:
+            try:
+                col /= torch.norm(col, dim=1, keepdim=True)
+            except ZeroDivisionError:
+                col.fill_(0.0)
+        else:
+            col /= torch.norm(col, dim=1, keepdim=True) + epsilon
+        if i + 1 < num_cols:
+            rest = matrices[:, :, i + 1:]
+            rest -= torch.sum(col * rest, dim=1, keepdim=True) * col
+
+
+def _should_compress(num_rows, num_cols, rank, min_compression_rate):
+    uncompressed = num_rows * num_cols
+    compressed = (num_rows + num_cols) * rank
+    return compressed * min_compression_rate < uncompressed, uncompressed, compressed
+
+
+class PowerSGDState:
+    __slots__ = ["process_group", "matrix_approximation_rank", "start_powerSGD_iter", "min_compression_rate",
+                 "orthogonalization_epsilon", "use_error_feedback", "warm_start", "batch_tensors_with_same_shape",
+                 "rng", "error_dict", "p_memory_dict", "q_memory_dict", "iter", "total_numel_before_compression",
+                 "total_numel_after_compression", "compression_stats_logging_frequency",
+                 "next_stats_report"]
+
+    def __init__(self, process_group=None, matrix_approximation_rank: int = 1, start_powerSGD_iter: int = 1_000,
+                 min_compression_rate: float = 2, use_error_feedback: bool = True, warm_start: bool = True,
+                 orthogonalization_epsilon: float = 0, random_seed: int = 0,
+                 compression_stats_logging_frequency: int = 10_000, batch_tensors_with_same_shape: bool = False):
+        if use_error_feedback or warm_start:
+            if start_powerSGD_iter <= 1:
+                raise ValueError("start_powerSGD_iter must be > 1 when error feedback or warm start is enabled")
+        self.process_group = process_group
+        self.matrix_approximation_rank = matrix_approximation_rank
+        self.start_powerSGD_iter = start_powerSGD_iter
+        self.min_compression_rate = min_compression_rate
+        self.use_error_feedback = use_error_feedback
+        self.warm_start = warm_start
+        self.orthogonalization_epsilon = orthogonalization_epsilon
+        import numpy as np
+
+        self.rng = np.random.RandomState(random_seed)
+        self.error_dict: Dict[int, torch.Tensor] = {}
+        self.p_memory_dict: Dict[int, torch.Tensor] = {}
+        self.q_memory_dict: Dict[int, torch.Tensor] = {}
+        self.iter = 0
+        self.total_numel_before_compression = 0
+        self.total_numel_after_compression = 0
+        self.compression_stats_logging_frequency = max(1, compression_stats_logging_frequency)
+        self.next_stats_report = 0
+        self.batch_tensors_with_same_shape = batch_tensors_with_same_shape
+
+    def maybe_increase_iter(self, bucket):
+        if bucket.is_last():
+            self.iter += 1
+
+    def compression_stats(self):
+        ratio = (self.total_numel_before_compression / self.total_numel_after_compression
+                 if self.total_numel_after_compression > 0 else 0)
+        return ratio, self.total_numel_before_compression, self.total_numel_after_compression
+
+
+def powerSGD_hook(state: PowerSGDState, bucket) -> torch.futures.Future:
+    pg = state.process_group if state.process_group is not None else xdist.get_default_group()
+    world = pg.size()
+    input_tensor = bucket.buffer()
+    if state.iter < state.start_powerSGD_iter:
+        state.maybe_increase_iter(bucket)
+        return _allreduce_fut(pg, input_tensor)
+
+    device = input_tensor.device
+    dtype = input_tensor.dtype
+    bucket_index = bucket.index()
+    total_length = input_tensor.numel()
+    if state.use_error_feedback:
+        if bucket_index in state.error_dict and state.error_dict[bucket_index].numel() == total_length:
+            input_tensor.add_(state.error_dict[bucket_index])
+        else:
+            state.error_dict[bucket_index] = torch.zeros(total_length, device=device, dtype=dtype)
+        input_tensor_cp = input_tensor.clone()
+
+    tensors = bucket.gradients()
+    rank1_tensors, high_rank_tensors, high_rank_shapes = [], [], []
+    total_Ps, total_Qs = 0, 0
+    for t in tensors:
+        m = t.view(t.shape[0], -1)
+        n, mcols = m.shape
+        r = min(n, mcols, state.matrix_approximation_rank)
+        compress, u, c = _should_compress(n, mcols, r, state.min_compression_rate)
+        state.total_numel_before_compression += u
+        if compress:
+            high_rank_tensors.append(m)
+            total_Ps += n * r
+            total_Qs += mcols * r
+            state.total_numel_after_compression += c
+        else:
+            rank1_tensors.append(t)
+            state.total_numel_after_compression += u
+
+    rank1_buffer = (torch.cat([t.reshape(-1) for t in rank1_tensors]) if rank1_tensors
+                    else torch.tensor([], device=device, dtype=dtype))
+    need_randomize = bucket_index not in state.p_memory_dict or not state.warm_start
+    if bucket_index not in state.p_memory_dict or state.p_memory_dict[bucket_index].numel() != total_Ps:
+        state.p_memory_dict[bucket_index] = torch.empty(total_Ps, device=device, dtype=dtype)
+        state.q_memory_dict[bucket_index] = torch.empty(total_Qs, device=device, dtype=dtype)
+        need_randomize = True
+
+    ps, qs = [], []
+    p_idx, q_idx = 0, 0
+    for m in high_rank_tensors:
+        n, mcols = m.shape
+        r = min(n, mcols, state.matrix_approximation_rank)
+        ps.append(state.p_memory_dict[bucket_index][p_idx: p_idx + n * r].view(n, r))
+        qs.append(state.q_memory_dict[bucket_index][q_idx: q_idx + mcols * r].view(mcols, r))
+        p_idx += n * r
+        q_idx += mcols * r
+
+    if need_randomize:
+        torch.manual_seed(state.rng.randint(1_000_000_000))
+        for q in qs:
+            q.copy_(torch.randn(*q.shape, device="cpu", dtype=dtype))
+            _orthogonalize(q.unsqueeze(0), state.orthogonalization_epsilon)
+    else:
+        pass
+
+    # P = M Q (then all-reduce P) ; rank-1 tensors all-reduced uncompressed
+    for m, q, p in zip(high_rank_tensors, qs, ps):
+        torch.matmul(m, q, out=p)
+    if rank1_buffer.numel():
+        pg.allreduce(rank1_buffer).wait()
+        rank1_buffer.div_(world)
+        off = 0
+        for t in rank1_tensors:
+            t.copy_(rank1_buffer[off: off + t.numel()].view_as(t))
+            off += t.numel()
+    if total_Ps:
+        pg.allreduce(state.p_memory_dict[bucket_index]).wait()
+        for p in ps:
+            _orthogonalize(p.unsqueeze(0), state.orthogonalization_epsilon)
+        for m, q, p in zip(high_rank_tensors, qs, ps):
+            torch.matmul(m.t(), p, out=q)
+        pg.allreduce(state.q_memory_dict[bucket_index]).wait()
+        state.q_memory_dict[bucket_index].div_(world)
+        for m, q, p in zip(high_rank_tensors, qs, ps):
+            torch.matmul(p, q.t(), out=m)
+    if state.use_error_feedback:
+        state.error_dict[bucket_index] = input_tensor_cp - input_tensor
+    if not state.warm_start:
+        state.p_memory_dict.clear()
+        state.q_memory_dict.clear()
+    state.maybe_increase_iter(bucket)
+    fut = torch.futures.Future()
+    fut.set_result(input_tensor)
+    return fut
+
+
+def batched_powerSGD_hook(state: PowerSGDState, bucket) -> torch.futures.Future:
+    """Bucket-level PowerSGD: the whole flat bucket is one square-ish matrix."""
+    pg = state.process_group if state.process_group is not None else xdist.get_default_group()
+    world = pg.size()
+    input_tensor = bucket.buffer()
+    if state.iter < state.start_powerSGD_iter:
+        state.maybe_increase_iter(bucket)
+        return _allreduce_fut(pg, input_tensor)
+    device, dtype = input_tensor.device, input_tensor.dtype
+    total_length = input_tensor.numel()
+    square_side = math.ceil(math.sqrt(total_length))
+    padded = square_side ** 2
+    bi = bucket.index()
+    if state.use_error_feedback:
+        if bi in state.error_dict and state.error_dict[bi].numel() == padded:
+            pass
+        else:
+            state.error_dict[bi] = torch.zeros(padded, device=device, dtype=dtype)
+    work = torch.zeros(padded, device=device, dtype=dtype)
+    work[:total_length] = input_tensor
+    if state.use_error_feedback:
+        work.add_(state.error_dict[bi])
+        before = work.clone()
+    mat = work.view(square_side, square_side)
+    r = state.matrix_approximation_rank
+    if bi not in state.q_memory_dict or not state.warm_start or state.q_memory_dict[bi].shape != (square_side, r):
+        torch.manual_seed(state.rng.randint(1_000_000_000))
+        state.q_memory_dict[bi] = torch.randn(square_side, r, device="cpu", dtype=dtype).to(device)
+        _orthogonalize(state.q_memory_dict[bi].unsqueeze(0))
+    q = state.q_memory_dict[bi]
+    p = mat @ q
+    pg.allreduce(p).wait()
+    _orthogonalize(p.unsqueeze(0))
+    torch.matmul(mat.t(), p, out=q)
+    pg.allreduce(q).wait()
+    q.div_(world)
+    torch.matmul(p, q.t(), out=mat)
+    if state.use_error_feedback:
+        state.error_dict[bi] = before - work
+    input_tensor.copy_(work[:total_length])
+    state.total_numel_before_compression += total_length
+    state.total_numel_after_compression += 2 * square_side * r
+    state.maybe_increase_iter(bucket)
+    fut = torch.futures.Future()
+    fut.set_result(input_tensor)
+    return fut
