@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--grad-as-bucket-view", type=int, default=1)
     ap.add_argument("--channels-last", type=int, default=1)
     ap.add_argument("--no-sync-accum", type=int, default=1, help="micro-batches per step (no_sync accumulation)")
+    ap.add_argument("--seq-len", type=int, default=4096, help="LM configs: tokens per sequence")
+    ap.add_argument("--checkpoint", type=int, default=0, help="activation checkpointing (transformers)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -53,19 +55,30 @@ def parse():
 def build_model(args, device):
     from distributeddataparallel_amd import models
 
-    norm_layer = None
-    if args.norm == "xddp":
-        from distributeddataparallel_amd.ops.batch_norm import FusedBatchNorm2d
-
-        norm_layer = FusedBatchNorm2d
     if args.model.startswith("resnet"):
+        norm_layer = None
+        if args.norm == "xddp":
+            from distributeddataparallel_amd.ops.batch_norm import FusedBatchNorm2d
+
+            norm_layer = FusedBatchNorm2d
         m = getattr(models, args.model)(norm_layer=norm_layer)
+    elif args.model.startswith("vit"):
+        m = getattr(models, args.model)(checkpoint_activations=bool(args.checkpoint))
+    elif args.model == "llama3_8b":
+        with torch.device(device):
+            m = models.llama3_8b(max_seq_len=args.seq_len, checkpoint_activations=bool(args.checkpoint))
+    elif args.model == "llama_tiny":
+        m = models.llama_tiny(max_seq_len=args.seq_len)
     else:
         raise SystemExit(f"unknown model {args.model}")
     m = m.to(device=device, dtype=torch.bfloat16)
-    if args.channels_last:
+    if args.channels_last and args.model.startswith("resnet"):
         m = m.to(memory_format=torch.channels_last)
     return m
+
+
+def is_lm(args):
+    return args.model.startswith("llama")
 
 
 def main():
@@ -105,7 +118,12 @@ def main():
         comm_dtype = None if args.comm_dtype == "none" else getattr(torch, args.comm_dtype)
         ddp = xddp.DDP(model, device_ids=[local_rank], bucket_cap_mb=args.bucket_cap_mb,
                        gradient_as_bucket_view=bool(args.grad_as_bucket_view), comm_dtype=comm_dtype)
-        opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, master_weights=True)
+        if args.model.startswith("resnet"):
+            opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, master_weights=True)
+        else:
+            from distributeddataparallel_amd.optim import FusedAdamW
+
+            opt = FusedAdamW(ddp.parameters(), lr=1e-4, weight_decay=0.1, master_weights=True)
         zero_kw = dict(set_to_none=True)
     else:
         ddp = torch.nn.parallel.DistributedDataParallel(
@@ -115,10 +133,20 @@ def main():
         zero_kw = dict(set_to_none=True)
 
     B, S = args.batch_size, args.image_size
-    mf = torch.channels_last if args.channels_last else torch.contiguous_format
     g = torch.Generator(device=device).manual_seed(1234 + rank)
-    x = torch.randn(B, 3, S, S, device=device, generator=g).to(torch.bfloat16).contiguous(memory_format=mf)
-    y = torch.randint(0, 1000, (B,), device=device, generator=g)
+    if is_lm(args):
+        vocab = model.cfg.vocab_size
+        x = torch.randint(0, vocab, (B, args.seq_len), device=device, generator=g)
+        y = torch.randint(0, vocab, (B, args.seq_len), device=device, generator=g)
+    else:
+        mf = torch.channels_last if (args.channels_last and args.model.startswith("resnet")) else torch.contiguous_format
+        x = torch.randn(B, 3, S, S, device=device, generator=g).to(torch.bfloat16).contiguous(memory_format=mf)
+        y = torch.randint(0, 1000, (B,), device=device, generator=g)
+
+    def loss_fn(out, tgt):
+        if is_lm(args):
+            return F.cross_entropy(out.float().view(-1, out.shape[-1]), tgt.view(-1))
+        return F.cross_entropy(out.float(), tgt)
     micro = max(1, args.no_sync_accum)
     xs, ys = x.chunk(micro), y.chunk(micro)
 
@@ -127,9 +155,9 @@ def main():
         for i in range(micro):
             if i < micro - 1:
                 with ddp.no_sync():
-                    F.cross_entropy(ddp(xs[i]).float(), ys[i]).backward()
+                    loss_fn(ddp(xs[i]), ys[i]).backward()
             else:
-                loss = F.cross_entropy(ddp(xs[i]).float(), ys[i])
+                loss = loss_fn(ddp(xs[i]), ys[i])
                 loss.backward()
         opt.step()
         return loss
@@ -154,13 +182,19 @@ def main():
     elapsed = float(et.item())
     final_loss = float(loss.float().item())
     ms = elapsed / args.steps * 1e3
-    total_imgs = B * world * args.steps
-    value = total_imgs / elapsed
+    units = B * world * args.steps * (args.seq_len if is_lm(args) else 1)
+    value = units / elapsed
     if rank == 0:
+        if args.model == "resnet50":
+            metric = "images/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X; scaling efficiency"
+        elif is_lm(args):
+            metric = f"tokens/sec (whole node) {args.model} pure DDP"
+        else:
+            metric = f"images/sec (whole node) {args.model} DDP"
         out = {
-            "metric": "images/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X; scaling efficiency",
+            "metric": metric,
             "value": round(value, 2),
-            "unit": "images/s",
+            "unit": "tokens/s" if is_lm(args) else "images/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -169,17 +203,19 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (random ImageNet-shaped 3x224x224 bf16 inputs, random labels; random-init weights)",
+            "data": ("synthetic (random token ids; random-init weights)" if is_lm(args) else
+                     "synthetic (random ImageNet-shaped 3x224x224 bf16 inputs, random labels; random-init weights)"),
             "config": {
                 "model": args.model,
                 "global_batch": B * world,
                 "per_gpu_batch": B,
-                "seq_len": None,
+                "seq_len": args.seq_len if is_lm(args) else None,
                 "image_size": S,
                 "parallelism": f"dp{world}",
                 "impl": args.impl,
                 "norm": args.norm,
-                "optimizer": "SGD(momentum=0.9, wd=1e-4) fp32 master weights",
+                "optimizer": ("SGD(momentum=0.9, wd=1e-4) fp32 master weights" if args.model.startswith("resnet")
+                              else "AdamW(wd=0.1) fp32 master weights"),
                 "channels_last": bool(args.channels_last),
                 "comm_dtype": args.comm_dtype,
                 "gradient_as_bucket_view": bool(args.grad_as_bucket_view),

@@ -1,0 +1,133 @@
+"""Llama-3 decoder (8B config) — BASELINE.json config 5 (Llama-3-8B bf16 pure DDP).
+
+RMSNorm on xddp's fused kernel, rotary embeddings from a precomputed cos/sin table,
+grouped-query attention through ``F.scaled_dot_product_attention`` (causal), SwiGLU MLP.
+Pure DDP sizing on MI355X: 8.03B params → 16 GB bf16 params + 16 GB bf16
+grads (bucket views) + 96 GB fp32 master/Adam ≈ 128 GB of the 288 GB HBM3E, leaving room
+for activations (optionally checkpointed per layer).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.layer_norm import FusedRMSNorm
+
+__all__ = ["LlamaConfig", "Llama", "llama3_8b", "llama_tiny"]
+
+
+@dataclass
+class LlamaConfig:
+    vocab_size: int = 128256
+    dim: int = 4096
+    n_layers: int = 32
+    n_heads: int = 32
+    n_kv_heads: int = 8
+    ffn_dim: int = 14336
+    norm_eps: float = 1e-5
+    rope_theta: float = 500000.0
+    max_seq_len: int = 8192
+    checkpoint_activations: bool = False
+
+
+def _rope_table(head_dim, max_len, theta, device=None):
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float32, device=device) / head_dim))
+    t = torch.arange(max_len, dtype=torch.float32, device=device)
+    f = torch.outer(t, inv)
+    return torch.cos(f), torch.sin(f)
+
+
+def _apply_rope(x, cos, sin):
+    # x: [B, H, S, Dh]; rotate pairs (even, odd)
+    x1, x2 = x[..., 0::2].float(), x[..., 1::2].float()
+    c, s = cos[None, None], sin[None, None]
+    out = torch.stack([x1 * c - x2 * s, x1 * s + x2 * c], dim=-1).flatten(-2)
+    return out.to(x.dtype)
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.h, self.kvh = cfg.n_heads, cfg.n_kv_heads
+        self.hd = cfg.dim // cfg.n_heads
+        self.wq = nn.Linear(cfg.dim, self.h * self.hd, bias=False)
+        self.wk = nn.Linear(cfg.dim, self.kvh * self.hd, bias=False)
+        self.wv = nn.Linear(cfg.dim, self.kvh * self.hd, bias=False)
+        self.wo = nn.Linear(self.h * self.hd, cfg.dim, bias=False)
+
+    def forward(self, x, cos, sin):
+        B, S, _ = x.shape
+        q = self.wq(x).view(B, S, self.h, self.hd).transpose(1, 2)
+        k = self.wk(x).view(B, S, self.kvh, self.hd).transpose(1, 2)
+        v = self.wv(x).view(B, S, self.kvh, self.hd).transpose(1, 2)
+        q, k = _apply_rope(q, cos, sin), _apply_rope(k, cos, sin)
+        if self.kvh != self.h:
+            rep = self.h // self.kvh
+            k = k.repeat_interleave(rep, dim=1)
+            v = v.repeat_interleave(rep, dim=1)
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        return self.wo(o.transpose(1, 2).reshape(B, S, -1))
+
+
+class FeedForward(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.w1 = nn.Linear(cfg.dim, cfg.ffn_dim, bias=False)
+        self.w2 = nn.Linear(cfg.ffn_dim, cfg.dim, bias=False)
+        self.w3 = nn.Linear(cfg.dim, cfg.ffn_dim, bias=False)
+
+    def forward(self, x):
+        return self.w2(F.silu(self.w1(x)) * self.w3(x))
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.attention_norm = FusedRMSNorm(cfg.dim, eps=cfg.norm_eps)
+        self.attention = Attention(cfg)
+        self.ffn_norm = FusedRMSNorm(cfg.dim, eps=cfg.norm_eps)
+        self.feed_forward = FeedForward(cfg)
+
+    def forward(self, x, cos, sin):
+        x = x + self.attention(self.attention_norm(x), cos, sin)
+        return x + self.feed_forward(self.ffn_norm(x))
+
+
+class Llama(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.tok_embeddings = nn.Embedding(cfg.vocab_size, cfg.dim)
+        self.layers = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layers)])
+        self.norm = FusedRMSNorm(cfg.dim, eps=cfg.norm_eps)
+        self.output = nn.Linear(cfg.dim, cfg.vocab_size, bias=False)
+        cos, sin = _rope_table(cfg.dim // cfg.n_heads, cfg.max_seq_len, cfg.rope_theta)
+        self.register_buffer("rope_cos", cos, persistent=False)
+        self.register_buffer("rope_sin", sin, persistent=False)
+        for m in self.modules():
+            if isinstance(m, (nn.Linear, nn.Embedding)):
+                nn.init.normal_(m.weight, std=0.02)
+
+    def forward(self, tokens):
+        S = tokens.shape[1]
+        cos, sin = self.rope_cos[:S].float(), self.rope_sin[:S].float()
+        h = self.tok_embeddings(tokens)
+        for blk in self.layers:
+            if self.cfg.checkpoint_activations and self.training:
+                h = torch.utils.checkpoint.checkpoint(blk, h, cos, sin, use_reentrant=False)
+            else:
+                h = blk(h, cos, sin)
+        return self.output(self.norm(h))
+
+
+def llama3_8b(**kw):
+    return Llama(LlamaConfig(**kw))
+
+
+def llama_tiny(**kw):
+    base = dict(vocab_size=512, dim=64, n_layers=2, n_heads=4, n_kv_heads=2, ffn_dim=128, max_seq_len=128)
+    base.update(kw)
+    return Llama(LlamaConfig(**base))

@@ -1,0 +1,90 @@
+"""Vision Transformer (ViT-B/16, ViT-L/16, ...) — BASELINE.json config 4 (ViT-L/16 bf16 DDP).
+
+Pre-norm encoder blocks with xddp's fused LayerNorm kernel, attention through
+``F.scaled_dot_product_attention`` (flash path on ROCm), GELU MLP. Random init; the
+structure/parameter count matches torchvision's ``vit_l_16`` (304,326,632 params at 1000
+classes).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.layer_norm import FusedLayerNorm
+
+__all__ = ["VisionTransformer", "vit_b_16", "vit_l_16", "vit_tiny"]
+
+
+class _Attention(nn.Module):
+    def __init__(self, dim, heads):
+        super().__init__()
+        self.heads = heads
+        self.in_proj = nn.Linear(dim, 3 * dim)
+        self.out_proj = nn.Linear(dim, dim)
+
+    def forward(self, x):
+        B, N, D = x.shape
+        qkv = self.in_proj(x).view(B, N, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
+        o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
+        return self.out_proj(o.transpose(1, 2).reshape(B, N, D))
+
+
+class EncoderBlock(nn.Module):
+    def __init__(self, dim, heads, mlp_dim, norm_layer):
+        super().__init__()
+        self.ln_1 = norm_layer(dim, eps=1e-6)
+        self.self_attention = _Attention(dim, heads)
+        self.ln_2 = norm_layer(dim, eps=1e-6)
+        self.mlp = nn.Sequential(nn.Linear(dim, mlp_dim), nn.GELU(), nn.Linear(mlp_dim, dim))
+
+    def forward(self, x):
+        x = x + self.self_attention(self.ln_1(x))
+        return x + self.mlp(self.ln_2(x))
+
+
+class VisionTransformer(nn.Module):
+    def __init__(self, image_size=224, patch_size=16, num_layers=24, num_heads=16, hidden_dim=1024, mlp_dim=4096,
+                 num_classes=1000, norm_layer=FusedLayerNorm, checkpoint_activations: bool = False):
+        super().__init__()
+        self.patch_size = patch_size
+        self.hidden_dim = hidden_dim
+        self.checkpoint_activations = checkpoint_activations
+        self.conv_proj = nn.Conv2d(3, hidden_dim, kernel_size=patch_size, stride=patch_size)
+        n = (image_size // patch_size) ** 2 + 1
+        self.class_token = nn.Parameter(torch.zeros(1, 1, hidden_dim))
+        self.pos_embedding = nn.Parameter(torch.empty(1, n, hidden_dim).normal_(std=0.02))
+        self.layers = nn.ModuleList([EncoderBlock(hidden_dim, num_heads, mlp_dim, norm_layer)
+                                     for _ in range(num_layers)])
+        self.ln = norm_layer(hidden_dim, eps=1e-6)
+        self.head = nn.Linear(hidden_dim, num_classes)
+        nn.init.trunc_normal_(self.conv_proj.weight, std=(1.0 / (3 * patch_size * patch_size)) ** 0.5)
+        nn.init.zeros_(self.conv_proj.bias)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.xavier_uniform_(m.weight)
+                nn.init.normal_(m.bias, std=1e-6)
+        nn.init.zeros_(self.head.weight)
+        nn.init.zeros_(self.head.bias)
+
+    def forward(self, x):
+        x = self.conv_proj(x).flatten(2).transpose(1, 2)
+        x = torch.cat([self.class_token.expand(x.shape[0], -1, -1), x], dim=1) + self.pos_embedding
+        for blk in self.layers:
+            if self.checkpoint_activations and self.training:
+                x = torch.utils.checkpoint.checkpoint(blk, x, use_reentrant=False)
+            else:
+                x = blk(x)
+        return self.head(self.ln(x)[:, 0])
+
+
+def vit_b_16(**kw):
+    return VisionTransformer(num_layers=12, num_heads=12, hidden_dim=768, mlp_dim=3072, **kw)
+
+
+def vit_l_16(**kw):
+    return VisionTransformer(num_layers=24, num_heads=16, hidden_dim=1024, mlp_dim=4096, **kw)
+
+
+def vit_tiny(**kw):
+    return VisionTransformer(image_size=32, patch_size=8, num_layers=2, num_heads=2, hidden_dim=64, mlp_dim=128, **kw)
