@@ -73,6 +73,7 @@ def test_ddp_matches_local_training(pg, grad_as_view, comm_dtype):
     assert d["has_rebuilt_buckets"] == "1"
 
 
+@pytest.mark.parametrize("fused_bn", [False, True])
 def test_ddp_bf16_channels_last_fused_sgd(pg, fused_bn):
     from distributeddataparallel_amd.models import resnet50
     from distributeddataparallel_amd.ops import FusedBatchNorm2d
@@ -102,16 +103,23 @@ def test_resnet50_fused_bn_matches_torch_bn(pg):
     from distributeddataparallel_amd.models import resnet50
     from distributeddataparallel_amd.ops import FusedBatchNorm2d
 
-    torch.manual_seed(0)
-    a = resnet50(norm_layer=FusedBatchNorm2d).cuda().to(memory_format=torch.channels_last)
-    b = resnet50().cuda().to(memory_format=torch.channels_last)
-    b.load_state_dict(a.state_dict())
-    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (4,), device="cuda")
-    la = F.cross_entropy(a(x), y)
-    lb = F.cross_entropy(b(x), y)
-    torch.testing.assert_close(la, lb, rtol=1e-3, atol=1e-3)
-    la.backward()
-    lb.backward()
-    for (n, p), q in zip(a.named_parameters(), b.parameters()):
-        torch.testing.assert_close(p.grad, q.grad, rtol=2e-2, atol=2e-3, msg=n)
+    torch.backends.cudnn.deterministic = True
+    try:
+        torch.manual_seed(0)
+        a = resnet50(norm_layer=FusedBatchNorm2d).cuda().to(memory_format=torch.channels_last)
+        b = resnet50().cuda().to(memory_format=torch.channels_last)
+        b.load_state_dict(a.state_dict())
+        x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (4,), device="cuda")
+        la = F.cross_entropy(a(x), y)
+        lb = F.cross_entropy(b(x), y)
+        torch.testing.assert_close(la, lb, rtol=1e-3, atol=1e-3)
+        la.backward()
+        lb.backward()
+        for (n, p), q in zip(a.named_parameters(), b.parameters()):
+            rel = ((p.grad - q.grad).norm() / (q.grad.norm() + 1e-12)).item()
+            assert rel < 1e-2, (n, rel)
+        for (n, ba), bb in zip(a.named_buffers(), b.buffers()):
+            torch.testing.assert_close(ba.float(), bb.float(), rtol=1e-3, atol=1e-4, msg=n)
+    finally:
+        torch.backends.cudnn.deterministic = False

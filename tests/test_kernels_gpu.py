@@ -126,7 +126,9 @@ def test_fused_sgd_master_weights_bf16():
         o2.step()
     for p, q in zip(ps, refq):
         torch.testing.assert_close(o1.state[p]["master"], q.detach(), rtol=1e-5, atol=1e-5)
-        torch.testing.assert_close(p.float(), q.detach().to(torch.bfloat16).float())
+        # the bf16 param is the rounded master: at most one bf16 ulp from the rounded reference
+        torch.testing.assert_close(p.float(), o1.state[p]["master"].to(torch.bfloat16).float(), rtol=0, atol=0)
+        torch.testing.assert_close(p.float(), q.detach().float(), rtol=8e-3, atol=1e-5)
 
 
 @pytest.mark.parametrize("wd", [0.0, 0.01])
