@@ -227,29 +227,41 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
 
 // ---------------------------------------------------------------- backward reduce
 // part layout [rblocks][C][2] = (sum dy_eff, sum dy_eff*(x-mean))
-template <typename T, bool RELU>
+// MASK: 0 = no ReLU, 1 = ReLU mask from the saved output y, 2 = ReLU mask recomputed from x
+// (x*scale+shift > 0, exact for BN+ReLU without residual; saves reading y)
+template <typename T, int MASK>
 __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                                const T* __restrict__ y, int64_t M, int C,
                                                                int64_t rows_per, const float* __restrict__ mean,
+                                                               const float* __restrict__ ss,
                                                                float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
   const int c0 = (blockIdx.x * TX + tx) * 8;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per;
   const int64_t r1 = min(M, r0 + rows_per);
-  float mu[8];
+  float mu[8], sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) mu[j] = mean[c0 + j];
+  for (int j = 0; j < 8; ++j) {
+    mu[j] = mean[c0 + j];
+    if (MASK == 2) {
+      sc[j] = ss[c0 + j];
+      sh[j] = ss[C + c0 + j];
+    }
+  }
   float sd[8] = {0}, sdx[8] = {0};
   for (int64_t r = r0 + ty; r < r1; r += TY) {
     float g[8], a[8];
     Vec8<T>::ld(dy + r * C + c0, g);
     Vec8<T>::ld(x + r * C + c0, a);
-    if (RELU) {
+    if (MASK == 1) {
       float o[8];
       Vec8<T>::ld(y + r * C + c0, o);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = o[j] > 0.f ? g[j] : 0.f;
+    } else if (MASK == 2) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = fmaf(a[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -321,12 +333,13 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __
   coef[2 * C + c] = -g * inv * sd * invM;              // k3
 }
 
-template <typename T, bool RELU, bool DRES>
+template <typename T, int MASK, bool DRES>
 __global__ __launch_bounds__(kBlock) void bn_bwd_elem_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                              const T* __restrict__ y, T* __restrict__ dx,
                                                              T* __restrict__ dres, int64_t nvec, int C,
                                                              const float* __restrict__ mean,
-                                                             const float* __restrict__ coef) {
+                                                             const float* __restrict__ coef,
+                                                             const float* __restrict__ ss) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
     const int64_t e = v * 8;
@@ -334,11 +347,14 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_elem_kernel(const T* __restrict
     float g[8], a[8];
     Vec8<T>::ld(dy + e, g);
     Vec8<T>::ld(x + e, a);
-    if (RELU) {
+    if (MASK == 1) {
       float o[8];
       Vec8<T>::ld(y + e, o);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = o[j] > 0.f ? g[j] : 0.f;
+    } else if (MASK == 2) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = fmaf(a[j], ss[c0 + j], ss[C + c0 + j]) > 0.f ? g[j] : 0.f;
     }
     if (DRES) Vec8<T>::st(dres + e, g);
     float out[8];
@@ -452,17 +468,21 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
       XDDP_HIP_CHECK(hipGetLastError());
     });
   });
-  return {y, mean, invstd};
+  return {y, mean, invstd, ss};
 }
 
 // returns (dx, dweight, dbias, dresidual)
 std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x, const c10::optional<at::Tensor>& y,
                                     const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
-                                    const at::Tensor& invstd, bool relu, bool need_dres, bool need_dweight) {
+                                    const at::Tensor& invstd, const c10::optional<at::Tensor>& ss, bool relu,
+                                    bool need_dres, bool need_dweight) {
   check_nhwc(x);
   auto dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "dy must match x");
-  if (relu) TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the forward output");
+  const bool have_y = y.has_value() && y->defined();
+  const bool have_ss = ss.has_value() && ss->defined();
+  if (relu) TORCH_CHECK(have_y || have_ss, "relu backward needs the forward output or the scale/shift");
+  const int mask = relu ? (have_y ? 1 : 2) : 0;
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), Wd = x.size(3);
   const int64_t M = N * H * Wd;
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
@@ -480,12 +500,13 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
     using T = decltype(tag_t);
     dispatch_w(wdt, [&](auto tag_w) {
       using W = decltype(tag_w);
-      const T* yp = relu ? reinterpret_cast<const T*>(y->data_ptr()) : nullptr;
+      const T* yp = mask == 1 ? reinterpret_cast<const T*>(y->data_ptr()) : nullptr;
+      const float* ssp = mask == 2 ? ss->data_ptr<float>() : nullptr;
       const size_t lds = (size_t)kBlock * 8 * 2 * sizeof(float);
-      auto red = relu ? bn_bwd_reduce_kernel<T, true> : bn_bwd_reduce_kernel<T, false>;
+      auto red = mask == 1 ? bn_bwd_reduce_kernel<T, 1> : (mask == 2 ? bn_bwd_reduce_kernel<T, 2> : bn_bwd_reduce_kernel<T, 0>);
       hipLaunchKernelGGL(red, dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds, stream,
                          reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(x.data_ptr()), yp, M,
-                         (int)C, g.rows_per, mean.data_ptr<float>(), part.data_ptr<float>());
+                         (int)C, g.rows_per, mean.data_ptr<float>(), ssp, part.data_ptr<float>());
       XDDP_HIP_CHECK(hipGetLastError());
       hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(kBlock), 0, stream,
                          part.data_ptr<float>(), g.rblocks, (int)C, M,
@@ -499,10 +520,11 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
                            reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(x.data_ptr()), yp,
                            reinterpret_cast<T*>(dx.data_ptr()),
                            need_dres ? reinterpret_cast<T*>(dres.data_ptr()) : nullptr, nvec, (int)C,
-                           mean.data_ptr<float>(), coef.data_ptr<float>());
+                           mean.data_ptr<float>(), coef.data_ptr<float>(), ssp);
       };
-      if (relu) { if (need_dres) launch(bn_bwd_elem_kernel<T, true, true>); else launch(bn_bwd_elem_kernel<T, true, false>); }
-      else { if (need_dres) launch(bn_bwd_elem_kernel<T, false, true>); else launch(bn_bwd_elem_kernel<T, false, false>); }
+      if (mask == 1) { if (need_dres) launch(bn_bwd_elem_kernel<T, 1, true>); else launch(bn_bwd_elem_kernel<T, 1, false>); }
+      else if (mask == 2) { if (need_dres) launch(bn_bwd_elem_kernel<T, 2, true>); else launch(bn_bwd_elem_kernel<T, 2, false>); }
+      else { if (need_dres) launch(bn_bwd_elem_kernel<T, 0, true>); else launch(bn_bwd_elem_kernel<T, 0, false>); }
       XDDP_HIP_CHECK(hipGetLastError());
     });
   });

@@ -96,9 +96,17 @@ class Bottleneck(nn.Module):
 class ResNet(nn.Module):
     def __init__(self, block: Type[Union[BasicBlock, Bottleneck]], layers: List[int], num_classes: int = 1000,
                  zero_init_residual: bool = False, groups: int = 1, width_per_group: int = 64,
-                 norm_layer: Optional[Callable[..., nn.Module]] = None):
+                 norm_layer: Optional[Callable[..., nn.Module]] = None,
+                 pool_layer: Optional[Callable[..., nn.Module]] = None):
         super().__init__()
         norm_layer = norm_layer or nn.BatchNorm2d
+        if pool_layer is None:
+            if getattr(norm_layer, "fuses_relu", False):  # the fused-kernel stack: native NHWC max-pool too
+                from ..ops.pool import FusedMaxPool2d
+
+                pool_layer = FusedMaxPool2d
+            else:
+                pool_layer = nn.MaxPool2d
         self._norm_layer = norm_layer
         self.inplanes = 64
         self.dilation = 1
@@ -106,7 +114,7 @@ class ResNet(nn.Module):
         self.base_width = width_per_group
         self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1, self.relu = _bn_relu(norm_layer, self.inplanes)
-        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.maxpool = pool_layer(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)

@@ -24,19 +24,22 @@ class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, residual, relu):
         C = load()
-        y, mean, invstd = C.bn_forward(x, weight, bias, running_mean, running_var, nbt, True, momentum, cma, eps,
-                                       residual, relu)
+        y, mean, invstd, ss = C.bn_forward(x, weight, bias, running_mean, running_var, nbt, True, momentum, cma,
+                                           eps, residual, relu)
         ctx.relu = relu
         ctx.has_res = residual is not None
-        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        # ReLU mask: from y when a residual was added (mask depends on it), else recomputed
+        # from x*scale+shift in the backward kernels (one fewer activation read)
+        keep_y = relu and residual is not None
+        ctx.save_for_backward(x, y if keep_y else None, weight, mean, invstd, ss)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         C = load()
-        x, y, weight, mean, invstd = ctx.saved_tensors
+        x, y, weight, mean, invstd, ss = ctx.saved_tensors
         need_dw = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
-        dx, dw, db, dres = C.bn_backward(dy, x, y, weight, mean, invstd, ctx.relu,
+        dx, dw, db, dres = C.bn_backward(dy, x, y, weight, mean, invstd, ss, ctx.relu,
                                          ctx.has_res and ctx.needs_input_grad[9], need_dw)
         return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, None, dres if ctx.has_res else None, None)
@@ -61,8 +64,8 @@ def batch_norm_act(x, running_mean, running_var, weight=None, bias=None, trainin
     if use_kernel and not training and not (torch.is_grad_enabled() and (
             x.requires_grad or (weight is not None and weight.requires_grad))):
         C = load()
-        y, _, _ = C.bn_forward(x, weight, bias, running_mean, running_var, None, False, 0.0, False, float(eps),
-                               residual, relu)
+        y, _, _, _ = C.bn_forward(x, weight, bias, running_mean, running_var, None, False, 0.0, False, float(eps),
+                                  residual, relu)
         return y
     # reference path
     if training and num_batches_tracked is not None:

@@ -124,3 +124,39 @@ def test_rmsnorm(dt):
     y2.backward(g.float())
     torch.testing.assert_close(x1.grad.float(), x2.grad, **_tol(dt))
     torch.testing.assert_close(rn.weight.grad.float(), w.grad, rtol=3e-2, atol=0.3)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((2, 16, 9, 7), 3, 2, 1), ((2, 8, 8, 8), 2, 2, 0),
+                                         ((1, 24, 10, 10), 3, 1, 1)])
+def test_maxpool_nhwc(dt, shape, k, s, p):
+    from distributeddataparallel_amd.ops import FusedMaxPool2d
+
+    torch.manual_seed(0)
+    x = torch.randn(shape, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    x1 = x.clone().requires_grad_()
+    x2 = x.float().clone().requires_grad_()
+    y1 = FusedMaxPool2d(k, s, p)(x1)
+    y2 = F.max_pool2d(x2, k, s, p)
+    torch.testing.assert_close(y1.float(), y2, rtol=0, atol=0)
+    g = torch.randn(y2.shape, device=DEV).to(dt)
+    y1.backward(g.contiguous(memory_format=torch.channels_last))
+    y2.backward(g.float())
+    torch.testing.assert_close(x1.grad.float(), x2.grad, **_tol(dt))
+
+
+def test_batchnorm_relu_mask_recompute_matches_saved_output_path():
+    """Non-residual BN+ReLU recomputes the mask from x in backward; residual BN+ReLU reads y."""
+    torch.manual_seed(1)
+    bn = FusedBatchNorm2d(32).cuda()
+    x = torch.randn(8, 32, 6, 6, device=DEV).contiguous(memory_format=torch.channels_last)
+    zero = torch.zeros_like(x)
+    a = x.clone().requires_grad_()
+    b = x.clone().requires_grad_()
+    ya = bn(a, relu=True)
+    yb = bn(b, residual=zero, relu=True)
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    torch.testing.assert_close(ya, yb)
+    torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-6)
