@@ -68,7 +68,7 @@ def write_ninja(debug: bool = False) -> Path:
     cpp_flags = f"{common} -x c++"
     libs = (
         f"-L{tlib} -Wl,-rpath,{tlib} -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip "
-        f"-ltorch_python -lamdhip64 -lrccl -lpthread"
+        f"-ltorch_python -lamdhip64 -lrccl -lroctx64 -lpthread"
     )
     hip, cpp = _sources()
     BUILD_DIR.mkdir(exist_ok=True)

@@ -174,6 +174,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                               std::chrono::milliseconds(static_cast<int64_t>(timeout_s * 1000)), high_priority);
       }, py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("timeout_s") = 600.0,
       py::arg("high_priority") = true, py::call_guard<py::gil_scoped_release>());
+  m.def("make_debug_comm", &make_debug_comm, py::arg("inner"), py::arg("fingerprint") = true,
+        py::arg("nan_check") = false);
   m.def("rccl_version", &rccl_version);
   m.def("rccl_stream_handle", &rccl_stream_handle);
 

@@ -110,7 +110,7 @@ class Comm : public std::enable_shared_from_this<Comm> {
   virtual void abort() {}
   virtual void shutdown() {}
 
-  FlightRecorder& flight() { return flight_; }
+  virtual FlightRecorder& flight() { return flight_; }
   // Debug: TORCH_DISTRIBUTED_DEBUG=DETAIL-style fingerprint check before each collective.
   bool debug_fingerprint = false;
 
@@ -129,6 +129,9 @@ std::shared_ptr<Comm> make_tcp_comm_host(std::shared_ptr<Store> store, int rank,
 // RCCL backend --------------------------------------------------------------------------
 std::shared_ptr<Comm> make_rccl_comm(std::shared_ptr<Store> store, int rank, int size, int device,
                                      std::chrono::milliseconds timeout, bool high_priority_stream);
+
+// Debug wrapper: per-collective cross-rank fingerprint check and/or NaN check.
+std::shared_ptr<Comm> make_debug_comm(std::shared_ptr<Comm> inner, bool fingerprint, bool nan_check);
 
 // Extra RCCL-only entry points (no-ops / errors for other backends).
 std::string rccl_version();

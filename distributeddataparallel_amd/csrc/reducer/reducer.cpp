@@ -2,7 +2,9 @@
 #include "reducer/reducer.h"
 
 #include <ATen/hip/HIPContext.h>
+#include <ATen/record_function.h>
 #include <c10/hip/HIPGuard.h>
+#include <roctracer/roctx.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/csrc/autograd/engine.h>
 #include <torch/csrc/autograd/utils/lambda_post_hook.h>
@@ -18,6 +20,12 @@
 namespace xddp {
 
 namespace {
+
+// Scoped marker visible in both torch.profiler (RECORD_FUNCTION) and rocprofv3 (roctx range).
+struct Range {
+  explicit Range(const char* name) { roctxRangePushA(name); }
+  ~Range() { roctxRangePop(); }
+};
 
 constexpr int64_t kPad = 16;  // element alignment of every gradient slot in a bucket
 
@@ -420,6 +428,8 @@ void Reducer::mark_bucket_ready(int64_t b) {
 }
 
 void Reducer::launch_bucket(int64_t b) {
+  RECORD_FUNCTION("xddp::reducer::launch_bucket", std::vector<c10::IValue>());
+  Range range("xddp::reducer::launch_bucket");
   auto& bk = buckets_[b];
   const bool cast = !bk.comm.is_same(bk.flat);
   // In view mode grads live in `flat`; otherwise (cast) we pack straight into the comm buffer.
@@ -498,6 +508,8 @@ void Reducer::all_reduce_local_used_map() {
 }
 
 void Reducer::finalize_backward() {
+  RECORD_FUNCTION("xddp::reducer::finalize_backward", std::vector<c10::IValue>());
+  Range range("xddp::reducer::finalize_backward");
   std::lock_guard<std::mutex> g(mu_);
   if (!expect_hooks_) return;
   const bool static_first = opts_.static_graph && !static_first_iter_done_;
@@ -615,6 +627,7 @@ std::vector<std::vector<int64_t>> Reducer::sync_bucket_indices(std::vector<std::
 }
 
 bool Reducer::rebuild_buckets() {
+  RECORD_FUNCTION("xddp::reducer::rebuild_buckets", std::vector<c10::IValue>());
   std::lock_guard<std::mutex> g(mu_);
   if (!should_rebuild_buckets() || prev_ready_order_.empty()) return false;
   TORCH_CHECK(!require_finalize_, "xddp Reducer: cannot rebuild buckets while a reduction is in flight");

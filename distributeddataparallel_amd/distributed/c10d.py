@@ -248,11 +248,19 @@ def _device_for(backend: str, device_id):
 
 
 def _make_comm(backend: str, store, rank: int, size: int, device, timeout: timedelta, master_addr: str):
+    """Create the native communicator; XDDP_DEBUG=DETAIL / XDDP_NAN_CHECK=1 wrap it in the debug
+    communicator (cross-rank collective fingerprints / NaN scan)."""
     C = load()
     if backend == "rccl":
         hp = os.environ.get("XDDP_COMM_HIGH_PRIORITY", "1") != "0"
-        return C.make_rccl_comm(store, rank, size, device.index, timeout.total_seconds(), hp)
-    return C.make_cpu_comm(store, rank, size, timeout.total_seconds(), advertise_host(master_addr))
+        comm = C.make_rccl_comm(store, rank, size, device.index, timeout.total_seconds(), hp)
+    else:
+        comm = C.make_cpu_comm(store, rank, size, timeout.total_seconds(), advertise_host(master_addr))
+    detail = os.environ.get("XDDP_DEBUG", os.environ.get("TORCH_DISTRIBUTED_DEBUG", "OFF")).upper() == "DETAIL"
+    nan = os.environ.get("XDDP_NAN_CHECK", "0") == "1"
+    if detail or nan:
+        comm = C.make_debug_comm(comm, detail, nan)
+    return comm
 
 
 def init_process_group(backend: Optional[str] = None, init_method: Optional[str] = None,
