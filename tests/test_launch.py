@@ -89,3 +89,19 @@ def test_sampler_matches_reference(n, world, drop_last, shuffle):
             b.set_epoch(ep)
             assert list(a) == list(b)
         assert len(a) == len(b)
+
+
+def test_reference_workload_example_runs_and_resumes(tmp_path):
+    """examples/train_ddp_cifar.py (the ref:dpp.py workflow) on the CPU backend, with checkpoint+resume."""
+    ck = tmp_path / "ck.pt"
+    ex = os.path.join(REPO, "examples", "train_ddp_cifar.py")
+    base = [sys.executable, ex, "--spawn", "2", "--backend", "cpu", "--synthetic-len", "256", "--max-steps", "3",
+            "--batch-size", "8"]
+    r = subprocess.run(base + ["--epochs", "1", "--checkpoint", str(ck)], env=_env(), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Epoch 0, Batch 0, Loss:" in r.stdout and ck.exists()
+    r = subprocess.run(base + ["--epochs", "2", "--resume", str(ck)], env=_env(), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Epoch 1, Batch 0" in r.stdout and "Epoch 0," not in r.stdout
