@@ -202,9 +202,12 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
                                                           const float* __restrict__ shift, int64_t* nbt_inc) {
   if (nbt_inc && blockIdx.x == 0 && threadIdx.x == 0) nbt_inc[0] += 1;  // num_batches_tracked.add_(1), fused
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+  const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // channel offset advanced incrementally: no 64-bit modulo in the loop
+  const int cstep = (int)((stride * 8) % C);
+  int c0 = (int)((v0 * 8) % C);
+  for (int64_t v = v0; v < nvec; v += stride, c0 = (c0 + cstep >= C) ? c0 + cstep - C : c0 + cstep) {
     const int64_t e = v * 8;
-    const int c0 = (int)(e % C);
     float a[8], r[8];
     Vec8<T>::ld(x + e, a);
     if (RES) Vec8<T>::ld(res + e, r);
@@ -341,9 +344,11 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_elem_kernel(const T* __restrict
                                                              const float* __restrict__ coef,
                                                              const float* __restrict__ ss) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+  const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cstep = (int)((stride * 8) % C);
+  int c0 = (int)((v0 * 8) % C);
+  for (int64_t v = v0; v < nvec; v += stride, c0 = (c0 + cstep >= C) ? c0 + cstep - C : c0 + cstep) {
     const int64_t e = v * 8;
-    const int c0 = (int)(e % C);
     float g[8], a[8];
     Vec8<T>::ld(dy + e, g);
     Vec8<T>::ld(x + e, a);
@@ -353,16 +358,21 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_elem_kernel(const T* __restrict
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = o[j] > 0.f ? g[j] : 0.f;
     } else if (MASK == 2) {
+      float sc[8], sh[8];
+      Vec8<float>::ld(ss + c0, sc);
+      Vec8<float>::ld(ss + C + c0, sh);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = fmaf(a[j], ss[c0 + j], ss[C + c0 + j]) > 0.f ? g[j] : 0.f;
+      for (int j = 0; j < 8; ++j) g[j] = fmaf(a[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
     }
     if (DRES) Vec8<T>::st(dres + e, g);
-    float out[8];
+    // per-channel coefficients as 16-B vector loads (L1/L2 resident; C*16 B per array)
+    float k1[8], k2[8], k3[8], mu[8], out[8];
+    Vec8<float>::ld(coef + c0, k1);
+    Vec8<float>::ld(coef + C + c0, k2);
+    Vec8<float>::ld(coef + 2 * C + c0, k3);
+    Vec8<float>::ld(mean + c0, mu);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      out[j] = fmaf(coef[c], g[j], fmaf(coef[C + c], a[j] - mean[c], coef[2 * C + c]));
-    }
+    for (int j = 0; j < 8; ++j) out[j] = fmaf(k1[j], g[j], fmaf(k2[j], a[j] - mu[j], k3[j]));
     Vec8<T>::st(dx + e, out);
   }
 }
