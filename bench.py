@@ -22,13 +22,11 @@ import os
 import sys
 import time
 
-# MIOpen conv tuning (MI355X-specific): an exhaustive search picks conv solutions ~13% faster
+# MIOpen conv tuning (MI355X-specific): an exhaustive search picks conv solutions ~11% faster
 # than MIOpen's default heuristic for this config but costs ~200 s. The repo ships the resulting
 # find-db + perf-db + compiled-kernel cache (tuning/miopen, generated on MI355X by
 # scripts/gpu_tune.sh); each process copies it to a private temp dir (MIOpen writes to it) and
-# MIOpen's NORMAL find mode then resolves every conv from the db. Without the shipped db the
-# search runs inside the untimed warmup steps.
-os.environ.setdefault("MIOPEN_FIND_MODE", "1")
+# MIOpen's default DYNAMIC_HYBRID find mode resolves every conv from the db (first step <1 s).
 
 
 def _install_miopen_tuning():

@@ -46,8 +46,9 @@ Geo make_geo(int64_t M, int C) {
   while (cvec % g.tx) g.tx--;  // tx divides the channel-vector count
   g.ty = kBlock / g.tx;
   g.cblocks = cvec / g.tx;
-  // aim for ~1024 blocks total (8 waves/CU-worth), each row-block >= ty rows
-  int64_t want = std::max<int64_t>(1, 1024 / g.cblocks);
+  // ~512 blocks total (2 per CU, 8 waves/CU) keeps HBM busy while the per-channel finalize
+  // only has <= 512 row-block partials to merge
+  int64_t want = std::max<int64_t>(1, 512 / g.cblocks);
   int64_t maxr = std::max<int64_t>(1, (M + g.ty - 1) / g.ty);
   g.rblocks = (int)std::min<int64_t>(std::min<int64_t>(want, maxr), 65535);
   g.rows_per = (M + g.rblocks - 1) / g.rblocks;
@@ -87,6 +88,21 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
     Vec8<T>::ld(x + r * C + c0, k);
     cnt = 1;
     r += TY;
+  }
+  // 4 independent 16-B loads in flight per lane (memory-level parallelism), then the tail
+  for (; r + 3 * TY < r1; r += 4 * TY) {
+    float v0[8], v1[8], v2[8], v3[8];
+    Vec8<T>::ld(x + r * C + c0, v0);
+    Vec8<T>::ld(x + (r + TY) * C + c0, v1);
+    Vec8<T>::ld(x + (r + 2 * TY) * C + c0, v2);
+    Vec8<T>::ld(x + (r + 3 * TY) * C + c0, v3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d0 = v0[j] - k[j], d1 = v1[j] - k[j], d2 = v2[j] - k[j], d3 = v3[j] - k[j];
+      s[j] += (d0 + d1) + (d2 + d3);
+      ss[j] = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, ss[j]))));
+    }
+    cnt += 4;
   }
   for (; r < r1; r += TY) {
     float v[8];
@@ -253,6 +269,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
     }
   }
   float sd[8] = {0}, sdx[8] = {0};
+#pragma unroll 2
   for (int64_t r = r0 + ty; r < r1; r += TY) {
     float g[8], a[8];
     Vec8<T>::ld(dy + r * C + c0, g);
