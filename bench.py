@@ -71,6 +71,7 @@ def parse():
     ap.add_argument("--no-sync-accum", type=int, default=1, help="micro-batches per step (no_sync accumulation)")
     ap.add_argument("--seq-len", type=int, default=4096, help="LM configs: tokens per sequence")
     ap.add_argument("--checkpoint", type=int, default=0, help="activation checkpointing (transformers)")
+    ap.add_argument("--graphs", type=int, default=0, help="replay the whole DDP step as one captured HIP graph")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -78,13 +79,16 @@ def parse():
 def build_model(args, device):
     from distributeddataparallel_amd import models
 
-    if args.model.startswith("resnet"):
+    if args.model.startswith("resnet") or args.model == "simplecnn":
         norm_layer = None
         if args.norm == "xddp":
             from distributeddataparallel_amd.ops.batch_norm import FusedBatchNorm2d
 
             norm_layer = FusedBatchNorm2d
-        m = getattr(models, args.model)(norm_layer=norm_layer)
+        if args.model == "simplecnn":  # the reference's model: ResNet-18 with a 10-class head
+            m = models.SimpleCNN(norm_layer=norm_layer)
+        else:
+            m = getattr(models, args.model)(norm_layer=norm_layer)
     elif args.model.startswith("vit"):
         m = getattr(models, args.model)(checkpoint_activations=bool(args.checkpoint))
     elif args.model == "llama3_8b":
@@ -95,7 +99,7 @@ def build_model(args, device):
     else:
         raise SystemExit(f"unknown model {args.model}")
     m = m.to(device=device, dtype=torch.bfloat16)
-    if args.channels_last and args.model.startswith("resnet"):
+    if args.channels_last and (args.model.startswith("resnet") or args.model == "simplecnn"):
         m = m.to(memory_format=torch.channels_last)
     return m
 
@@ -141,7 +145,7 @@ def main():
         comm_dtype = None if args.comm_dtype == "none" else getattr(torch, args.comm_dtype)
         ddp = xddp.DDP(model, device_ids=[local_rank], bucket_cap_mb=args.bucket_cap_mb,
                        gradient_as_bucket_view=bool(args.grad_as_bucket_view), comm_dtype=comm_dtype)
-        if args.model.startswith("resnet"):
+        if args.model.startswith("resnet") or args.model == "simplecnn":
             opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, master_weights=True)
         else:
             from distributeddataparallel_amd.optim import FusedAdamW
@@ -162,9 +166,10 @@ def main():
         x = torch.randint(0, vocab, (B, args.seq_len), device=device, generator=g)
         y = torch.randint(0, vocab, (B, args.seq_len), device=device, generator=g)
     else:
-        mf = torch.channels_last if (args.channels_last and args.model.startswith("resnet")) else torch.contiguous_format
+        conv = args.model.startswith("resnet") or args.model == "simplecnn"
+        mf = torch.channels_last if (args.channels_last and conv) else torch.contiguous_format
         x = torch.randn(B, 3, S, S, device=device, generator=g).to(torch.bfloat16).contiguous(memory_format=mf)
-        y = torch.randint(0, 1000, (B,), device=device, generator=g)
+        y = torch.randint(0, 10 if args.model == "simplecnn" else 1000, (B,), device=device, generator=g)
 
     def loss_fn(out, tgt):
         if is_lm(args):
@@ -173,7 +178,17 @@ def main():
     micro = max(1, args.no_sync_accum)
     xs, ys = x.chunk(micro), y.chunk(micro)
 
+    graphed = None
+    if args.graphs:
+        if micro > 1:
+            raise SystemExit("--graphs does not combine with --no-sync-accum")
+        from distributeddataparallel_amd.utils.graphs import GraphedTrainStep
+
+        graphed = GraphedTrainStep(ddp, opt, loss_fn, x, y, warmup_steps=3)
+
     def step():
+        if graphed is not None:
+            return graphed(x, y)
         opt.zero_grad(**zero_kw)
         for i in range(micro):
             if i < micro - 1:
@@ -232,7 +247,7 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": ("synthetic (random token ids; random-init weights)" if is_lm(args) else
-                     "synthetic (random ImageNet-shaped 3x224x224 bf16 inputs, random labels; random-init weights)"),
+                     f"synthetic (random 3x{S}x{S} bf16 inputs, random labels; random-init weights)"),
             "config": {
                 "model": args.model,
                 "global_batch": B * world,
@@ -248,6 +263,7 @@ def main():
                 "comm_dtype": args.comm_dtype,
                 "gradient_as_bucket_view": bool(args.grad_as_bucket_view),
                 "micro_batches": micro,
+                "hip_graphs": bool(args.graphs),
             },
             "final_loss": round(final_loss, 4),
         }

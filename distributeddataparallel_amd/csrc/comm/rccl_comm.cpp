@@ -103,6 +103,7 @@ class RcclWork : public Work {
   ~RcclWork() override { pool_->put(ev); }
   bool is_completed() override {
     check_error();
+    if (captured) return true;
     return hipEventQuery(ev) == hipSuccess;
   }
   void wait() override {
@@ -112,6 +113,7 @@ class RcclWork : public Work {
   }
   void synchronize() override {
     check_error();
+    if (captured) return;  // host sync inside a capture is illegal; replay ordering is by stream
     XDDP_HIP_CHECK(hipEventSynchronize(ev));
     check_error();
   }
@@ -123,6 +125,7 @@ class RcclWork : public Work {
   }
   hipEvent_t ev;
   int64_t t_start;
+  bool captured = false;
 
  private:
   std::shared_ptr<EventPool> pool_;
@@ -299,6 +302,11 @@ class RcclComm : public Comm {
     TORCH_CHECK(!destroyed_, "xddp rccl: communicator was shut down");
     c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
     auto cur = c10::hip::getCurrentHIPStream(device_);
+    // HIP-graph capture: the comm stream joins the capture through the event wait below; works
+    // recorded inside a capture are graph nodes, so the watchdog must not poll them.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    XDDP_HIP_CHECK(hipStreamIsCapturing(cur.stream(), &cap));
+    capturing_ = cap == hipStreamCaptureStatusActive;
     hipEvent_t pre = pool_->get();
     XDDP_HIP_CHECK(hipEventRecord(pre, cur.stream()));
     XDDP_HIP_CHECK(hipStreamWaitEvent(stream_.stream(), pre, 0));
@@ -306,11 +314,14 @@ class RcclComm : public Comm {
     auto w = std::make_shared<RcclWork>(pool_, device_, err_);
     w->seq = flight_.record(name, meta.numel(), meta.scalar_type());
     body(stream_.stream());
-    for (auto& t : keep) {
-      if (t.defined() && t.is_cuda())
-        c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_);
+    if (!capturing_) {
+      for (auto& t : keep) {
+        if (t.defined() && t.is_cuda())
+          c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_);
+      }
     }
     w->outputs = std::move(keep);
+    w->captured = capturing_;
     if (in_group_ > 0) group_works_.push_back(w);
     else finish_launch(w);
     return w;
@@ -329,6 +340,7 @@ class RcclComm : public Comm {
 
   void finish_launch(const std::shared_ptr<RcclWork>& w) {
     XDDP_HIP_CHECK(hipEventRecord(w->ev, stream_.stream()));
+    if (w->captured) return;  // a graph node, not a live collective
     std::lock_guard<std::mutex> g(wd_mu_);
     inflight_.push_back(w);
   }
@@ -383,6 +395,7 @@ class RcclComm : public Comm {
   bool aborted_ = false;
   bool destroyed_ = false;
   int in_group_ = 0;
+  bool capturing_ = false;
   std::vector<std::shared_ptr<RcclWork>> group_works_;
   at::Tensor barrier_buf_;
   std::thread watchdog_;

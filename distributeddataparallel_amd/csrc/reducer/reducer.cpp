@@ -257,8 +257,17 @@ hipStream_t Reducer::current_stream() const {
 
 void Reducer::timer_record(int slot) {
   if (!timing_this_iter_) return;
-  if (on_gpu()) XDDP_HIP_CHECK(hipEventRecord(gpu_ev_[slot], current_stream()));
-  else cpu_ts_[slot] = now_ns();
+  if (on_gpu()) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    XDDP_HIP_CHECK(hipStreamIsCapturing(current_stream(), &cap));
+    if (cap == hipStreamCaptureStatusActive) {  // no timing inside a HIP-graph capture
+      timing_this_iter_ = false;
+      return;
+    }
+    XDDP_HIP_CHECK(hipEventRecord(gpu_ev_[slot], current_stream()));
+  } else {
+    cpu_ts_[slot] = now_ns();
+  }
 }
 
 void Reducer::harvest_timings() {

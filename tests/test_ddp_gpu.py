@@ -125,3 +125,45 @@ def test_resnet50_fused_bn_matches_torch_bn(pg):
             torch.testing.assert_close(ba.float(), bb.float(), rtol=1e-3, atol=1e-4, msg=n)
     finally:
         torch.backends.cudnn.deterministic = False
+
+
+def test_graphed_train_step_matches_eager(pg):
+    """HIP-graph capture of the whole DDP step (fwd, bwd + bucket all-reduce, FusedSGD) replays
+    to the same parameters as eager steps."""
+    from distributeddataparallel_amd.ops import FusedBatchNorm2d
+    from distributeddataparallel_amd.optim import FusedSGD
+    from distributeddataparallel_amd.utils.graphs import GraphedTrainStep
+
+    torch.backends.cudnn.deterministic = True
+    try:
+        def make():
+            torch.manual_seed(0)
+            m = SimpleCNN(norm_layer=FusedBatchNorm2d).cuda().to(memory_format=torch.channels_last)
+            d = xddp.DDP(m, device_ids=[0], gradient_as_bucket_view=True)
+            return m, d, FusedSGD(d.parameters(), lr=0.05, momentum=0.9)
+
+        g = torch.Generator(device="cuda").manual_seed(3)
+        xs = [torch.randn(32, 3, 32, 32, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+              for _ in range(8)]
+        ys = [torch.randint(0, 10, (32,), device="cuda", generator=g) for _ in range(8)]
+        lf = F.cross_entropy
+        m1, d1, o1 = make()
+        for x, y in zip(xs[:3] + xs, ys[:3] + ys):  # 3 warmup steps like the capture helper
+            o1.zero_grad(set_to_none=True)
+            lf(d1(x), y).backward()
+            o1.step()
+        m2, d2, o2 = make()
+        step = GraphedTrainStep(d2, o2, lf, xs[0], ys[0], warmup_steps=3)
+        # the helper's warmup used xs[0] three times; redo the eager reference the same way
+        m3, d3, o3 = make()
+        for x, y in zip([xs[0]] * 3 + xs, [ys[0]] * 3 + ys):
+            o3.zero_grad(set_to_none=True)
+            lf(d3(x), y).backward()
+            o3.step()
+        for x, y in zip(xs, ys):
+            step(x, y)
+        torch.cuda.synchronize()
+        for (n, a), b in zip(m2.named_parameters(), m3.parameters()):
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5, msg=n)
+    finally:
+        torch.backends.cudnn.deterministic = False
