@@ -142,44 +142,40 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
   }
 }
 
-// One block per 8-channel vector: 256 threads stride over the row-block partials (96-B
-// contiguous loads), Chan-merge in registers, then a tree merge in LDS; lane j<8 then
-// finalizes channel cv*8+j (mean, invstd, running-stat EMA, scale/shift).
+// One 64-lane wave per 8-channel vector: lanes stride over the <=512 row-block partials
+// (Chan-merging 8 independent channel chains per lane), then a 6-step shuffle butterfly merges
+// across lanes — no LDS, no barriers (this kernel is pure latency: ~C/8 waves on 256 CUs).
+// Lane j < 8 finalizes channel cv*8+j (mean, invstd, running-stat EMA, scale/shift).
 template <typename W>
-__global__ __launch_bounds__(kBlock) void bn_stats_finalize_kernel(
+__global__ __launch_bounds__(64) void bn_stats_finalize_kernel(
     const float* __restrict__ part, int rblocks, int C, int64_t M, const W* __restrict__ weight,
     const W* __restrict__ bias, W* running_mean, W* running_var, const int64_t* nbt, float momentum, bool cma,
     float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale,
     float* __restrict__ shift) {
-  __shared__ float lds[kBlock * 24];
-  const int cv = blockIdx.x, t = threadIdx.x;
+  const int cv = blockIdx.x, lane = threadIdx.x;
   float n[8], mu[8], m2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) n[j] = mu[j] = m2[j] = 0.f;
-  for (int b = t; b < rblocks; b += kBlock) {
+  for (int b = lane; b < rblocks; b += 64) {
     const float* p = part + ((int64_t)b * C + cv * 8) * 3;
 #pragma unroll
     for (int j = 0; j < 8; ++j) chan_merge(n[j], mu[j], m2[j], p[j * 3], p[j * 3 + 1], p[j * 3 + 2]);
   }
-  float* my = lds + t * 24;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    my[j * 3] = n[j];
-    my[j * 3 + 1] = mu[j];
-    my[j * 3 + 2] = m2[j];
-  }
-  __syncthreads();
-  for (int stride = kBlock / 2; stride > 0; stride >>= 1) {
-    if (t < stride) {
-      const float* o = lds + (t + stride) * 24;
+  for (int o = 32; o > 0; o >>= 1) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) chan_merge(my[j * 3], my[j * 3 + 1], my[j * 3 + 2], o[j * 3], o[j * 3 + 1], o[j * 3 + 2]);
+    for (int j = 0; j < 8; ++j) {
+      const float on = __shfl_xor(n[j], o, 64), om = __shfl_xor(mu[j], o, 64), o2 = __shfl_xor(m2[j], o, 64);
+      chan_merge(n[j], mu[j], m2[j], on, om, o2);
     }
-    __syncthreads();
   }
-  if (t >= 8) return;
-  const int c = cv * 8 + t;
-  const float cn = lds[t * 3], mean = lds[t * 3 + 1], cm2 = lds[t * 3 + 2];
+  if (lane >= 8) return;
+  // lane j picks channel j out of its (identical) registers without dynamic indexing
+  float cn = n[0], mean = mu[0], cm2 = m2[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j)
+    if (lane == j) { cn = n[j]; mean = mu[j]; cm2 = m2[j]; }
+  const int c = cv * 8 + lane;
   const float var = cm2 / fmaxf(cn, 1.f);
   const float inv = rsqrtf(var + eps);
   mean_out[c] = mean;
@@ -311,38 +307,30 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
   }
 }
 
-// per channel: dgamma, dbeta; dx = k1*dy_eff + k2*(x-mean) + k3. Same parallel shape as the
-// stats finalize: one block per 8-channel vector, threads stride over row-block partials.
+// per channel: dgamma, dbeta; dx = k1*dy_eff + k2*(x-mean) + k3. Same single-wave shape as the
+// stats finalize: lanes stride over row-block partials, then a shuffle butterfly.
 template <typename W>
-__global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __restrict__ part, int rblocks, int C,
-                                                                 int64_t M, const W* __restrict__ weight,
-                                                                 const float* __restrict__ invstd, W* dweight,
-                                                                 W* dbias, float* __restrict__ coef) {
-  __shared__ float lds[kBlock * 16];
-  const int cv = blockIdx.x, t = threadIdx.x;
+__global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(const float* __restrict__ part, int rblocks, int C,
+                                                             int64_t M, const W* __restrict__ weight,
+                                                             const float* __restrict__ invstd, W* dweight,
+                                                             W* dbias, float* __restrict__ coef) {
+  const int cv = blockIdx.x, lane = threadIdx.x;
   float acc[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-  for (int b = t; b < rblocks; b += kBlock) {
+  for (int b = lane; b < rblocks; b += 64) {
     const float* p = part + ((int64_t)b * C + cv * 8) * 2;
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] += p[j];
   }
-  float* my = lds + t * 16;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) my[j] = acc[j];
-  __syncthreads();
-  for (int stride = kBlock / 2; stride > 0; stride >>= 1) {
-    if (t < stride) {
-      const float* o = lds + (t + stride) * 16;
+  for (int j = 0; j < 16; ++j) acc[j] = dev::wave_sum(acc[j]);
+  if (lane >= 8) return;
+  float sd = acc[0], sdx = acc[1];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) my[j] += o[j];
-    }
-    __syncthreads();
-  }
-  if (t >= 8) return;
-  const int c = cv * 8 + t;
-  const float sd = lds[t * 2], sdx = lds[t * 2 + 1];
+  for (int j = 1; j < 8; ++j)
+    if (lane == j) { sd = acc[2 * j]; sdx = acc[2 * j + 1]; }
+  const int c = cv * 8 + lane;
   const float inv = invstd[c];
   const float g = weight ? Elem<W, float>::ld(weight, c) : 1.f;
   if (dweight) Elem<W, float>::st(dweight, c, sdx * inv);
@@ -466,7 +454,7 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
         hipLaunchKernelGGL((bn_stats_kernel<T>), dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds, stream,
                            reinterpret_cast<const T*>(x.data_ptr()), M, (int)C, g.rows_per, part.data_ptr<float>());
         XDDP_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL((bn_stats_finalize_kernel<W>), dim3(C / 8), dim3(kBlock), 0, stream,
+        hipLaunchKernelGGL((bn_stats_finalize_kernel<W>), dim3(C / 8), dim3(64), 0, stream,
                            part.data_ptr<float>(), g.rblocks, (int)C, M, opt_ptr<const W>(weight),
                            opt_ptr<const W>(bias), opt_ptr<W>(running_mean), opt_ptr<W>(running_var),
                            (num_batches_tracked.has_value() && num_batches_tracked->defined())
@@ -535,7 +523,7 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
                          reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(x.data_ptr()), yp, M,
                          (int)C, g.rows_per, mean.data_ptr<float>(), ssp, part.data_ptr<float>());
       XDDP_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(kBlock), 0, stream,
+      hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(64), 0, stream,
                          part.data_ptr<float>(), g.rblocks, (int)C, M,
                          has_w ? reinterpret_cast<const W*>(weight->data_ptr()) : nullptr, invstd.data_ptr<float>(),
                          dw.defined() ? reinterpret_cast<W*>(dw.data_ptr()) : nullptr,

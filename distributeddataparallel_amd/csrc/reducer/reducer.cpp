@@ -295,6 +295,16 @@ void Reducer::harvest_timings() {
 
 void Reducer::prepare_for_forward() {
   std::lock_guard<std::mutex> g(mu_);
+  if (on_gpu()) {
+    // event queries are illegal while the caller's stream is being captured into a HIP graph
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    XDDP_HIP_CHECK(hipStreamIsCapturing(current_stream(), &cap));
+    if (cap == hipStreamCaptureStatusActive) {
+      num_iterations_++;
+      timing_this_iter_ = false;
+      return;
+    }
+  }
   harvest_timings();
   num_iterations_++;
   timing_this_iter_ = !timing_pending_ && (num_iterations_ <= 10 || num_iterations_ % sample_rate_ == 0);

@@ -27,6 +27,10 @@ class GraphedTrainStep:
         self.model, self.optimizer, self.loss_fn = model, optimizer, loss_fn
         self.static_input = example_input.clone()
         self.static_target = example_target.clone()
+        # MIOpen's immediate-mode path compiles/looks up solutions per call, which is illegal while
+        # a stream is capturing; with benchmark mode torch resolves each conv once through the
+        # Find API during warmup and replays the cached algorithm inside the capture.
+        torch.backends.cudnn.benchmark = True
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -39,7 +43,7 @@ class GraphedTrainStep:
         optimizer.zero_grad(set_to_none=set_to_none)
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: the communicator's watchdog thread keeps polling live (non-captured) work
-        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+        with torch.cuda.graph(self.graph, stream=side, capture_error_mode="thread_local"):
             self.static_loss = loss_fn(model(self.static_input), self.static_target)
             self.static_loss.backward()
             optimizer.step()

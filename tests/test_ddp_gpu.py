@@ -167,3 +167,48 @@ def test_graphed_train_step_matches_eager(pg):
             torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5, msg=n)
     finally:
         torch.backends.cudnn.deterministic = False
+
+
+@pytest.mark.parametrize("which", ["llama", "vit"])
+def test_transformer_ddp_fused_norms_adamw(pg, which):
+    """Transformer configs on the native path: fused LayerNorm/RMSNorm kernels, bucketed DDP,
+    FusedAdamW with fp32 master weights (bf16 params) — grads match a plain model."""
+    from distributeddataparallel_amd.models import llama_tiny, vit_tiny
+    from distributeddataparallel_amd.optim import FusedAdamW
+
+    def make():
+        torch.manual_seed(0)
+        return (llama_tiny() if which == "llama" else vit_tiny(num_classes=10)).cuda()
+
+    m, ref = make(), make()
+    ddp = xddp.DDP(m, device_ids=[0], bucket_cap_mb=0.05, first_bucket_cap_mb=0.01, gradient_as_bucket_view=True)
+    if which == "llama":
+        x = torch.randint(0, 512, (4, 32), device="cuda")
+        y = torch.randint(0, 512, (4, 32), device="cuda")
+        lf = lambda o, t: F.cross_entropy(o.float().reshape(-1, o.shape[-1]), t.reshape(-1))  # noqa: E731
+    else:
+        x = torch.randn(4, 3, 32, 32, device="cuda")
+        y = torch.randint(0, 10, (4,), device="cuda")
+        lf = lambda o, t: F.cross_entropy(o.float(), t)  # noqa: E731
+    for _ in range(2):
+        ref.load_state_dict(m.state_dict())
+        m.zero_grad(set_to_none=True)
+        ref.zero_grad(set_to_none=True)
+        lf(ddp(x), y).backward()
+        lf(ref(x), y).backward()
+        for (n, a), b in zip(m.named_parameters(), ref.parameters()):
+            torch.testing.assert_close(a.grad, b.grad, rtol=1e-4, atol=1e-5, msg=n)
+    assert len(ddp.reducer.bucket_sizes_bytes()) > 1
+    # bf16 model + fp32-master AdamW steps through the fused kernel
+    mb = make().to(torch.bfloat16)
+    ddpb = xddp.DDP(mb, device_ids=[0], gradient_as_bucket_view=True)
+    opt = FusedAdamW(ddpb.parameters(), lr=1e-3, master_weights=True)
+    losses = []
+    for _ in range(5):
+        opt.zero_grad(set_to_none=True)
+        xx = x if which == "llama" else x.to(torch.bfloat16)
+        loss = lf(ddpb(xx), y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0], losses
