@@ -244,10 +244,13 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
 // part layout [rblocks][C][2] = (sum dy_eff, sum dy_eff*(x-mean))
 // MASK: 0 = no ReLU, 1 = ReLU mask from the saved output y, 2 = ReLU mask recomputed from x
 // (x*scale+shift > 0, exact for BN+ReLU without residual; saves reading y)
-template <typename T, int MASK>
-__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
-                                                               const T* __restrict__ y, int64_t M, int C,
-                                                               int64_t rows_per, const float* __restrict__ mean,
+// DUAL: the output had two consumers whose gradients arrive separately (dy + dy2 summed here,
+// in registers, instead of by an autograd add kernel).
+template <typename T, int MASK, bool DUAL>
+__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                               const T* __restrict__ x, const T* __restrict__ y,
+                                                               int64_t M, int C, int64_t rows_per,
+                                                               const float* __restrict__ mean,
                                                                const float* __restrict__ ss,
                                                                float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -269,6 +272,12 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
   for (int64_t r = r0 + ty; r < r1; r += TY) {
     float g[8], a[8];
     Vec8<T>::ld(dy + r * C + c0, g);
+    if (DUAL) {
+      float g2[8];
+      Vec8<T>::ld(dy2 + r * C + c0, g2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] += g2[j];
+    }
     Vec8<T>::ld(x + r * C + c0, a);
     if (MASK == 1) {
       float o[8];
@@ -341,8 +350,9 @@ __global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(const float* __rest
   coef[2 * C + c] = -g * inv * sd * invM;              // k3
 }
 
-template <typename T, int MASK, bool DRES>
-__global__ __launch_bounds__(kBlock) void bn_bwd_elem_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+template <typename T, int MASK, bool DRES, bool DUAL>
+__global__ __launch_bounds__(kBlock) void bn_bwd_elem_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                             const T* __restrict__ x,
                                                              const T* __restrict__ y, T* __restrict__ dx,
                                                              T* __restrict__ dres, int64_t nvec, int C,
                                                              const float* __restrict__ mean,
@@ -356,6 +366,12 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_elem_kernel(const T* __restrict
     const int64_t e = v * 8;
     float g[8], a[8];
     Vec8<T>::ld(dy + e, g);
+    if (DUAL) {
+      float g2[8];
+      Vec8<T>::ld(dy2 + e, g2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] += g2[j];
+    }
     Vec8<T>::ld(x + e, a);
     if (MASK == 1) {
       float o[8];
@@ -490,9 +506,12 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
 std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x, const c10::optional<at::Tensor>& y,
                                     const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
                                     const at::Tensor& invstd, const c10::optional<at::Tensor>& ss, bool relu,
-                                    bool need_dres, bool need_dweight) {
+                                    bool need_dres, bool need_dweight, const c10::optional<at::Tensor>& dy2_in) {
   check_nhwc(x);
   auto dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  const bool dual = dy2_in.has_value() && dy2_in->defined();
+  at::Tensor dy2 = dual ? dy2_in->contiguous(at::MemoryFormat::ChannelsLast) : at::Tensor();
+  if (dual) TORCH_CHECK(dy2.sizes() == x.sizes() && dy2.scalar_type() == x.scalar_type(), "dy2 must match x");
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "dy must match x");
   const bool have_y = y.has_value() && y->defined();
   const bool have_ss = ss.has_value() && ss->defined();
@@ -518,10 +537,21 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
       const T* yp = mask == 1 ? reinterpret_cast<const T*>(y->data_ptr()) : nullptr;
       const float* ssp = mask == 2 ? ss->data_ptr<float>() : nullptr;
       const size_t lds = (size_t)kBlock * 8 * 2 * sizeof(float);
-      auto red = mask == 1 ? bn_bwd_reduce_kernel<T, 1> : (mask == 2 ? bn_bwd_reduce_kernel<T, 2> : bn_bwd_reduce_kernel<T, 0>);
-      hipLaunchKernelGGL(red, dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds, stream,
-                         reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(x.data_ptr()), yp, M,
-                         (int)C, g.rows_per, mean.data_ptr<float>(), ssp, part.data_ptr<float>());
+      const T* d2p = dual ? reinterpret_cast<const T*>(dy2.data_ptr()) : nullptr;
+      auto launch_red = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds, stream,
+                           reinterpret_cast<const T*>(dy.data_ptr()), d2p, reinterpret_cast<const T*>(x.data_ptr()),
+                           yp, M, (int)C, g.rows_per, mean.data_ptr<float>(), ssp, part.data_ptr<float>());
+      };
+      if (dual) {
+        if (mask == 1) launch_red(bn_bwd_reduce_kernel<T, 1, true>);
+        else if (mask == 2) launch_red(bn_bwd_reduce_kernel<T, 2, true>);
+        else launch_red(bn_bwd_reduce_kernel<T, 0, true>);
+      } else {
+        if (mask == 1) launch_red(bn_bwd_reduce_kernel<T, 1, false>);
+        else if (mask == 2) launch_red(bn_bwd_reduce_kernel<T, 2, false>);
+        else launch_red(bn_bwd_reduce_kernel<T, 0, false>);
+      }
       XDDP_HIP_CHECK(hipGetLastError());
       hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(64), 0, stream,
                          part.data_ptr<float>(), g.rblocks, (int)C, M,
@@ -532,14 +562,17 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
       const int64_t nvec = M * C / 8;
       auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
-                           reinterpret_cast<const T*>(dy.data_ptr()), reinterpret_cast<const T*>(x.data_ptr()), yp,
-                           reinterpret_cast<T*>(dx.data_ptr()),
+                           reinterpret_cast<const T*>(dy.data_ptr()), d2p, reinterpret_cast<const T*>(x.data_ptr()),
+                           yp, reinterpret_cast<T*>(dx.data_ptr()),
                            need_dres ? reinterpret_cast<T*>(dres.data_ptr()) : nullptr, nvec, (int)C,
                            mean.data_ptr<float>(), coef.data_ptr<float>(), ssp);
       };
-      if (mask == 1) { if (need_dres) launch(bn_bwd_elem_kernel<T, 1, true>); else launch(bn_bwd_elem_kernel<T, 1, false>); }
-      else if (mask == 2) { if (need_dres) launch(bn_bwd_elem_kernel<T, 2, true>); else launch(bn_bwd_elem_kernel<T, 2, false>); }
-      else { if (need_dres) launch(bn_bwd_elem_kernel<T, 0, true>); else launch(bn_bwd_elem_kernel<T, 0, false>); }
+#define XDDP_BN_ELEM(MK, DR)                                                              \
+  if (dual) launch(bn_bwd_elem_kernel<T, MK, DR, true>); else launch(bn_bwd_elem_kernel<T, MK, DR, false>)
+      if (mask == 1) { if (need_dres) { XDDP_BN_ELEM(1, true); } else { XDDP_BN_ELEM(1, false); } }
+      else if (mask == 2) { if (need_dres) { XDDP_BN_ELEM(2, true); } else { XDDP_BN_ELEM(2, false); } }
+      else { if (need_dres) { XDDP_BN_ELEM(0, true); } else { XDDP_BN_ELEM(0, false); } }
+#undef XDDP_BN_ELEM
       XDDP_HIP_CHECK(hipGetLastError());
     });
   });

@@ -18,7 +18,7 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
 std::vector<at::Tensor> bn_backward(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& y,
                                     const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
                                     const at::Tensor& invstd, const c10::optional<at::Tensor>& ss, bool relu,
-                                    bool need_dres, bool need_dweight);
+                                    bool need_dres, bool need_dweight, const c10::optional<at::Tensor>& dy2);
 std::vector<at::Tensor> ln_forward(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
                                    const c10::optional<at::Tensor>& beta, double eps, bool rms);
 std::vector<at::Tensor> ln_backward(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
@@ -27,7 +27,7 @@ std::vector<at::Tensor> ln_backward(const at::Tensor& dy, const at::Tensor& x, c
 
 std::vector<at::Tensor> maxpool_forward(const at::Tensor& x, int64_t k, int64_t stride, int64_t pad);
 at::Tensor maxpool_backward(const at::Tensor& dy, const at::Tensor& idx, const at::Tensor& x_like, int64_t k,
-                            int64_t stride, int64_t pad);
+                            int64_t stride, int64_t pad, const c10::optional<at::Tensor>& dy2);
 
 void bind_norm_kernels(pybind11::module_& m);
 

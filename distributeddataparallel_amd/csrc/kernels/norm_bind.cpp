@@ -12,10 +12,11 @@ void bind_norm_kernels(py::module_& m) {
         py::arg("running_var"), py::arg("num_batches_tracked"), py::arg("training"), py::arg("momentum"),
         py::arg("cumulative"), py::arg("eps"), py::arg("residual"), py::arg("relu"));
   m.def("bn_backward", &bn_backward, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("weight"), py::arg("mean"),
-        py::arg("invstd"), py::arg("scale_shift"), py::arg("relu"), py::arg("need_dres"), py::arg("need_dweight"));
+        py::arg("invstd"), py::arg("scale_shift"), py::arg("relu"), py::arg("need_dres"), py::arg("need_dweight"),
+        py::arg("dy2") = py::none());
   m.def("maxpool_forward", &maxpool_forward, py::arg("x"), py::arg("kernel"), py::arg("stride"), py::arg("pad"));
   m.def("maxpool_backward", &maxpool_backward, py::arg("dy"), py::arg("idx"), py::arg("x_like"), py::arg("kernel"),
-        py::arg("stride"), py::arg("pad"));
+        py::arg("stride"), py::arg("pad"), py::arg("dy2") = py::none());
   m.def("ln_forward", &ln_forward, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("rms"));
   m.def("ln_backward", &ln_backward, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
         py::arg("rms"), py::arg("need_dgamma"), py::arg("need_dbeta"));

@@ -71,7 +71,8 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                          const uint8_t* __restrict__ idx,
                                                           T* __restrict__ dx, int N, int H, int W, int C, int OH,
                                                           int OW, int k, int s, int p) {
   const int cv = C / 8;
@@ -99,6 +100,12 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
         const uint64_t packed = *reinterpret_cast<const uint64_t*>(idx + o);
         float g[8];
         Vec8<T>::ld(dy + o, g);
+        if (dy2) {  // second consumer of the pooled output (dual-output ResNet stem)
+          float g2[8];
+          Vec8<T>::ld(dy2 + o, g2);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] += g2[j];
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if ((int)((packed >> (8 * j)) & 0xff) == pos) acc[j] += g[j];
@@ -149,8 +156,10 @@ std::vector<at::Tensor> maxpool_forward(const at::Tensor& x, int64_t k, int64_t 
 }
 
 at::Tensor maxpool_backward(const at::Tensor& dy_in, const at::Tensor& idx, const at::Tensor& x_like, int64_t k,
-                            int64_t stride, int64_t pad) {
+                            int64_t stride, int64_t pad, const c10::optional<at::Tensor>& dy2_in) {
   auto dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  at::Tensor dy2 = (dy2_in.has_value() && dy2_in->defined()) ? dy2_in->contiguous(at::MemoryFormat::ChannelsLast)
+                                                              : at::Tensor();
   const int N = (int)x_like.size(0), C = (int)x_like.size(1), H = (int)x_like.size(2), W = (int)x_like.size(3);
   const int OH = (int)dy.size(2), OW = (int)dy.size(3);
   TORCH_CHECK(idx.numel() == dy.numel(), "maxpool backward: index/dy size mismatch");
@@ -161,7 +170,8 @@ at::Tensor maxpool_backward(const at::Tensor& dy_in, const at::Tensor& idx, cons
   dispatch_pool(dy.scalar_type(), [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL((maxpool_bwd_kernel<T>), dim3(grid_for(total)), dim3(256), 0, stream,
-                       reinterpret_cast<const T*>(dy.data_ptr()), idx.data_ptr<uint8_t>(),
+                       reinterpret_cast<const T*>(dy.data_ptr()),
+                       dy2.defined() ? reinterpret_cast<const T*>(dy2.data_ptr()) : nullptr, idx.data_ptr<uint8_t>(),
                        reinterpret_cast<T*>(dx.data_ptr()), N, H, W, C, OH, OW, (int)k, (int)stride, (int)pad);
     XDDP_HIP_CHECK(hipGetLastError());
   });

@@ -52,11 +52,12 @@ class BasicBlock(nn.Module):
         self._fused_add = getattr(self.bn2, "supports_add_relu", False)
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
+        x, xr = x if isinstance(x, tuple) else (x, x)  # (main, residual-path alias) from a fused producer
+        identity = xr if self.downsample is None else self.downsample(xr)
         out = self.act1(self.bn1(self.conv1(x)))
         out = self.conv2(out)
         if self._fused_add:
-            return self.bn2(out, residual=identity, relu=True)
+            return self.bn2(out, residual=identity, relu=True, dual_output=True)
         out = self.bn2(out)
         out += identity
         return self.relu(out)
@@ -82,12 +83,13 @@ class Bottleneck(nn.Module):
         self._fused_add = getattr(self.bn3, "supports_add_relu", False)
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
+        x, xr = x if isinstance(x, tuple) else (x, x)  # (main, residual-path alias) from a fused producer
+        identity = xr if self.downsample is None else self.downsample(xr)
         out = self.act1(self.bn1(self.conv1(x)))
         out = self.act2(self.bn2(self.conv2(out)))
         out = self.conv3(out)
         if self._fused_add:
-            return self.bn3(out, residual=identity, relu=True)
+            return self.bn3(out, residual=identity, relu=True, dual_output=True)
         out = self.bn3(out)
         out += identity
         return self.relu(out)
@@ -115,6 +117,8 @@ class ResNet(nn.Module):
         self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1, self.relu = _bn_relu(norm_layer, self.inplanes)
         self.maxpool = pool_layer(kernel_size=3, stride=2, padding=1)
+        if hasattr(self.maxpool, "dual_output"):
+            self.maxpool.dual_output = True
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
@@ -155,6 +159,8 @@ class ResNet(nn.Module):
         x = self.layer2(x)
         x = self.layer3(x)
         x = self.layer4(x)
+        if isinstance(x, tuple):  # fused blocks hand (output, alias) to the next block
+            x = x[0]
         x = self.avgpool(x)
         x = torch.flatten(x, 1)
         return self.fc(x)

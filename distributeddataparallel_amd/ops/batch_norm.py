@@ -22,8 +22,9 @@ __all__ = ["FusedBatchNorm2d", "batch_norm_act"]
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, residual, relu):
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, residual, relu, dual):
         C = load()
+        ctx.set_materialize_grads(False)
         y, mean, invstd, ss = C.bn_forward(x, weight, bias, running_mean, running_var, nbt, True, momentum, cma,
                                            eps, residual, relu)
         ctx.relu = relu
@@ -32,17 +33,26 @@ class _BNAct(torch.autograd.Function):
         # from x*scale+shift in the backward kernels (one fewer activation read)
         keep_y = relu and residual is not None
         ctx.save_for_backward(x, y if keep_y else None, weight, mean, invstd, ss)
+        if dual:
+            # two consumers (next block's conv and its residual) get separate autograd outputs over
+            # the same memory, so their gradients reach backward() unsummed: the kernels add them
+            # in registers instead of an autograd add kernel over the whole activation
+            return y, y.view_as(y)
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dy2=None):
         C = load()
         x, y, weight, mean, invstd, ss = ctx.saved_tensors
+        if dy is None:
+            dy, dy2 = dy2, None
+        if dy is None:
+            return (None,) * 12
         need_dw = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         dx, dw, db, dres = C.bn_backward(dy, x, y, weight, mean, invstd, ss, ctx.relu,
-                                         ctx.has_res and ctx.needs_input_grad[9], need_dw)
+                                         ctx.has_res and ctx.needs_input_grad[9], need_dw, dy2)
         return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
-                None, None, None, None, None, None, dres if ctx.has_res else None, None)
+                None, None, None, None, None, None, dres if ctx.has_res else None, None, None)
 
 
 def _kernel_ok(x: torch.Tensor) -> bool:
@@ -53,20 +63,22 @@ def _kernel_ok(x: torch.Tensor) -> bool:
 
 
 def batch_norm_act(x, running_mean, running_var, weight=None, bias=None, training=True, momentum=0.1, eps=1e-5,
-                   num_batches_tracked=None, residual: Optional[torch.Tensor] = None, relu: bool = False):
-    """Functional fused BN(+add)(+ReLU). ``momentum=None`` means cumulative moving average."""
+                   num_batches_tracked=None, residual: Optional[torch.Tensor] = None, relu: bool = False,
+                   dual_output: bool = False):
+    """Functional fused BN(+add)(+ReLU). ``momentum=None`` means cumulative moving average.
+    ``dual_output=True`` returns ``(y, y_alias)`` for an output with two consumers."""
     use_kernel = _kernel_ok(x) and (residual is None or (residual.shape == x.shape and residual.dtype == x.dtype and
                                                          residual.is_contiguous(memory_format=torch.channels_last)))
     if use_kernel and training:
         cma = momentum is None
         return _BNAct.apply(x, weight, bias, running_mean, running_var, num_batches_tracked,
-                            0.0 if cma else float(momentum), cma, float(eps), residual, relu)
+                            0.0 if cma else float(momentum), cma, float(eps), residual, relu, dual_output)
     if use_kernel and not training and not (torch.is_grad_enabled() and (
             x.requires_grad or (weight is not None and weight.requires_grad))):
         C = load()
         y, _, _, _ = C.bn_forward(x, weight, bias, running_mean, running_var, None, False, 0.0, False, float(eps),
                                   residual, relu)
-        return y
+        return (y, y) if dual_output else y
     # reference path
     if training and num_batches_tracked is not None:
         num_batches_tracked.add_(1)
@@ -78,7 +90,7 @@ def batch_norm_act(x, running_mean, running_var, weight=None, bias=None, trainin
         y = y + residual
     if relu:
         y = F.relu(y)
-    return y
+    return (y, y) if dual_output else y
 
 
 class FusedBatchNorm2d(nn.BatchNorm2d):
@@ -92,7 +104,8 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
         super().__init__(num_features, eps, momentum, affine, track_running_stats, device, dtype)
         self.relu = False
 
-    def forward(self, x, residual: Optional[torch.Tensor] = None, relu: Optional[bool] = None):
+    def forward(self, x, residual: Optional[torch.Tensor] = None, relu: Optional[bool] = None,
+                dual_output: bool = False):
         self._check_input_dim(x)
         relu = self.relu if relu is None else relu
         training = self.training or not self.track_running_stats
@@ -100,7 +113,7 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         nbt = self.num_batches_tracked if (self.training and self.track_running_stats) else None
         return batch_norm_act(x, rm, rv, self.weight, self.bias, training, self.momentum, self.eps, nbt, residual,
-                              relu)
+                              relu, dual_output)
 
     def extra_repr(self):
         return super().extra_repr() + (", relu=True" if self.relu else "")
