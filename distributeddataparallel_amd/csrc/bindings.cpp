@@ -14,6 +14,10 @@
 namespace py = pybind11;
 using namespace xddp;
 
+namespace xddp {
+std::shared_ptr<Comm> make_py_comm(py::object impl, int rank, int size, const std::string& name);
+}
+
 namespace {
 
 at::ScalarType dtype_from_str(const std::string& s) {
@@ -174,6 +178,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                               std::chrono::milliseconds(static_cast<int64_t>(timeout_s * 1000)), high_priority);
       }, py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("timeout_s") = 600.0,
       py::arg("high_priority") = true, py::call_guard<py::gil_scoped_release>());
+  m.def("make_py_comm", &make_py_comm, py::arg("impl"), py::arg("rank"), py::arg("size"),
+        py::arg("name") = "torch");
   m.def("make_debug_comm", &make_debug_comm, py::arg("inner"), py::arg("fingerprint") = true,
         py::arg("nan_check") = false);
   m.def("rccl_version", &rccl_version);

@@ -127,7 +127,7 @@ class DistributedDataParallel(nn.Module, Joinable):
             raise NotImplementedError("device_mesh is not supported; pass process_group")
         if delay_all_reduce_named_params is not None or param_to_hook_all_reduce is not None:
             raise NotImplementedError("delay_all_reduce_named_params is not supported")
-        self.process_group = process_group if process_group is not None else xdist.get_default_group()
+        self.process_group = self._resolve_process_group(process_group)
         self.module = module
         self.dim = dim
         self.broadcast_buffers = broadcast_buffers
@@ -194,6 +194,25 @@ class DistributedDataParallel(nn.Module, Joinable):
             self._set_static_graph()
 
     # ----------------------------------------------------------------------------- setup
+    @staticmethod
+    def _resolve_process_group(process_group):
+        """xddp group, or a torch.distributed group (wrapped), or the default of either."""
+        if process_group is not None and not isinstance(process_group, xdist.ProcessGroup):
+            from ..distributed.torch_adapter import from_torch_process_group
+
+            return from_torch_process_group(process_group)
+        if process_group is not None:
+            return process_group
+        if xdist.is_initialized():
+            return xdist.get_default_group()
+        import torch.distributed as tdist
+
+        if tdist.is_available() and tdist.is_initialized():
+            from ..distributed.torch_adapter import from_torch_process_group
+
+            return from_torch_process_group(None)
+        return xdist.get_default_group()  # raises the "not initialized" error
+
     def _build_reducer(self):
         C = load()
         params = self._module_parameters
@@ -396,7 +415,7 @@ class DistributedDataParallel(nn.Module, Joinable):
         return attrs
 
     def __setstate__(self, state):
-        self.process_group = xdist.get_default_group()
+        self.process_group = self._resolve_process_group(None)
         super().__setstate__(state)
         self.__dict__.setdefault("require_forward_param_sync", True)
         self.__dict__.setdefault("require_backward_grad_sync", True)
@@ -406,7 +425,7 @@ class DistributedDataParallel(nn.Module, Joinable):
             self._set_static_graph()
 
     def _check_default_group(self):
-        if self.process_group is not xdist.get_default_group():
+        if xdist.is_initialized() and self.process_group is not xdist.get_default_group():
             raise RuntimeError("DDP pickling/unpickling are only supported when using DDP with the default process "
                                "group.")
 
