@@ -33,4 +33,6 @@ def load():
 
             _build.build()
             _C = importlib.import_module("distributeddataparallel_amd._C")
+        if os.environ.get("XDDP_NATIVE_BACKTRACE") == "1":
+            _C.install_crash_handler()
     return _C

@@ -15,6 +15,7 @@ namespace py = pybind11;
 using namespace xddp;
 
 namespace xddp {
+bool install_crash_handler();
 std::shared_ptr<Comm> make_py_comm(py::object impl, int rank, int size, const std::string& name);
 }
 
@@ -178,6 +179,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                               std::chrono::milliseconds(static_cast<int64_t>(timeout_s * 1000)), high_priority);
       }, py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("timeout_s") = 600.0,
       py::arg("high_priority") = true, py::call_guard<py::gil_scoped_release>());
+  m.def("install_crash_handler", &install_crash_handler,
+        "Print a native backtrace on fatal signals, then chain to the previous handler");
   m.def("make_py_comm", &make_py_comm, py::arg("impl"), py::arg("rank"), py::arg("size"),
         py::arg("name") = "torch");
   m.def("make_debug_comm", &make_debug_comm, py::arg("inner"), py::arg("fingerprint") = true,
@@ -270,6 +273,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mt_unpack", [](at::Tensor flat, const std::vector<int64_t>& offs, const std::vector<at::Tensor>& dst,
                         double scale) { kernels::mt_unpack(flat, offs, dst, scale, stream_of(flat)); },
         py::arg("flat"), py::arg("offsets"), py::arg("dst"), py::arg("scale") = 1.0);
+  m.def("mt_copy_bytes", [](const std::vector<at::Tensor>& src, const std::vector<at::Tensor>& dst) {
+        TORCH_CHECK(src.size() == dst.size(), "mt_copy_bytes: list length mismatch");
+        if (src.empty()) return;
+        std::vector<const void*> s;
+        std::vector<void*> d;
+        std::vector<int64_t> n;
+        for (size_t i = 0; i < src.size(); ++i) {
+          TORCH_CHECK(src[i].is_cuda() && dst[i].is_cuda(), "mt_copy_bytes expects device tensors");
+          TORCH_CHECK(src[i].is_non_overlapping_and_dense() && dst[i].is_non_overlapping_and_dense() &&
+                      src[i].nbytes() == dst[i].nbytes(), "mt_copy_bytes: dense tensors of equal byte size");
+          s.push_back(src[i].data_ptr());
+          d.push_back(dst[i].data_ptr());
+          n.push_back((int64_t)src[i].nbytes());
+        }
+        kernels::mt_copy_bytes(s, d, n, stream_of(dst[0]));
+      }, py::arg("src"), py::arg("dst"), "Bit-exact multi-tensor copy (any dtypes; byte sizes must match)");
   m.def("mt_l2norm", [](const std::vector<at::Tensor>& ts, at::Tensor out, double max_norm) {
         kernels::mt_l2norm(ts, out, max_norm, stream_of(out));
       }, py::arg("tensors"), py::arg("out"), py::arg("max_norm") = 0.0);

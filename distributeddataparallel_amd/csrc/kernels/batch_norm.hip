@@ -11,8 +11,8 @@
 //             → elementwise pass writing dx (and d(residual) when the add was fused).
 // Layout: rows = N·H·W, each row has C contiguous channels. A lane owns 8 consecutive
 // channels (16-byte bf16 loads); the block tiles TX lanes across channels × TY lanes down rows.
-// Per-thread partial sums are converted to (n, mean, M2) and merged with Chan's formula
-// (in LDS, then across row-blocks) so large N·H·W does not cancel catastrophically.
+// Forward statistics are sums of (x - K_c) with one shared per-channel shift K_c = x[0, c],
+// so partials add exactly like the backward's and large |mean|/std does not cancel.
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
@@ -56,21 +56,11 @@ Geo make_geo(int64_t M, int C) {
   return g;
 }
 
-__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
-  const float nn = n + nb;
-  if (nb == 0.f) return;
-  if (n == 0.f) {
-    n = nb; mean = meanb; m2 = m2b;
-    return;
-  }
-  const float d = meanb - mean;
-  const float f = nb / nn;
-  mean += d * f;
-  m2 += m2b + d * d * n * f;
-  n = nn;
-}
-
 // ---------------------------------------------------------------- forward stats
+// Common-shift sums: every lane subtracts K_c = x[row 0, c] (a sample of the same channel, so
+// |mean - K| is O(std) and sum/sumsq of (x - K) do not cancel even when |mean| >> std — guide
+// §5.4 rule 26; the large-offset case has its own test). Partials are then plain additive
+// (sum, sumsq) pairs: LDS tree and finalize are adds, no per-merge divisions.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ x, int64_t M, int C, int64_t rows_per,
                                                           float* __restrict__ part) {
@@ -79,16 +69,9 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
   const int c0 = (blockIdx.x * TX + tx) * 8;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per;
   const int64_t r1 = min(M, r0 + rows_per);
-  // shifted sums: K = the thread's first sample per channel, so sum/sumsq of (x-K) do not
-  // cancel when |mean| >> std (guide §5.4 rule 26: the large-offset case has its own test)
-  float s[8] = {0}, ss[8] = {0}, k[8] = {0};
-  int cnt = 0;
+  float s[8] = {0}, ss[8] = {0}, k[8];
+  Vec8<T>::ld(x + c0, k);
   int64_t r = r0 + ty;
-  if (r < r1) {
-    Vec8<T>::ld(x + r * C + c0, k);
-    cnt = 1;
-    r += TY;
-  }
   // 4 independent 16-B loads in flight per lane (memory-level parallelism), then the tail
   for (; r + 3 * TY < r1; r += 4 * TY) {
     float v0[8], v1[8], v2[8], v3[8];
@@ -102,7 +85,6 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
       s[j] += (d0 + d1) + (d2 + d3);
       ss[j] = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, ss[j]))));
     }
-    cnt += 4;
   }
   for (; r < r1; r += TY) {
     float v[8];
@@ -113,70 +95,81 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
       s[j] += d;
       ss[j] = fmaf(d, d, ss[j]);
     }
-    cnt++;
   }
-  // thread partials -> (n, mean, m2) in LDS: layout [ty][tx][8][3]
-  float* my = lds + ((ty * TX + tx) * 8) * 3;
-  const float n = (float)cnt;
+  // LDS layout [ty][tx][16]: 8 sums then 8 sums of squares, 16-B vector stores
+  float* my = lds + (ty * TX + tx) * 16;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float dm = cnt ? s[j] / n : 0.f;
-    my[j * 3 + 0] = n;
-    my[j * 3 + 1] = k[j] + dm;
-    my[j * 3 + 2] = cnt ? fmaxf(ss[j] - s[j] * dm, 0.f) : 0.f;
+    my[j] = s[j];
+    my[8 + j] = ss[j];
   }
   __syncthreads();
-  // tree-merge across ty
   for (int stride = TY / 2; stride > 0; stride >>= 1) {
     if (ty < stride) {
-      float* o = lds + (((ty + stride) * TX + tx) * 8) * 3;
+      const float* o = lds + ((ty + stride) * TX + tx) * 16;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) chan_merge(my[j * 3], my[j * 3 + 1], my[j * 3 + 2], o[j * 3], o[j * 3 + 1], o[j * 3 + 2]);
+      for (int j = 0; j < 16; ++j) my[j] += o[j];
     }
     __syncthreads();
   }
   if (ty == 0) {
-    float* dst = part + ((int64_t)blockIdx.y * C + c0) * 3;
+    float* dst = part + ((int64_t)blockIdx.y * C + c0) * 2;  // [rblock][c/8][16]
 #pragma unroll
-    for (int j = 0; j < 24; ++j) dst[j] = my[j];
+    for (int j = 0; j < 16; ++j) dst[j] = my[j];
   }
 }
 
-// One 64-lane wave per 8-channel vector: lanes stride over the <=512 row-block partials
-// (Chan-merging 8 independent channel chains per lane), then a 6-step shuffle butterfly merges
-// across lanes — no LDS, no barriers (this kernel is pure latency: ~C/8 waves on 256 CUs).
+// One 64-lane wave per 8-channel vector: lanes stride over the row-block partials (4 loads in
+// flight), then a 6-step xor-shuffle butterfly of plain adds — no LDS, no barriers.
 // Lane j < 8 finalizes channel cv*8+j (mean, invstd, running-stat EMA, scale/shift).
-template <typename W>
+template <typename T, typename W>
 __global__ __launch_bounds__(64) void bn_stats_finalize_kernel(
-    const float* __restrict__ part, int rblocks, int C, int64_t M, const W* __restrict__ weight,
-    const W* __restrict__ bias, W* running_mean, W* running_var, const int64_t* nbt, float momentum, bool cma,
-    float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale,
-    float* __restrict__ shift) {
+    const float* __restrict__ part, int rblocks, int C, int64_t M, const T* __restrict__ x,
+    const W* __restrict__ weight, const W* __restrict__ bias, W* running_mean, W* running_var,
+    const int64_t* nbt, float momentum, bool cma, float eps, float* __restrict__ mean_out,
+    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift) {
   const int cv = blockIdx.x, lane = threadIdx.x;
-  float n[8], mu[8], m2[8];
+  float a[16];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) n[j] = mu[j] = m2[j] = 0.f;
-  for (int b = lane; b < rblocks; b += 64) {
-    const float* p = part + ((int64_t)b * C + cv * 8) * 3;
+  for (int j = 0; j < 16; ++j) a[j] = 0.f;
+  const float* base = part + (int64_t)cv * 16;
+  const int64_t rstride = (int64_t)C * 2;
+  int b = lane;
+  for (; b + 192 < rblocks; b += 256) {
+    float4 q[4][4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) chan_merge(n[j], mu[j], m2[j], p[j * 3], p[j * 3 + 1], p[j * 3 + 2]);
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) q[u][v] = reinterpret_cast<const float4*>(base + (b + 64 * u) * rstride)[v];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        a[4 * v] += q[u][v].x; a[4 * v + 1] += q[u][v].y; a[4 * v + 2] += q[u][v].z; a[4 * v + 3] += q[u][v].w;
+      }
   }
+  for (; b < rblocks; b += 64) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float on = __shfl_xor(n[j], o, 64), om = __shfl_xor(mu[j], o, 64), o2 = __shfl_xor(m2[j], o, 64);
-      chan_merge(n[j], mu[j], m2[j], on, om, o2);
+    for (int v = 0; v < 4; ++v) {
+      const float4 q = reinterpret_cast<const float4*>(base + b * rstride)[v];
+      a[4 * v] += q.x; a[4 * v + 1] += q.y; a[4 * v + 2] += q.z; a[4 * v + 3] += q.w;
     }
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j] += __shfl_xor(a[j], o, 64);
   if (lane >= 8) return;
   // lane j picks channel j out of its (identical) registers without dynamic indexing
-  float cn = n[0], mean = mu[0], cm2 = m2[0];
+  float S = a[0], SS = a[8];
 #pragma unroll
   for (int j = 1; j < 8; ++j)
-    if (lane == j) { cn = n[j]; mean = mu[j]; cm2 = m2[j]; }
+    if (lane == j) { S = a[j]; SS = a[8 + j]; }
   const int c = cv * 8 + lane;
-  const float var = cm2 / fmaxf(cn, 1.f);
+  const float inv_m = 1.f / (float)M;
+  const float dm = S * inv_m;
+  const float var = fmaxf(SS * inv_m - dm * dm, 0.f);
+  const float mean = Elem<T, float>::ld(x, c) + dm;
   const float inv = rsqrtf(var + eps);
   mean_out[c] = mean;
   invstd_out[c] = inv;
@@ -465,13 +458,14 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
       if (training) {
         TORCH_CHECK(M > 0, "batch_norm on empty input");
         Geo g = make_geo(M, (int)C);
-        auto part = at::empty({(int64_t)g.rblocks, C, 3}, fopt);
-        const size_t lds = (size_t)kBlock * 8 * 3 * sizeof(float);
+        auto part = at::empty({(int64_t)g.rblocks, C, 2}, fopt);
+        const size_t lds = (size_t)kBlock * 16 * sizeof(float);
         hipLaunchKernelGGL((bn_stats_kernel<T>), dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds, stream,
                            reinterpret_cast<const T*>(x.data_ptr()), M, (int)C, g.rows_per, part.data_ptr<float>());
         XDDP_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL((bn_stats_finalize_kernel<W>), dim3(C / 8), dim3(64), 0, stream,
-                           part.data_ptr<float>(), g.rblocks, (int)C, M, opt_ptr<const W>(weight),
+        hipLaunchKernelGGL((bn_stats_finalize_kernel<T, W>), dim3(C / 8), dim3(64), 0, stream,
+                           part.data_ptr<float>(), g.rblocks, (int)C, M, reinterpret_cast<const T*>(x.data_ptr()),
+                           opt_ptr<const W>(weight),
                            opt_ptr<const W>(bias), opt_ptr<W>(running_mean), opt_ptr<W>(running_var),
                            (num_batches_tracked.has_value() && num_batches_tracked->defined())
                                ? num_batches_tracked->data_ptr<int64_t>() : nullptr,

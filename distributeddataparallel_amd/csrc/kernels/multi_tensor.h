@@ -20,6 +20,9 @@ void mt_scale_copy(const std::vector<at::Tensor>& src, const std::vector<at::Ten
                    const c10::optional<at::Tensor>& scale_tensor, hipStream_t stream);
 
 // Pack a list of dense tensors into consecutive slices of `flat` at `offsets` (elements) and back.
+// Raw byte copies (dtype-agnostic, bit-exact) of up to any number of (src, dst, nbytes) regions.
+void mt_copy_bytes(const std::vector<const void*>& src, const std::vector<void*>& dst,
+                   const std::vector<int64_t>& nbytes, hipStream_t stream);
 void mt_pack(const std::vector<at::Tensor>& src, const at::Tensor& flat, const std::vector<int64_t>& offsets,
              double scale, hipStream_t stream);
 void mt_unpack(const at::Tensor& flat, const std::vector<int64_t>& offsets, const std::vector<at::Tensor>& dst,

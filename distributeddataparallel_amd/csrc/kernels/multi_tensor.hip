@@ -137,6 +137,41 @@ struct DevType<at::Half> {
     default: TORCH_CHECK(false, "xddp multi-tensor: unsupported dtype ", st);  \
   }
 
+// ------------------------------------------------------------------------------------
+// byte-exact copy (any dtype, bit patterns preserved): "numel" is bytes; a block owns
+// kChunk bytes, 16 B per lane per iteration when both ends of the segment are aligned.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void copy_bytes_kernel(SegTable<2> t) {
+  const int s = find_seg(t, blockIdx.x);
+  const int64_t blk = blockIdx.x - (s ? t.blk_end[s - 1] : 0);
+  const char* __restrict__ src = reinterpret_cast<const char*>(t.ptr[0][s]);
+  char* __restrict__ dst = reinterpret_cast<char*>(t.ptr[1][s]);
+  const int64_t n = t.numel[s];
+  const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
+  constexpr int kIt = kChunk / (kThreads * 16);
+  const int64_t base = blk * kChunk;
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int64_t i = base + ((int64_t)it * kThreads + threadIdx.x) * 16;
+    if (vec && i + 16 <= n) {
+      *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(src + i);
+    } else {
+      for (int64_t k = i; k < i + 16 && k < n; ++k) dst[k] = src[k];
+    }
+  }
+}
+
+void mt_copy_bytes(const std::vector<const void*>& src, const std::vector<void*>& dst,
+                   const std::vector<int64_t>& nbytes, hipStream_t stream) {
+  TORCH_CHECK(src.size() == dst.size() && src.size() == nbytes.size(), "copy_bytes: list length mismatch");
+  std::vector<std::array<void*, 2>> ptrs;
+  for (size_t i = 0; i < src.size(); ++i) ptrs.push_back({const_cast<void*>(src[i]), dst[i]});
+  for_each_table<2>(ptrs, nbytes, [&](const SegTable<2>& t, int32_t nb) {
+    hipLaunchKernelGGL(copy_bytes_kernel, dim3(nb), dim3(kThreads), 0, stream, t);
+    XDDP_HIP_CHECK(hipGetLastError());
+  });
+}
+
 static void check_dense_pair(const at::Tensor& a, const at::Tensor& b) {
   TORCH_CHECK(a.numel() == b.numel(), "numel mismatch ", a.numel(), " vs ", b.numel());
   TORCH_CHECK(a.is_non_overlapping_and_dense() && b.is_non_overlapping_and_dense(),

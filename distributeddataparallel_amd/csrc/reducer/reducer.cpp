@@ -1,6 +1,8 @@
 // xddp Reducer implementation. See reducer.h for the contract and the MI355X design notes.
 #include "reducer/reducer.h"
 
+#include <cstring>
+
 #include <ATen/hip/HIPContext.h>
 #include <ATen/record_function.h>
 #include <c10/hip/HIPGuard.h>
@@ -804,52 +806,59 @@ void verify_params_across_processes(const std::shared_ptr<Comm>& comm, const std
 
 void broadcast_coalesced(const std::shared_ptr<Comm>& comm, std::vector<at::Tensor> tensors, int64_t buffer_bytes,
                          int src) {
+  // All dtypes travel in ONE byte buffer per <= buffer_bytes chunk (each tensor 16-B aligned
+  // inside it): DDP's per-forward BN-buffer sync is one latency-bound broadcast instead of one
+  // per dtype. Pack/unpack are single byte-exact multi-tensor kernels on the GPU.
   if (tensors.empty() || comm->size() == 1) return;
-  // group consecutive-by-dtype chunks of <= buffer_bytes, preserving order within each dtype
-  std::map<at::ScalarType, std::vector<at::Tensor>> by_dtype;
-  std::vector<at::ScalarType> order;
-  for (auto& t : tensors) {
-    if (!by_dtype.count(t.scalar_type())) order.push_back(t.scalar_type());
-    by_dtype[t.scalar_type()].push_back(t);
-  }
-  for (auto dt : order) {
-    auto& list = by_dtype[dt];
-    size_t i = 0;
-    while (i < list.size()) {
-      std::vector<at::Tensor> chunk;
-      std::vector<int64_t> offs;
-      int64_t bytes = 0, elems = 0;
-      while (i < list.size() && (chunk.empty() || bytes + list[i].nbytes() <= static_cast<size_t>(buffer_bytes))) {
-        chunk.push_back(list[i]);
-        offs.push_back(elems);
-        elems = round_up(elems + list[i].numel(), kPad);
-        bytes += list[i].nbytes();
-        ++i;
-      }
-      auto dev = chunk[0].device();
-      auto flat = at::empty({std::max<int64_t>(elems, 1)}, chunk[0].options().requires_grad(false));
-      const bool gpu = dev.is_cuda();
-      bool all_dense = true;
-      for (auto& c : chunk) all_dense = all_dense && c.is_non_overlapping_and_dense();
-      if (comm->rank() == src) {
-        if (gpu && all_dense) {
-          kernels::mt_pack(chunk, flat, offs, 1.0, c10::hip::getCurrentHIPStream(dev.index()).stream());
-        } else {
-          for (size_t k = 0; k < chunk.size(); ++k)
-            flat.narrow(0, offs[k], chunk[k].numel()).copy_(chunk[k].reshape(-1));
+  size_t i = 0;
+  while (i < tensors.size()) {
+    std::vector<at::Tensor> chunk, staged;
+    std::vector<int64_t> offs;
+    int64_t bytes = 0;
+    while (i < tensors.size() && (chunk.empty() || bytes + (int64_t)tensors[i].nbytes() <= buffer_bytes)) {
+      const auto& t = tensors[i];
+      TORCH_CHECK(t.device() == tensors[0].device(), "broadcast_coalesced: tensors on different devices");
+      chunk.push_back(t);
+      staged.push_back(t.is_non_overlapping_and_dense() ? t : t.contiguous());
+      offs.push_back(bytes);
+      bytes = round_up(bytes + (int64_t)t.nbytes(), 16);
+      ++i;
+    }
+    const auto dev = chunk[0].device();
+    auto flat = at::empty({std::max<int64_t>(bytes, 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
+    auto* base = static_cast<char*>(flat.data_ptr());
+    const bool gpu = dev.is_cuda();
+    std::vector<int64_t> nb;
+    for (auto& t : staged) nb.push_back((int64_t)t.nbytes());
+    if (comm->rank() == src) {
+      if (gpu) {
+        std::vector<const void*> s;
+        std::vector<void*> d;
+        for (size_t k = 0; k < staged.size(); ++k) {
+          s.push_back(staged[k].data_ptr());
+          d.push_back(base + offs[k]);
         }
+        kernels::mt_copy_bytes(s, d, nb, c10::hip::getCurrentHIPStream(dev.index()).stream());
+      } else {
+        for (size_t k = 0; k < staged.size(); ++k) std::memcpy(base + offs[k], staged[k].data_ptr(), nb[k]);
       }
-      comm->broadcast(flat, src)->wait();
-      if (comm->rank() != src) {
-        if (gpu && all_dense) {
-          kernels::mt_unpack(flat, offs, chunk, 1.0, c10::hip::getCurrentHIPStream(dev.index()).stream());
-        } else {
-          for (size_t k = 0; k < chunk.size(); ++k) {
-            at::NoGradGuard ng;
-            chunk[k].copy_(flat.narrow(0, offs[k], chunk[k].numel()).view(chunk[k].sizes()));
-          }
+    }
+    comm->broadcast(flat, src)->wait();
+    if (comm->rank() != src) {
+      if (gpu) {
+        std::vector<const void*> s;
+        std::vector<void*> d;
+        for (size_t k = 0; k < staged.size(); ++k) {
+          s.push_back(base + offs[k]);
+          d.push_back(staged[k].data_ptr());
         }
+        kernels::mt_copy_bytes(s, d, nb, c10::hip::getCurrentHIPStream(dev.index()).stream());
+      } else {
+        for (size_t k = 0; k < staged.size(); ++k) std::memcpy(staged[k].data_ptr(), base + offs[k], nb[k]);
       }
+      at::NoGradGuard ng;
+      for (size_t k = 0; k < chunk.size(); ++k)
+        if (!staged[k].is_same(chunk[k])) chunk[k].copy_(staged[k]);
     }
   }
 }

@@ -59,6 +59,20 @@ def test_pack_unpack_roundtrip():
         torch.testing.assert_close(a, b)
 
 
+def test_copy_bytes_bit_exact_mixed_dtypes():
+    C = load()
+    g = torch.Generator(device=DEV).manual_seed(0)
+    raw = torch.randint(-2**62, 2**62, (4097,), device=DEV, dtype=torch.int64, generator=g)
+    src = [raw[:1], raw[1:9].view(torch.float64), raw[:100].view(torch.float32)[1:33],  # 4-B aligned only
+           raw[:50].view(torch.bfloat16)[3:101], raw.view(torch.uint8)[5:20000],  # odd byte offsets
+           torch.full((3,), float("nan"), device=DEV, dtype=torch.bfloat16)]
+    dst = [torch.empty_like(t) for t in src]
+    C.mt_copy_bytes(src, dst)
+    for a, b in zip(src, dst):
+        assert torch.equal(a.view(torch.uint8) if a.dtype != torch.uint8 else a,
+                           b.view(torch.uint8) if b.dtype != torch.uint8 else b)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_l2norm_and_clip(dt):
     C = load()
