@@ -16,6 +16,7 @@ using namespace xddp;
 
 namespace xddp {
 bool install_crash_handler();
+std::shared_ptr<Store> make_file_store(const std::string& path, int world_size);
 std::shared_ptr<Comm> make_py_comm(py::object impl, int rank, int size, const std::string& name);
 }
 
@@ -112,6 +113,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("underlying_store", &PrefixStore::base);
 
   py::class_<HashStore, Store, std::shared_ptr<HashStore>>(m, "HashStore").def(py::init<>());
+
+  m.def("FileStore", [](const std::string& path, int world_size, double timeout_s) {
+        auto s = make_file_store(path, world_size);
+        s->timeout = std::chrono::milliseconds(static_cast<int64_t>(timeout_s * 1000));
+        return s;
+      }, py::arg("path"), py::arg("world_size") = -1, py::arg("timeout_s") = 1800.0,
+      "File-backed store on a shared filesystem (file:// rendezvous)");
 
   py::register_exception<StoreTimeout>(m, "StoreTimeout", PyExc_TimeoutError);
 
@@ -253,7 +261,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("runtime_stats", &Reducer::runtime_stats)
       .def("construction_data", &Reducer::construction_data)
       .def("native_launches", &Reducer::native_launches)
-      .def("remove_autograd_hooks", &Reducer::remove_autograd_hooks);
+      .def("remove_autograd_hooks", &Reducer::remove_autograd_hooks)
+      .def("reinstall_hooks", [](Reducer& r) {
+            r.remove_autograd_hooks();
+            r.install_hooks();
+          },
+          "Drop and re-acquire the parameters' AccumulateGrad nodes (recreated on the current stream "
+          "once nothing else holds them) and re-register the hooks");
 
   m.def("compute_bucket_assignment_by_size", &compute_bucket_assignment_by_size, py::arg("tensors"),
         py::arg("limits"), py::arg("expect_sparse") = std::vector<bool>{},

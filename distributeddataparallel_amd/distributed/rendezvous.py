@@ -8,6 +8,9 @@ chosen by the launcher (or 29500).
 Under ``torchrun`` the elastic agent already owns a store on MASTER_PORT. Then rank 0 starts
 the xddp store on an ephemeral port and publishes its address through the agent's store, so
 the two never fight over the port.
+
+``file:///path`` uses the native FileStore (an flock-guarded append-only log on a shared
+filesystem); rank/world_size come from the query string or the arguments.
 """
 from __future__ import annotations
 
@@ -80,8 +83,18 @@ def rendezvous(init_method: str | None, rank: int, world_size: int, timeout: tim
         if world_size <= 0:
             world_size = int(q.get("world_size", [1])[0])
         host, port = url.hostname or "127.0.0.1", int(url.port or DEFAULT_MASTER_PORT)
+    elif url.scheme == "file":
+        q = parse_qs(url.query)
+        if rank < 0:
+            rank = int(q.get("rank", [os.environ.get("RANK", 0)])[0])
+        if world_size <= 0:
+            world_size = int(q.get("world_size", [os.environ.get("WORLD_SIZE", 1)])[0])
+        if rank < 0 or world_size <= 0 or rank >= world_size:
+            raise ValueError(f"invalid rank/world_size: {rank}/{world_size}")
+        store = C.FileStore(url.path, world_size, timeout.total_seconds())
+        return store, rank, world_size, os.environ.get("MASTER_ADDR", "127.0.0.1")
     else:
-        raise ValueError(f"unsupported init_method {init_method!r} (use env:// or tcp://host:port)")
+        raise ValueError(f"unsupported init_method {init_method!r} (use env://, tcp://host:port or file:///path)")
     if rank < 0 or world_size <= 0 or rank >= world_size:
         raise ValueError(f"invalid rank/world_size: {rank}/{world_size}")
     store = C.TCPStore(host, port, rank == 0, world_size, timeout.total_seconds(), False)

@@ -234,6 +234,22 @@ class DistributedDataParallel(nn.Module, Joinable):
             param_names=self._param_names,
         )
 
+    def _rebind_grad_accumulators(self, stream=None):
+        """Re-create the AccumulateGrad nodes the Reducer hooks on under ``stream``.
+
+        Autograd runs an AccumulateGrad node on the stream current when the node was created —
+        for DDP that is the stream at construction time. A step captured into a HIP graph on a
+        side stream must not touch another stream, so the graph helper rebinds the nodes to the
+        capture stream first (call with no live autograd graph referencing the parameters)."""
+        import gc
+
+        gc.collect()
+        if stream is None or self.device_type != "cuda":
+            self.reducer.reinstall_hooks()
+            return
+        with torch.cuda.stream(stream):
+            self.reducer.reinstall_hooks()
+
     def _sync_module_states(self, src: int = 0):
         C = load()
         tensors = [p.detach() for p in self.module.parameters()] + [b for b in self._buffers_list]

@@ -33,6 +33,10 @@ class GraphedTrainStep:
         torch.backends.cudnn.benchmark = True
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
+        if hasattr(model, "_rebind_grad_accumulators"):
+            # AccumulateGrad nodes created at DDP construction run on the construction stream;
+            # re-create them on the capture stream so backward stays inside the capture
+            model._rebind_grad_accumulators(side)
         with torch.cuda.stream(side):
             for _ in range(max(2, warmup_steps)):  # >=2: bucket rebuild happens in iteration 1
                 optimizer.zero_grad(set_to_none=set_to_none)

@@ -16,6 +16,8 @@ def try_capture(name, make, bench):
     try:
         model, x, lossf = make()
         s = torch.cuda.Stream(); s.wait_stream(torch.cuda.current_stream())
+        if hasattr(model, "_rebind_grad_accumulators"):
+            model._rebind_grad_accumulators(s)
         with torch.cuda.stream(s):
             for _ in range(3):
                 model.zero_grad(set_to_none=True)

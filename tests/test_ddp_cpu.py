@@ -42,7 +42,7 @@ def _shard(t, rank, world):
 
 
 # --------------------------------------------------------------------------------------------
-def _w_parity(rank, world, grad_as_view, bucket_cap):
+def _w_parity(rank, world, grad_as_view, bucket_cap, rebind=False):
     import distributeddataparallel_amd as xddp
 
     tdist = _torch_pg(rank, world)
@@ -51,10 +51,12 @@ def _w_parity(rank, world, grad_as_view, bucket_cap):
     ddp = xddp.DDP(m1, gradient_as_bucket_view=grad_as_view, bucket_cap_mb=bucket_cap)
     tddp = torch.nn.parallel.DistributedDataParallel(m2, gradient_as_bucket_view=grad_as_view)
     opts = [torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9) for m in (m1, m2, base)]
-    for x, y in _batches(world, 5):
+    for it, (x, y) in enumerate(_batches(world, 5)):
         xs, ys = _shard(x, rank, world), _shard(y, rank, world)
         for o in opts:
             o.zero_grad()
+        if rebind and it == 2:
+            ddp._rebind_grad_accumulators()  # what the HIP-graph helper does before capture
         F.cross_entropy(ddp(xs), ys).backward()
         F.cross_entropy(tddp(xs), ys).backward()
         F.cross_entropy(base(x), y).backward()
@@ -81,6 +83,10 @@ def test_parity_mlp_w2(grad_as_view):
 
 def test_parity_w3_small_buckets():
     run_ranks(_w_parity, world=3, args=(False, 0.01))
+
+
+def test_parity_after_rebinding_grad_accumulators():
+    run_ranks(_w_parity, world=2, args=(True, 0.01, True))
 
 
 # --------------------------------------------------------------------------------------------

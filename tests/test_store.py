@@ -63,3 +63,47 @@ def test_many_clients_concurrent_add():
     [t.start() for t in ts]
     [t.join() for t in ts]
     assert s.add("ctr", 0) == 400
+
+
+def test_file_store_semantics_and_cleanup(tmp_path):
+    C = load()
+    path = str(tmp_path / "fs")
+    a = C.FileStore(path, 2, 10.0)
+    b = C.FileStore(path, 2, 10.0)  # second handle = another process on the shared file
+    a.set("k", "v")
+    assert b.get("k") == b"v"
+    assert a.add("n", 3) == 3 and b.add("n", 4) == 7
+    assert b.compare_set("k", "v", "w") == b"w" and a.compare_set("k", "zz", "q") == b"w"
+    b.append("k", "!")
+    assert a.get("k") == b"w!"
+    assert a.delete_key("k") and not b.check(["k"])
+    assert a.num_keys() == 1
+    threading.Timer(0.2, lambda: a.set("late", "1")).start()
+    assert b.get("late") == b"1"
+    b.timeout_s = 0.2
+    with pytest.raises(TimeoutError):
+        b.get("never")
+    del a
+    import os
+
+    assert os.path.exists(path)
+    del b  # last handle removes the file
+    assert not os.path.exists(path)
+
+
+def _file_rdzv_worker(rank, world, path):
+    import torch
+
+    from distributeddataparallel_amd import distributed as xdist
+
+    xdist.init_process_group("cpu", init_method=f"file://{path}", rank=rank, world_size=world)
+    t = torch.full((4,), float(rank + 1))
+    xdist.all_reduce(t)
+    assert torch.equal(t, torch.full((4,), float(sum(range(1, world + 1)))))
+    xdist.destroy_process_group()
+
+
+def test_file_rendezvous_multiprocess(tmp_path):
+    from distributeddataparallel_amd.utils.spawn import spawn
+
+    spawn(_file_rdzv_worker, args=(3, str(tmp_path / "rdzv")), nprocs=3, env={"OMP_NUM_THREADS": "1"})
