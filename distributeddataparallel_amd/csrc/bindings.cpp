@@ -174,7 +174,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         }
         return out;
       })
-      .def("num_collectives", [](Comm& c) { return c.flight().count(); });
+      .def("num_collectives", [](Comm& c) { return c.flight().count(); })
+      .def("flight_json", [](Comm& c, const std::string& reason) {
+            return c.flight().to_json(c.rank(), c.backend(), reason);
+          }, py::arg("reason") = "on demand")
+      .def("dump_flight", &Comm::dump_flight, py::arg("reason") = "on demand", py::arg("force") = true,
+           "Write the flight record JSON to $XDDP_FLIGHT_DUMP_PREFIX<rank>.json; returns the path");
 
   m.def("make_cpu_comm", [](std::shared_ptr<Store> store, int rank, int size, double timeout_s, const std::string& host) {
         return make_tcp_comm_host(std::move(store), rank, size,

@@ -76,6 +76,8 @@ class FlightRecorder {
     std::lock_guard<std::mutex> g(mu_);
     return std::vector<FlightEntry>(ring_.begin(), ring_.end());
   }
+  // JSON document of the ring (newest last), for post-mortem desync/timeout triage.
+  std::string to_json(int rank, const std::string& backend, const std::string& reason);
   int64_t count() const { return next_; }
 
  private:
@@ -111,6 +113,10 @@ class Comm : public std::enable_shared_from_this<Comm> {
   virtual void shutdown() {}
 
   virtual FlightRecorder& flight() { return flight_; }
+  // Writes the flight record to $XDDP_FLIGHT_DUMP_PREFIX<rank>.json (default
+  // /tmp/xddp_flight_rank_<rank>.json) unless XDDP_FLIGHT_DUMP_ON_ERROR=0 and !force;
+  // returns the path ("" if skipped). Called by the backends on timeout / comm error.
+  std::string dump_flight(const std::string& reason, bool force = false);
   // Debug: TORCH_DISTRIBUTED_DEBUG=DETAIL-style fingerprint check before each collective.
   bool debug_fingerprint = false;
 

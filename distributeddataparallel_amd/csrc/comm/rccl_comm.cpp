@@ -10,13 +10,19 @@
 //    caller's current stream wait on it (no host block);
 //  * ncclGroupStart/End coalescing for bucket bursts;
 //  * a watchdog thread polls in-flight events + ncclCommGetAsyncError and aborts the
-//    communicator on timeout/error so a hung peer surfaces as an exception, not a hang.
+//    communicator on timeout/error so a hung peer surfaces as an exception, not a hang;
+//    on error it dumps the flight record and posts the error to the store, and while a
+//    collective is overdue (>1 s) it polls the store for errors posted by peers, so every
+//    rank fails fast instead of each waiting out its own timeout;
+//  * a heartbeat monitor thread aborts the process (after a flight dump) if the watchdog
+//    itself stops ticking, e.g. stuck inside a driver call (XDDP_HEARTBEAT_TIMEOUT_SEC).
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <list>
@@ -120,7 +126,8 @@ class RcclWork : public Work {
   void check_error() {
     int e = err_->load();
     TORCH_CHECK(e == 0, "xddp rccl: communicator is in error state (",
-                e == 1 ? "collective timed out; watchdog aborted the communicator" : "asynchronous RCCL error",
+                e == 1 ? "collective timed out; watchdog aborted the communicator"
+                       : (e == 3 ? "a peer rank reported a communicator error" : "asynchronous RCCL error"),
                 ")");
   }
   hipEvent_t ev;
@@ -138,6 +145,7 @@ class RcclComm : public Comm {
   RcclComm(std::shared_ptr<Store> store, int rank, int size, int device, std::chrono::milliseconds timeout,
            bool high_priority)
       : Comm(rank, size),
+        store_(store),
         device_(device),
         timeout_(timeout),
         stream_(c10::hip::getStreamFromPool(high_priority, static_cast<c10::DeviceIndex>(device))),
@@ -154,7 +162,11 @@ class RcclComm : public Comm {
       std::memcpy(&id, s.data(), sizeof(id));
     }
     XDDP_NCCL_CHECK(ncclCommInitRank(&comm_, size, id, rank));
+    heartbeat_ = now_ns();
     watchdog_ = std::thread([this] { watchdog_loop(); });
+    const char* hb = std::getenv("XDDP_HEARTBEAT_TIMEOUT_SEC");
+    hb_timeout_s_ = hb ? std::atof(hb) : 480.0;
+    if (hb_timeout_s_ > 0) monitor_ = std::thread([this] { monitor_loop(); });
   }
 
   ~RcclComm() override {
@@ -346,12 +358,16 @@ class RcclComm : public Comm {
   }
 
   void watchdog_loop() {
+    std::string reason;
+    int64_t last_peer_poll = 0;
     while (!wd_stop_) {
+      heartbeat_ = now_ns();
       {
         std::unique_lock<std::mutex> g(wd_mu_);
         wd_cv_.wait_for(g, std::chrono::milliseconds(100), [&] { return wd_stop_.load(); });
         if (wd_stop_) break;
         const int64_t now = now_ns();
+        int64_t oldest = now;
         for (auto it = inflight_.begin(); it != inflight_.end();) {
           hipError_t q = hipEventQuery((*it)->ev);
           if (q == hipSuccess) {
@@ -359,32 +375,75 @@ class RcclComm : public Comm {
             it = inflight_.erase(it);
           } else if (now - (*it)->t_start > static_cast<int64_t>(timeout_.count()) * 1000000LL) {
             flight_.finish((*it)->seq, "timeout");
-            std::cerr << "[xddp rank " << rank_ << "] watchdog: collective seq " << (*it)->seq
-                      << " exceeded timeout of " << timeout_.count() << " ms; aborting communicator\n";
+            reason = "collective seq " + std::to_string((*it)->seq) + " exceeded timeout of " +
+                     std::to_string(timeout_.count()) + " ms";
+            std::cerr << "[xddp rank " << rank_ << "] watchdog: " << reason << "; aborting communicator\n";
             err_->store(1);
             it = inflight_.erase(it);
           } else {
+            oldest = std::min(oldest, (*it)->t_start);
             ++it;
+          }
+        }
+        // a healthy step never has a collective in flight for a second: only then ask the
+        // store whether a peer has already failed
+        if (err_->load() == 0 && now - oldest > 1000000000LL && now - last_peer_poll > 1000000000LL) {
+          last_peer_poll = now;
+          try {
+            if (store_->check({"rccl/error"})) {
+              reason = "peer error: " + store_->get("rccl/error");
+              std::cerr << "[xddp rank " << rank_ << "] watchdog: " << reason << "; aborting communicator\n";
+              err_->store(3);
+            }
+          } catch (...) {
           }
         }
       }
       if (err_->load() == 0 && comm_ && !aborted_ && !destroyed_) {
         ncclResult_t ae = ncclSuccess;
         if (ncclCommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
-          std::cerr << "[xddp rank " << rank_ << "] watchdog: async RCCL error " << ncclGetErrorString(ae) << "\n";
+          reason = std::string("async RCCL error ") + ncclGetErrorString(ae);
+          std::cerr << "[xddp rank " << rank_ << "] watchdog: " << reason << "\n";
           err_->store(2);
         }
       }
-      if (err_->load() != 0) abort();
+      if (err_->load() != 0 && !aborted_) {
+        dump_flight(reason);
+        if (err_->load() != 3) {
+          try {
+            store_->set("rccl/error", "rank " + std::to_string(rank_) + ": " + reason);
+          } catch (...) {
+          }
+        }
+        abort();
+      }
+    }
+  }
+
+  void monitor_loop() {
+    std::unique_lock<std::mutex> g(hb_mu_);
+    while (!wd_stop_) {
+      hb_cv_.wait_for(g, std::chrono::seconds(1), [&] { return wd_stop_.load(); });
+      if (wd_stop_) break;
+      const double idle_s = (now_ns() - heartbeat_.load()) * 1e-9;
+      if (idle_s > hb_timeout_s_) {
+        std::cerr << "[xddp rank " << rank_ << "] heartbeat monitor: watchdog silent for " << idle_s
+                  << " s (XDDP_HEARTBEAT_TIMEOUT_SEC=" << hb_timeout_s_ << "); aborting the process\n";
+        dump_flight("watchdog heartbeat lost", true);
+        std::abort();
+      }
     }
   }
 
   void stop_watchdog() {
     wd_stop_ = true;
     wd_cv_.notify_all();
+    hb_cv_.notify_all();
     if (watchdog_.joinable()) watchdog_.join();
+    if (monitor_.joinable()) monitor_.join();
   }
 
+  std::shared_ptr<Store> store_;
   int device_;
   std::chrono::milliseconds timeout_;
   c10::hip::HIPStream stream_;
@@ -403,6 +462,11 @@ class RcclComm : public Comm {
   std::mutex wd_mu_;
   std::condition_variable wd_cv_;
   std::list<std::shared_ptr<RcclWork>> inflight_;
+  std::atomic<int64_t> heartbeat_{0};
+  double hb_timeout_s_ = 480.0;
+  std::thread monitor_;
+  std::mutex hb_mu_;
+  std::condition_variable hb_cv_;
 };
 
 std::shared_ptr<Comm> make_rccl_comm(std::shared_ptr<Store> store, int rank, int size, int device,

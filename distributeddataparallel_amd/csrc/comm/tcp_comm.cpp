@@ -255,6 +255,7 @@ class TcpComm : public Comm {
           w->finish(nullptr);
         } catch (...) {
           flight_.finish(w->seq, "failed");
+          dump_flight("collective failed");
           w->finish(std::current_exception());
         }
       });

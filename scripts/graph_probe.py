@@ -44,7 +44,7 @@ def linear_only():
     return m, torch.randn(8, 64, device="cuda"), lambda o: o.float().pow(2).mean()
 def our_bn():
     m = nn.Sequential(FusedBatchNorm2d(16)).cuda()
-    return m, torch.randn(8, 16, 8, 8, device="cuda", requires_grad=True).contiguous(memory_format=torch.channels_last), lambda o: o.float().pow(2).mean()
+    return m, torch.randn(8, 16, 8, 8, device="cuda").contiguous(memory_format=torch.channels_last).requires_grad_(), lambda o: o.float().pow(2).mean()
 def ddp_linear():
     m = xddp.DDP(nn.Sequential(nn.Linear(64, 64), nn.ReLU(), nn.Linear(64, 10)).cuda(), device_ids=[0], gradient_as_bucket_view=True)
     return m, torch.randn(8, 64, device="cuda"), lambda o: o.float().pow(2).mean()

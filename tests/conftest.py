@@ -7,6 +7,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+# flight-record dumps from intentionally failing collectives go to a private temp dir
+import tempfile  # noqa: E402
+
+os.environ.setdefault("XDDP_FLIGHT_DUMP_PREFIX", os.path.join(tempfile.mkdtemp(prefix="xddp_flight_"), "rank_"))
 
 
 def pytest_configure(config):

@@ -50,3 +50,39 @@ def test_nan_check():
         run_ranks(_w_nan, world=2)
     finally:
         del os.environ["XDDP_NAN_CHECK"]
+
+
+def _timeout_worker(rank, world, prefix):
+    import json
+    import time
+    from datetime import timedelta
+
+    import torch
+
+    from distributeddataparallel_amd import distributed as xdist
+
+    os.environ["XDDP_FLIGHT_DUMP_PREFIX"] = prefix
+    xdist.init_process_group("cpu", rank=rank, world_size=world, timeout=timedelta(seconds=2))
+    t = torch.ones(8)
+    xdist.all_reduce(t)  # seq 0 completes on both ranks
+    if rank == 0:
+        try:
+            xdist.all_reduce(t)  # rank 1 never joins: times out
+            raise AssertionError("expected a timeout")
+        except RuntimeError as e:
+            assert "timed out" in str(e) or "closed" in str(e), e
+        rec = json.load(open(f"{prefix}{rank}.json"))
+        assert rec["rank"] == 0 and rec["backend"] == "cpu"
+        states = [e["state"] for e in rec["entries"]]
+        assert states[-1] == "failed" and "completed" in states
+        assert json.loads(xdist.get_default_group().comm.flight_json())["num_collectives"] >= 2
+    else:
+        time.sleep(4)
+    os._exit(0)  # the mesh is broken; skip the collective teardown
+
+
+def test_flight_record_dumped_on_collective_timeout(tmp_path):
+    from distributeddataparallel_amd.utils.spawn import free_port, spawn
+
+    spawn(_timeout_worker, args=(2, str(tmp_path / "flight_")), nprocs=2,
+          env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port()), "OMP_NUM_THREADS": "1"})
