@@ -76,6 +76,52 @@ def _to_device(obj, device, non_blocking=True):
     return obj
 
 
+class _CastParams(torch.autograd.Function):
+    """All parameters -> ``dtype`` copies in one multi-tensor launch; grads back in one launch."""
+
+    @staticmethod
+    def forward(ctx, dtype, *params):
+        ctx.src_dtypes = [p.dtype for p in params]
+        outs = [torch.empty_like(p, dtype=dtype) for p in params]
+        _mt_copy(list(params), outs)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        idx = [i for i, g in enumerate(grads) if g is not None]
+        res = [None] * len(grads)
+        src = [_dense(grads[i]) for i in idx]
+        dst = [torch.empty_like(g, dtype=ctx.src_dtypes[i]) for i, g in zip(idx, src)]
+        _mt_copy(src, dst)
+        for i, d in zip(idx, dst):
+            res[i] = d
+        return (None, *res)
+
+
+def _dense(t: torch.Tensor) -> torch.Tensor:
+    if t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last)):
+        return t
+    return t.contiguous()
+
+
+def _mt_copy(src: List[torch.Tensor], dst: List[torch.Tensor]):
+    """dtype-converting copy of a tensor list: one HIP launch per (src, dst) dtype pair on GPU."""
+    if not src:
+        return
+    if src[0].is_cuda:
+        groups = {}
+        for a, b in zip(src, dst):
+            groups.setdefault((a.dtype, b.dtype), ([], []))
+            groups[(a.dtype, b.dtype)][0].append(a)
+            groups[(a.dtype, b.dtype)][1].append(b)
+        for a, b in groups.values():
+            load().mt_scale_copy(a, b, 1.0)
+    else:
+        with torch.no_grad():
+            for a, b in zip(src, dst):
+                b.copy_(a)
+
+
 class _DDPJoinHook(JoinHook):
     """Shadows one DDP iteration's collectives on a rank that ran out of inputs."""
 
@@ -125,8 +171,9 @@ class DistributedDataParallel(nn.Module, Joinable):
         C = load()
         if device_mesh is not None:
             raise NotImplementedError("device_mesh is not supported; pass process_group")
-        if delay_all_reduce_named_params is not None or param_to_hook_all_reduce is not None:
-            raise NotImplementedError("delay_all_reduce_named_params is not supported")
+        if (delay_all_reduce_named_params is None) != (param_to_hook_all_reduce is None):
+            raise ValueError("delay_all_reduce_named_params and param_to_hook_all_reduce need to be set at the "
+                             "same time.")
         self.process_group = self._resolve_process_group(process_group)
         self.module = module
         self.dim = dim
@@ -139,10 +186,17 @@ class DistributedDataParallel(nn.Module, Joinable):
         self._divide_by_initial_world_size = True
         self.mixed_precision = mixed_precision
         if mixed_precision is not None:
-            raise NotImplementedError("native mixed_precision shadow params are not supported; use comm_dtype "
-                                      "or a bf16 model with a master-weight optimizer")
+            self._setup_mixed_precision(module, mixed_precision)
+            red = getattr(mixed_precision, "reduce_dtype", None)
+            if comm_dtype is None and red is not None and red != torch.float32:
+                comm_dtype = red  # reduce in reduce_dtype through the fused pack/cast kernel
 
         self._params_and_buffers_to_ignore = set(getattr(module, "_ddp_params_and_buffers_to_ignore", []))
+        self._delay_all_reduce_params = []
+        if delay_all_reduce_named_params is not None:
+            for name, param in delay_all_reduce_named_params:
+                self._params_and_buffers_to_ignore.add(name)
+                self._delay_all_reduce_params.append(param)
         named = [(n, p) for n, p in module.named_parameters() if n not in self._params_and_buffers_to_ignore]
         seen = set()
         self._module_parameters, self._param_names = [], []
@@ -151,10 +205,11 @@ class DistributedDataParallel(nn.Module, Joinable):
                 seen.add(id(p))
                 self._module_parameters.append(p)
                 self._param_names.append(n)
-        if not self._module_parameters:
+        self._delay_all_reduce_all_params = not self._module_parameters and bool(self._delay_all_reduce_params)
+        if not self._module_parameters and not self._delay_all_reduce_params:
             raise RuntimeError("DistributedDataParallel is not needed when a module doesn't have any parameter "
                                "that requires a gradient.")
-        devices = {p.device for p in self._module_parameters}
+        devices = {p.device for p in (self._module_parameters or self._delay_all_reduce_params)}
         if len(devices) > 1:
             raise ValueError(f"DistributedDataParallel's input module must be on a single device, found {devices}")
         self._param_device = next(iter(devices))
@@ -183,15 +238,119 @@ class DistributedDataParallel(nn.Module, Joinable):
         self._comm_dtype = comm_dtype
 
         self._buffers_list = [b for n, b in module.named_buffers() if n not in self._params_and_buffers_to_ignore]
+        self._comm_hooks = []
+        self._logging_sample_rate = 100
+        self._delay_grad_buffer = None
+        self._delay_grad_views: List[torch.Tensor] = []
+        if self._delay_all_reduce_params:
+            self._register_delay_all_reduce_hook(param_to_hook_all_reduce)
+        if self._delay_all_reduce_all_params:
+            self.reducer = None
+            return
         if init_sync:
             C.verify_params_across_processes(self.process_group.comm, self._module_parameters)
             self._sync_module_states(src=0)
 
         self._build_reducer()
-        self._comm_hooks = []
-        self._logging_sample_rate = 100
         if static_graph:
             self._set_static_graph()
+
+    # ----------------------------------------------------------------------------- delayed all-reduce
+    def _register_delay_all_reduce_hook(self, param_to_hook_all_reduce):
+        """T6j (``pt:nn/parallel/distributed.py:988-1036``): the listed params leave the Reducer;
+        their grads live in one flat buffer that is all-reduced (AVG) when the hook parameter's
+        gradient has been accumulated; backward's end waits for it on the compute stream."""
+        params = self._delay_all_reduce_params
+        dts = {p.dtype for p in params}
+        if len(dts) != 1:
+            raise ValueError(f"delayed all-reduce params must share one dtype, got {dts}")
+        self._delay_grad_buffer = torch.zeros(sum(p.numel() for p in params), dtype=dts.pop(), device=params[0].device)
+        load().broadcast_coalesced(self.process_group.comm, [p.detach() for p in params], self.broadcast_bucket_size, 0)
+        off = 0
+        for p in params:
+            self._delay_grad_views.append(self._delay_grad_buffer[off:off + p.numel()].view(p.shape))
+            off += p.numel()
+        ref = weakref.ref(self)
+        self._delay_state = {"arrived": 0, "work": None, "queued": False}
+        n_grad = sum(1 for p in params if p.requires_grad)
+
+        def launch(ddp):
+            st = ddp._delay_state
+            if st["work"] is None:
+                st["work"] = ddp.process_group.allreduce(ddp._delay_grad_buffer, xdist.ReduceOp.AVG)
+
+        def finish():
+            ddp = ref()
+            if ddp is None:
+                return
+            launch(ddp)  # a delayed param unused this iteration: reduce what arrived
+            ddp._delay_state["work"].wait()
+            ddp._delay_state.update(arrived=0, work=None, queued=False)
+
+        def hook(_param):
+            ddp = ref()
+            if ddp is None or not ddp.require_backward_grad_sync:
+                return
+            st = ddp._delay_state
+            st["arrived"] += 1
+            if not st["queued"]:
+                st["queued"] = True
+                torch.autograd.Variable._execution_engine.queue_callback(finish)
+            if st["arrived"] == n_grad:  # every delayed grad is in the buffer: overlap the rest of backward
+                launch(ddp)
+
+        # ``param_to_hook_all_reduce`` is the reference's trigger; launching once every delayed
+        # grad has been accumulated (its hook included) avoids reducing a half-filled buffer
+        self._delay_hook_handles = [p.register_post_accumulate_grad_hook(hook) for p in params if p.requires_grad]
+        if not param_to_hook_all_reduce.requires_grad:
+            raise ValueError("param_to_hook_all_reduce must require grad")
+
+    def _clear_grad_buffer(self):
+        """Point the delayed params' .grad at their buffer views before backward."""
+        if self._delay_grad_buffer is None:
+            return
+        all_none = all(p.grad is None for p in self._delay_all_reduce_params)
+        for i, p in enumerate(self._delay_all_reduce_params):
+            if p.grad is None:
+                p.grad = self._delay_grad_views[i]
+                if not all_none:
+                    p.grad.zero_()
+        if all_none:
+            self._delay_grad_buffer.zero_()
+
+    # ----------------------------------------------------------------------------- mixed precision
+    def _setup_mixed_precision(self, module, mp):
+        """T6i (``_MixedPrecision{param_dtype, reduce_dtype, buffer_dtype}``): fp32 parameters stay the
+        autograd leaves (grads accumulate and are reduced from fp32 buckets, in ``reduce_dtype`` on
+        the wire); each forward runs the module on ``param_dtype`` copies made by ONE multi-tensor
+        cast launch, and backward casts the grads back in one launch."""
+        self._mp_param_dtype = getattr(mp, "param_dtype", None) or torch.bfloat16
+        buf_dt = getattr(mp, "buffer_dtype", None)
+        if buf_dt is not None:
+            for mod in module.modules():
+                for n, b in list(mod._buffers.items()):
+                    if b is not None and b.is_floating_point():
+                        mod._buffers[n] = b.to(buf_dt)
+        self._mp_names = [n for n, _ in module.named_parameters()]
+        self._mp_params = [p for _, p in module.named_parameters()]
+
+    def _mixed_precision_forward(self, inputs, kwargs):
+        from torch.func import functional_call
+
+        dt = self._mp_param_dtype
+        casted = _CastParams.apply(dt, *self._mp_params)
+
+        def cast(o):
+            if isinstance(o, torch.Tensor):
+                return o.to(dt) if o.is_floating_point() else o
+            if isinstance(o, (list, tuple)):
+                return type(o)(cast(x) for x in o)
+            if isinstance(o, dict):
+                return {k: cast(v) for k, v in o.items()}
+            return o
+
+        return functional_call(self.module, dict(zip(self._mp_names, casted)), tuple(cast(inputs)), cast(kwargs),
+                               tie_weights=True, strict=False)
 
     # ----------------------------------------------------------------------------- setup
     @staticmethod
@@ -262,6 +421,11 @@ class DistributedDataParallel(nn.Module, Joinable):
     def _pre_forward(self, *inputs, **kwargs):
         self._forward_count = getattr(self, "_forward_count", 0) + 1
         _fault.maybe_fail(self.process_group.rank(), self._forward_count)
+        if self._delay_all_reduce_all_params:
+            if self.device_ids:
+                inputs = _to_device(inputs, self.device_ids[0])
+                kwargs = _to_device(kwargs, self.device_ids[0])
+            return inputs, kwargs
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             self.reducer.prepare_for_forward()
         work = Join.notify_join_context(self)
@@ -278,6 +442,9 @@ class DistributedDataParallel(nn.Module, Joinable):
         return inputs, kwargs
 
     def _post_forward(self, output):
+        self._clear_grad_buffer()
+        if self._delay_all_reduce_all_params:
+            return output
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             self.require_forward_param_sync = True
             outs = _find_tensors(output) if (self.find_unused_parameters and not self.static_graph) else []
@@ -289,7 +456,10 @@ class DistributedDataParallel(nn.Module, Joinable):
     def forward(self, *inputs, **kwargs):
         with record_function("DistributedDataParallel.forward"):
             inputs, kwargs = self._pre_forward(*inputs, **kwargs)
-            output = self.module(*inputs, **kwargs)
+            if self.mixed_precision is not None and torch.is_grad_enabled():
+                output = self._mixed_precision_forward(inputs, kwargs)
+            else:
+                output = self.module(*inputs, **kwargs)
             return self._post_forward(output)
 
     # ----------------------------------------------------------------------------- buffers
