@@ -16,6 +16,7 @@ using namespace xddp;
 
 namespace xddp {
 bool install_crash_handler();
+std::shared_ptr<Comm> make_fake_comm(int rank, int size);
 std::shared_ptr<Store> make_file_store(const std::string& path, int world_size);
 std::shared_ptr<Comm> make_py_comm(py::object impl, int rank, int size, const std::string& name);
 }
@@ -192,6 +193,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                               std::chrono::milliseconds(static_cast<int64_t>(timeout_s * 1000)), high_priority);
       }, py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("timeout_s") = 600.0,
       py::arg("high_priority") = true, py::call_guard<py::gil_scoped_release>());
+  m.def("make_fake_comm", &make_fake_comm, py::arg("rank"), py::arg("size"),
+        "Communicator whose collectives complete locally without peers (testing at any world size)");
   m.def("install_crash_handler", &install_crash_handler,
         "Print a native backtrace on fatal signals, then chain to the previous handler");
   m.def("make_py_comm", &make_py_comm, py::arg("impl"), py::arg("rank"), py::arg("size"),

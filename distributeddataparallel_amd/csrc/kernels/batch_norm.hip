@@ -200,11 +200,14 @@ __global__ void bn_eval_coef_kernel(int C, const W* weight, const W* bias, const
 }
 
 // ---------------------------------------------------------------- apply
+// mbits (optional, RELU only): one byte per 8-channel vector, bit j = (y_j > 0) — the backward
+// reads 1/16 of a bf16 activation pass instead of y to rebuild the ReLU mask.
 template <typename T, bool RES, bool RELU>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                           T* __restrict__ y, int64_t nvec, int C,
                                                           const float* __restrict__ scale,
-                                                          const float* __restrict__ shift, int64_t* nbt_inc) {
+                                                          const float* __restrict__ shift, int64_t* nbt_inc,
+                                                          uint8_t* __restrict__ mbits) {
   if (nbt_inc && blockIdx.x == 0 && threadIdx.x == 0) nbt_inc[0] += 1;  // num_batches_tracked.add_(1), fused
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -222,14 +225,19 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
     const dev::f32x4 h1 = *reinterpret_cast<const dev::f32x4*>(shift + c0 + 4);
     const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
     const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    uint32_t bits = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float o = fmaf(a[j], sc[j], sh[j]);
       if (RES) o += r[j];
-      if (RELU) o = fmaxf(o, 0.f);
+      if (RELU) {
+        bits |= (o > 0.f ? 1u : 0u) << j;
+        o = fmaxf(o, 0.f);
+      }
       a[j] = o;
     }
     Vec8<T>::st(y + e, a);
+    if (RELU && mbits) mbits[v] = (uint8_t)bits;
   }
 }
 
@@ -237,11 +245,16 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
 // part layout [rblocks][C][2] = (sum dy_eff, sum dy_eff*(x-mean))
 // MASK: 0 = no ReLU, 1 = ReLU mask from the saved output y, 2 = ReLU mask recomputed from x
 // (x*scale+shift > 0, exact for BN+ReLU without residual; saves reading y)
+// 3 = ReLU mask from the forward's bit mask (1 byte per 8 channels).
 // DUAL: the output had two consumers whose gradients arrive separately (dy + dy2 summed here,
 // in registers, instead of by an autograd add kernel).
-template <typename T, int MASK, bool DUAL>
+// WG: also store the effective gradient g = mask*(dy [+ dy2]) — it IS d(residual) — so the
+// elementwise pass reads g and x only (residual BN backward: 10 -> ~7 activation passes).
+template <typename T, int MASK, bool DUAL, bool WG>
 __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                                const T* __restrict__ x, const T* __restrict__ y,
+                                                               const uint8_t* __restrict__ mbits,
+                                                               T* __restrict__ gout,
                                                                int64_t M, int C, int64_t rows_per,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ ss,
@@ -280,6 +293,14 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
     } else if (MASK == 2) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = fmaf(a[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
+    } else if (MASK == 3) {
+      const uint32_t b = mbits[(r * C + c0) >> 3];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = ((b >> j) & 1u) ? g[j] : 0.f;
+    }
+    if (WG) {
+      Vec8<T>::st(gout + r * C + c0, g);
+      Vec8<T>::rt(g);  // the elementwise pass sees g at storage precision: keep the sums consistent
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -346,7 +367,8 @@ __global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(const float* __rest
 template <typename T, int MASK, bool DRES, bool DUAL>
 __global__ __launch_bounds__(kBlock) void bn_bwd_elem_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                              const T* __restrict__ x,
-                                                             const T* __restrict__ y, T* __restrict__ dx,
+                                                             const T* __restrict__ y,
+                                                             const uint8_t* __restrict__ mbits, T* __restrict__ dx,
                                                              T* __restrict__ dres, int64_t nvec, int C,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ coef,
@@ -377,6 +399,10 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_elem_kernel(const T* __restrict
       Vec8<float>::ld(ss + C + c0, sh);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = fmaf(a[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
+    } else if (MASK == 3) {
+      const uint32_t b = mbits[v];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = ((b >> j) & 1u) ? g[j] : 0.f;
     }
     if (DRES) Vec8<T>::st(dres + e, g);
     // per-channel coefficients as 16-B vector loads (L1/L2 resident; C*16 B per array)
@@ -433,7 +459,7 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
                                    const c10::optional<at::Tensor>& running_var,
                                    const c10::optional<at::Tensor>& num_batches_tracked, bool training,
                                    double momentum, bool cumulative, double eps,
-                                   const c10::optional<at::Tensor>& residual, bool relu) {
+                                   const c10::optional<at::Tensor>& residual, bool relu, bool save_mask) {
   check_nhwc(x);
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), Wd = x.size(3);
   const int64_t M = N * H * Wd;
@@ -443,6 +469,8 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
   auto ss = at::empty({2, C}, fopt);
   const bool has_res = residual.has_value() && residual->defined();
+  at::Tensor mask_bits = (relu && save_mask) ? at::empty({N * H * Wd * C / 8}, x.options().dtype(at::kByte))
+                                             : at::Tensor();
   if (has_res) {
     TORCH_CHECK(residual->sizes() == x.sizes() && residual->scalar_type() == x.scalar_type() &&
                     residual->is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -483,24 +511,26 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
       const T* res = has_res ? reinterpret_cast<const T*>(residual->data_ptr()) : nullptr;
       int64_t* nbt_inc = (training && num_batches_tracked.has_value() && num_batches_tracked->defined())
                              ? num_batches_tracked->data_ptr<int64_t>() : nullptr;
+      uint8_t* mb = mask_bits.defined() ? mask_bits.data_ptr<uint8_t>() : nullptr;
       auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
                            reinterpret_cast<const T*>(x.data_ptr()), res, reinterpret_cast<T*>(y.data_ptr()), nvec,
-                           (int)C, ss.data_ptr<float>(), ss.data_ptr<float>() + C, nbt_inc);
+                           (int)C, ss.data_ptr<float>(), ss.data_ptr<float>() + C, nbt_inc, mb);
       };
       if (has_res) { if (relu) launch(bn_apply_kernel<T, true, true>); else launch(bn_apply_kernel<T, true, false>); }
       else { if (relu) launch(bn_apply_kernel<T, false, true>); else launch(bn_apply_kernel<T, false, false>); }
       XDDP_HIP_CHECK(hipGetLastError());
     });
   });
-  return {y, mean, invstd, ss};
+  return {y, mean, invstd, ss, mask_bits};
 }
 
 // returns (dx, dweight, dbias, dresidual)
 std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x, const c10::optional<at::Tensor>& y,
                                     const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
                                     const at::Tensor& invstd, const c10::optional<at::Tensor>& ss, bool relu,
-                                    bool need_dres, bool need_dweight, const c10::optional<at::Tensor>& dy2_in) {
+                                    bool need_dres, bool need_dweight, const c10::optional<at::Tensor>& dy2_in,
+                                    const c10::optional<at::Tensor>& mask_bits) {
   check_nhwc(x);
   auto dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
   const bool dual = dy2_in.has_value() && dy2_in->defined();
@@ -509,10 +539,13 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "dy must match x");
   const bool have_y = y.has_value() && y->defined();
   const bool have_ss = ss.has_value() && ss->defined();
-  if (relu) TORCH_CHECK(have_y || have_ss, "relu backward needs the forward output or the scale/shift");
-  const int mask = relu ? (have_y ? 1 : 2) : 0;
+  const bool have_bits = mask_bits.has_value() && mask_bits->defined();
+  if (relu) TORCH_CHECK(have_bits || have_y || have_ss, "relu backward needs the mask bits, the output or scale/shift");
+  const int mask = relu ? (have_bits ? 3 : (have_y ? 1 : 2)) : 0;
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), Wd = x.size(3);
   const int64_t M = N * H * Wd;
+  if (mask == 3) TORCH_CHECK(mask_bits->numel() * 8 == M * C && mask_bits->scalar_type() == at::kByte,
+                             "mask bits must be uint8[M*C/8]");
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
   auto fopt = x.options().dtype(at::kFloat);
   auto dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
@@ -524,28 +557,34 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
   auto coef = at::empty({3, C}, fopt);
   Geo g = make_geo(M, (int)C);
   auto part = at::empty({(int64_t)g.rblocks, C, 2}, fopt);
+  // need_dres: the reduce pass writes g = mask*(dy+dy2) into dres; the elementwise pass then
+  // reads (g, x) with no mask and no second gradient
+  const bool wg = need_dres;
   dispatch_act(x.scalar_type(), [&](auto tag_t) {
     using T = decltype(tag_t);
     dispatch_w(wdt, [&](auto tag_w) {
       using W = decltype(tag_w);
       const T* yp = mask == 1 ? reinterpret_cast<const T*>(y->data_ptr()) : nullptr;
       const float* ssp = mask == 2 ? ss->data_ptr<float>() : nullptr;
+      const uint8_t* mbp = mask == 3 ? mask_bits->data_ptr<uint8_t>() : nullptr;
       const size_t lds = (size_t)kBlock * 8 * 2 * sizeof(float);
       const T* d2p = dual ? reinterpret_cast<const T*>(dy2.data_ptr()) : nullptr;
+      T* gp = wg ? reinterpret_cast<T*>(dres.data_ptr()) : nullptr;
       auto launch_red = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds, stream,
                            reinterpret_cast<const T*>(dy.data_ptr()), d2p, reinterpret_cast<const T*>(x.data_ptr()),
-                           yp, M, (int)C, g.rows_per, mean.data_ptr<float>(), ssp, part.data_ptr<float>());
+                           yp, mbp, gp, M, (int)C, g.rows_per, mean.data_ptr<float>(), ssp, part.data_ptr<float>());
       };
-      if (dual) {
-        if (mask == 1) launch_red(bn_bwd_reduce_kernel<T, 1, true>);
-        else if (mask == 2) launch_red(bn_bwd_reduce_kernel<T, 2, true>);
-        else launch_red(bn_bwd_reduce_kernel<T, 0, true>);
-      } else {
-        if (mask == 1) launch_red(bn_bwd_reduce_kernel<T, 1, false>);
-        else if (mask == 2) launch_red(bn_bwd_reduce_kernel<T, 2, false>);
-        else launch_red(bn_bwd_reduce_kernel<T, 0, false>);
-      }
+#define XDDP_BN_RED(MK)                                                                           \
+  if (dual) { if (wg) launch_red(bn_bwd_reduce_kernel<T, MK, true, true>);                        \
+              else launch_red(bn_bwd_reduce_kernel<T, MK, true, false>); }                        \
+  else { if (wg) launch_red(bn_bwd_reduce_kernel<T, MK, false, true>);                            \
+         else launch_red(bn_bwd_reduce_kernel<T, MK, false, false>); }
+      if (mask == 1) { XDDP_BN_RED(1) }
+      else if (mask == 2) { XDDP_BN_RED(2) }
+      else if (mask == 3) { XDDP_BN_RED(3) }
+      else { XDDP_BN_RED(0) }
+#undef XDDP_BN_RED
       XDDP_HIP_CHECK(hipGetLastError());
       hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(64), 0, stream,
                          part.data_ptr<float>(), g.rblocks, (int)C, M,
@@ -554,19 +593,27 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
                          db.defined() ? reinterpret_cast<W*>(db.data_ptr()) : nullptr, coef.data_ptr<float>());
       XDDP_HIP_CHECK(hipGetLastError());
       const int64_t nvec = M * C / 8;
-      auto launch = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
-                           reinterpret_cast<const T*>(dy.data_ptr()), d2p, reinterpret_cast<const T*>(x.data_ptr()),
-                           yp, reinterpret_cast<T*>(dx.data_ptr()),
-                           need_dres ? reinterpret_cast<T*>(dres.data_ptr()) : nullptr, nvec, (int)C,
-                           mean.data_ptr<float>(), coef.data_ptr<float>(), ssp);
-      };
-#define XDDP_BN_ELEM(MK, DR)                                                              \
-  if (dual) launch(bn_bwd_elem_kernel<T, MK, DR, true>); else launch(bn_bwd_elem_kernel<T, MK, DR, false>)
-      if (mask == 1) { if (need_dres) { XDDP_BN_ELEM(1, true); } else { XDDP_BN_ELEM(1, false); } }
-      else if (mask == 2) { if (need_dres) { XDDP_BN_ELEM(2, true); } else { XDDP_BN_ELEM(2, false); } }
-      else { if (need_dres) { XDDP_BN_ELEM(0, true); } else { XDDP_BN_ELEM(0, false); } }
+      if (wg) {
+        hipLaunchKernelGGL((bn_bwd_elem_kernel<T, 0, false, false>), dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
+                           reinterpret_cast<const T*>(dres.data_ptr()), nullptr,
+                           reinterpret_cast<const T*>(x.data_ptr()), nullptr, nullptr,
+                           reinterpret_cast<T*>(dx.data_ptr()), nullptr, nvec, (int)C, mean.data_ptr<float>(),
+                           coef.data_ptr<float>(), nullptr);
+      } else {
+        auto launch = [&](auto kern) {
+          hipLaunchKernelGGL(kern, dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
+                             reinterpret_cast<const T*>(dy.data_ptr()), d2p, reinterpret_cast<const T*>(x.data_ptr()),
+                             yp, mbp, reinterpret_cast<T*>(dx.data_ptr()), nullptr, nvec, (int)C,
+                             mean.data_ptr<float>(), coef.data_ptr<float>(), ssp);
+        };
+#define XDDP_BN_ELEM(MK) \
+  if (dual) launch(bn_bwd_elem_kernel<T, MK, false, true>); else launch(bn_bwd_elem_kernel<T, MK, false, false>)
+        if (mask == 1) { XDDP_BN_ELEM(1); }
+        else if (mask == 2) { XDDP_BN_ELEM(2); }
+        else if (mask == 3) { XDDP_BN_ELEM(3); }
+        else { XDDP_BN_ELEM(0); }
 #undef XDDP_BN_ELEM
+      }
       XDDP_HIP_CHECK(hipGetLastError());
     });
   });

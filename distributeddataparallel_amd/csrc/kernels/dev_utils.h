@@ -82,6 +82,8 @@ struct Vec8<float> {
     *reinterpret_cast<f32x4*>(p) = a;
     *reinterpret_cast<f32x4*>(p + 4) = b;
   }
+  // round values to storage precision in registers (identity for fp32)
+  static __device__ __forceinline__ void rt(float (&)[8]) {}
 };
 template <>
 struct Vec8<double> {
@@ -103,6 +105,7 @@ struct Vec8<double> {
       *reinterpret_cast<f64x2*>(p + 2 * j) = a;
     }
   }
+  static __device__ __forceinline__ void rt(float (&)[8]) {}
 };
 template <>
 struct Vec8<bf16_t> {
@@ -123,6 +126,14 @@ struct Vec8<bf16_t> {
     for (int j = 0; j < 4; ++j) a[j] = pack_bf16x2((float)v[2 * j], (float)v[2 * j + 1]);
     *reinterpret_cast<u32x4*>(p) = a;
   }
+  static __device__ __forceinline__ void rt(float (&v)[8]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t u = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+      v[2 * j] = __uint_as_float(u << 16);
+      v[2 * j + 1] = __uint_as_float(u & 0xffff0000u);
+    }
+  }
 };
 template <>
 struct Vec8<f16_t> {
@@ -142,6 +153,14 @@ struct Vec8<f16_t> {
 #pragma unroll
     for (int j = 0; j < 4; ++j) a[j] = pack_f16x2((float)v[2 * j], (float)v[2 * j + 1]);
     *reinterpret_cast<u32x4*>(p) = a;
+  }
+  static __device__ __forceinline__ void rt(float (&v)[8]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t u = pack_f16x2(v[2 * j], v[2 * j + 1]);
+      v[2 * j] = f16_to_f32((uint16_t)(u & 0xffffu));
+      v[2 * j + 1] = f16_to_f32((uint16_t)(u >> 16));
+    }
   }
 };
 

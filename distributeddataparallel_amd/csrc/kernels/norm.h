@@ -14,11 +14,12 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
                                    const c10::optional<at::Tensor>& running_var,
                                    const c10::optional<at::Tensor>& num_batches_tracked, bool training,
                                    double momentum, bool cumulative, double eps,
-                                   const c10::optional<at::Tensor>& residual, bool relu);
+                                   const c10::optional<at::Tensor>& residual, bool relu, bool save_mask);
 std::vector<at::Tensor> bn_backward(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& y,
                                     const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
                                     const at::Tensor& invstd, const c10::optional<at::Tensor>& ss, bool relu,
-                                    bool need_dres, bool need_dweight, const c10::optional<at::Tensor>& dy2);
+                                    bool need_dres, bool need_dweight, const c10::optional<at::Tensor>& dy2,
+                                    const c10::optional<at::Tensor>& mask_bits);
 std::vector<at::Tensor> ln_forward(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
                                    const c10::optional<at::Tensor>& beta, double eps, bool rms);
 std::vector<at::Tensor> ln_backward(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& gamma,

@@ -10,10 +10,10 @@ namespace kernels {
 void bind_norm_kernels(py::module_& m) {
   m.def("bn_forward", &bn_forward, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("num_batches_tracked"), py::arg("training"), py::arg("momentum"),
-        py::arg("cumulative"), py::arg("eps"), py::arg("residual"), py::arg("relu"));
+        py::arg("cumulative"), py::arg("eps"), py::arg("residual"), py::arg("relu"), py::arg("save_mask") = false);
   m.def("bn_backward", &bn_backward, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("weight"), py::arg("mean"),
         py::arg("invstd"), py::arg("scale_shift"), py::arg("relu"), py::arg("need_dres"), py::arg("need_dweight"),
-        py::arg("dy2") = py::none());
+        py::arg("dy2") = py::none(), py::arg("mask_bits") = py::none());
   m.def("maxpool_forward", &maxpool_forward, py::arg("x"), py::arg("kernel"), py::arg("stride"), py::arg("pad"));
   m.def("maxpool_backward", &maxpool_backward, py::arg("dy"), py::arg("idx"), py::arg("x_like"), py::arg("kernel"),
         py::arg("stride"), py::arg("pad"), py::arg("dy2") = py::none());

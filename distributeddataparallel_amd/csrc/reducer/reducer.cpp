@@ -809,7 +809,8 @@ void broadcast_coalesced(const std::shared_ptr<Comm>& comm, std::vector<at::Tens
   // All dtypes travel in ONE byte buffer per <= buffer_bytes chunk (each tensor 16-B aligned
   // inside it): DDP's per-forward BN-buffer sync is one latency-bound broadcast instead of one
   // per dtype. Pack/unpack are single byte-exact multi-tensor kernels on the GPU.
-  if (tensors.empty() || comm->size() == 1) return;
+  // one rank, or the fake backend (peers are hallucinated: local values stand for the root's)
+  if (tensors.empty() || comm->size() == 1 || comm->backend() == "fake") return;
   size_t i = 0;
   while (i < tensors.size()) {
     std::vector<at::Tensor> chunk, staged;

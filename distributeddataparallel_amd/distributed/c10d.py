@@ -67,6 +67,7 @@ class Backend:
     NCCL = "rccl"  # on ROCm, "nccl" *is* RCCL
     CPU = "cpu"
     GLOO = "cpu"
+    FAKE = "fake"  # hallucinated collectives (one process posing as rank r of W), for tests
 
     @staticmethod
     def normalize(name: Optional[str]) -> str:
@@ -77,6 +78,8 @@ class Backend:
             return "rccl"
         if n in ("gloo", "cpu", "tcp"):
             return "cpu"
+        if n == "fake":
+            return "fake"
         raise ValueError(f"unknown backend {name!r}")
 
 
@@ -251,6 +254,8 @@ def _make_comm(backend: str, store, rank: int, size: int, device, timeout: timed
     """Create the native communicator; XDDP_DEBUG=DETAIL / XDDP_NAN_CHECK=1 wrap it in the debug
     communicator (cross-rank collective fingerprints / NaN scan)."""
     C = load()
+    if backend == "fake":
+        return C.make_fake_comm(rank, size)
     if backend == "rccl":
         hp = os.environ.get("XDDP_COMM_HIGH_PRIORITY", "1") != "0"
         comm = C.make_rccl_comm(store, rank, size, device.index, timeout.total_seconds(), hp)
@@ -278,7 +283,11 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
     if timeout is None:
         timeout = DEFAULT_RCCL_TIMEOUT if be == "rccl" else DEFAULT_TIMEOUT
     master_addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
-    if store is None:
+    if store is None and be == "fake":
+        if rank < 0 or world_size <= 0:
+            raise ValueError("the fake backend needs explicit rank and world_size")
+        store = C.HashStore()
+    elif store is None:
         store, rank, world_size, master_addr = rendezvous(init_method, rank, world_size, timeout)
     else:
         if rank < 0 or world_size <= 0:
@@ -293,7 +302,7 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
     _world.groups[pg.group_name] = pg
     GroupMember.WORLD = pg
     _excepthook_prefix(rank)
-    if os.environ.get("XDDP_INIT_BARRIER", "1") == "1" and world_size > 1:
+    if os.environ.get("XDDP_INIT_BARRIER", "1") == "1" and world_size > 1 and be != "fake":
         # store-based barrier: every rank's communicator is up before returning
         n = store.add("xddp/init_barrier", 1)
         if n == world_size:

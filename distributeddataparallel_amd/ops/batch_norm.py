@@ -25,14 +25,14 @@ class _BNAct(torch.autograd.Function):
     def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, residual, relu, dual):
         C = load()
         ctx.set_materialize_grads(False)
-        y, mean, invstd, ss = C.bn_forward(x, weight, bias, running_mean, running_var, nbt, True, momentum, cma,
-                                           eps, residual, relu)
+        # ReLU mask: with a residual the mask depends on it, so the forward stores it as bits
+        # (1/16 of a bf16 activation); without one it is recomputed from x*scale+shift
+        keep_mask = relu and residual is not None
+        y, mean, invstd, ss, bits = C.bn_forward(x, weight, bias, running_mean, running_var, nbt, True, momentum,
+                                                 cma, eps, residual, relu, keep_mask)
         ctx.relu = relu
         ctx.has_res = residual is not None
-        # ReLU mask: from y when a residual was added (mask depends on it), else recomputed
-        # from x*scale+shift in the backward kernels (one fewer activation read)
-        keep_y = relu and residual is not None
-        ctx.save_for_backward(x, y if keep_y else None, weight, mean, invstd, ss)
+        ctx.save_for_backward(x, bits if keep_mask else None, weight, mean, invstd, ss)
         if dual:
             # two consumers (next block's conv and its residual) get separate autograd outputs over
             # the same memory, so their gradients reach backward() unsummed: the kernels add them
@@ -43,14 +43,14 @@ class _BNAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, dy2=None):
         C = load()
-        x, y, weight, mean, invstd, ss = ctx.saved_tensors
+        x, bits, weight, mean, invstd, ss = ctx.saved_tensors
         if dy is None:
             dy, dy2 = dy2, None
         if dy is None:
             return (None,) * 12
         need_dw = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
-        dx, dw, db, dres = C.bn_backward(dy, x, y, weight, mean, invstd, ss, ctx.relu,
-                                         ctx.has_res and ctx.needs_input_grad[9], need_dw, dy2)
+        dx, dw, db, dres = C.bn_backward(dy, x, None, weight, mean, invstd, ss, ctx.relu,
+                                         ctx.has_res and ctx.needs_input_grad[9], need_dw, dy2, bits)
         return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None, None, dres if ctx.has_res else None, None, None)
 
@@ -76,8 +76,8 @@ def batch_norm_act(x, running_mean, running_var, weight=None, bias=None, trainin
     if use_kernel and not training and not (torch.is_grad_enabled() and (
             x.requires_grad or (weight is not None and weight.requires_grad))):
         C = load()
-        y, _, _, _ = C.bn_forward(x, weight, bias, running_mean, running_var, None, False, 0.0, False, float(eps),
-                                  residual, relu)
+        y = C.bn_forward(x, weight, bias, running_mean, running_var, None, False, 0.0, False, float(eps),
+                         residual, relu)[0]
         return (y, y) if dual_output else y
     # reference path
     if training and num_batches_tracked is not None:

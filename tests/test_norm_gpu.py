@@ -160,3 +160,47 @@ def test_batchnorm_relu_mask_recompute_matches_saved_output_path():
     yb.backward(g)
     torch.testing.assert_close(ya, yb)
     torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_batchnorm_backward_mask_modes_agree(dt):
+    """Residual BN+ReLU backward: mask from y (mode 1) / from the forward's bit mask (mode 3),
+    with d(residual) written by the elementwise pass or by the reduce pass, single or dual
+    incoming gradients — all must agree."""
+    from distributeddataparallel_amd._native import load
+
+    C_ = load()
+    torch.manual_seed(2)
+    shape = (4, 64, 10, 9)
+    x = torch.randn(shape, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    r = torch.randn(shape, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    w = torch.rand(64, device=DEV) + 0.5
+    b = torch.randn(64, device=DEV) * 0.1
+    y, mean, invstd, ss, bits = C_.bn_forward(x, w, b, None, None, None, True, 0.1, False, 1e-5, r, True, True)
+    assert bits.numel() * 8 == x.numel() and bits.dtype == torch.uint8
+    ref_mask = (y.float() > 0).permute(0, 2, 3, 1).reshape(-1, 8)
+    unpacked = ((bits.view(-1, 1).int() >> torch.arange(8, device=DEV)) & 1).bool()
+    assert torch.equal(unpacked, ref_mask)
+    g1 = torch.randn(shape, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    g2 = torch.randn(shape, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    gsum = (g1.float() + g2.float()).to(dt).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for kw in (dict(y=y, bits=None), dict(y=None, bits=bits)):
+        for need_dres in (False, True):
+            for dual in (False, True):
+                dy, dy2 = (g1, g2) if dual else (gsum, None)
+                dx, dw, db, dres = C_.bn_backward(dy, x, kw["y"], w, mean, invstd, ss, True, need_dres, True, dy2,
+                                                  kw["bits"])
+                outs.append((dx.float(), dw.float(), db.float(), None if dres is None else dres.float()))
+    tol = _tol(dt)
+    # dgamma/dbeta are sums over N*H*W of bf16-rounded gradients: rounding g before the sum
+    # (reduce pass writing d(residual)) vs after (fp32 dy+dy2) moves them by ~sqrt(M)*eps
+    rtol = dict(rtol=3e-2, atol=0.02 * (x.numel() / 64) ** 0.5) if dt != torch.float32 else tol
+    for o in outs[1:]:
+        torch.testing.assert_close(o[0], outs[0][0], **tol)
+        for a, c in zip(o[1:3], outs[0][1:3]):
+            torch.testing.assert_close(a, c, **rtol)
+    dres_all = [o[3] for o in outs if o[3] is not None]
+    for d in dres_all[1:]:
+        torch.testing.assert_close(d, dres_all[0], **tol)
+    torch.testing.assert_close(dres_all[0], gsum.float() * (y.float() > 0), **tol)
