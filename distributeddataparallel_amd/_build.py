@@ -37,8 +37,10 @@ def _torch_paths():
 
 
 def _sources():
-    hip = sorted(CSRC.rglob("*.hip"))
-    cpp = sorted(CSRC.rglob("*.cpp"))
+    # csrc/tests holds standalone host programs (sanitizer stress drivers), not extension code
+    keep = lambda p: "tests" not in p.relative_to(CSRC).parts  # noqa: E731
+    hip = sorted(p for p in CSRC.rglob("*.hip") if keep(p))
+    cpp = sorted(p for p in CSRC.rglob("*.cpp") if keep(p))
     return hip, cpp
 
 
