@@ -162,6 +162,10 @@ class RcclComm : public Comm {
       std::memcpy(&id, s.data(), sizeof(id));
     }
     XDDP_NCCL_CHECK(ncclCommInitRank(&comm_, size, id, rank));
+    // XDDP_RCCL_FORCE_LAUNCH=1: issue real RCCL kernels even on one rank, so the multi-rank
+    // launch path (comm-stream ordering, events, allocator stream records) runs on a 1-GPU box
+    const char* fl = std::getenv("XDDP_RCCL_FORCE_LAUNCH");
+    force_launch_ = fl && std::string(fl) == "1";
     heartbeat_ = now_ns();
     watchdog_ = std::thread([this] { watchdog_loop(); });
     const char* hb = std::getenv("XDDP_HEARTBEAT_TIMEOUT_SEC");
@@ -179,7 +183,7 @@ class RcclComm : public Comm {
 
   std::shared_ptr<Work> allreduce(at::Tensor t, RedOp op, double premul) override {
     check_tensor(t);
-    if (size_ == 1 && op != RedOp::PREMUL_SUM) return local_noop("allreduce", t);  // identity on one rank
+    if (size_ == 1 && !force_launch_ && op != RedOp::PREMUL_SUM) return local_noop("allreduce", t);  // identity
     return launch("allreduce", t, {t}, [&](hipStream_t s) {
       if (op == RedOp::PREMUL_SUM) {
         TORCH_CHECK(at::isFloatingType(t.scalar_type()), "PREMUL_SUM needs a floating-point tensor");
@@ -203,7 +207,7 @@ class RcclComm : public Comm {
 
   std::shared_ptr<Work> broadcast(at::Tensor t, int root) override {
     check_tensor(t);
-    if (size_ == 1) return local_noop("broadcast", t);
+    if (size_ == 1 && !force_launch_) return local_noop("broadcast", t);
     return launch("broadcast", t, {t}, [&](hipStream_t s) {
       XDDP_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, s));
     });
@@ -453,6 +457,7 @@ class RcclComm : public Comm {
   std::mutex comm_mu_;
   bool aborted_ = false;
   bool destroyed_ = false;
+  bool force_launch_ = false;
   int in_group_ = 0;
   bool capturing_ = false;
   std::vector<std::shared_ptr<RcclWork>> group_works_;

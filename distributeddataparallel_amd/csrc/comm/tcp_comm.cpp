@@ -2,6 +2,8 @@
 // SURVEY.md §2.2 T5b). Ring reduce-scatter + all-gather for all-reduce, ring all-gather,
 // pipelined chain broadcast, pairwise all-to-all. Collectives run strictly in submission
 // order on one worker thread per communicator, so every rank issues the same wire sequence.
+// Device (GPU) tensors are staged through host memory, so the same backend also runs
+// multi-rank DDP on GPU tensors where RCCL cannot (e.g. several ranks sharing one GPU).
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netdb.h>
@@ -46,6 +48,24 @@ class CpuWork : public Work {
   std::exception_ptr err;
 };
 
+// A host-staged collective on device tensors: wait() finishes the host collective, then copies
+// each host result back into its device tensor on the waiter's current stream (once).
+class StagedWork : public Work {
+ public:
+  bool is_completed() override { return inner->is_completed(); }
+  void wait() override {
+    inner->wait();
+    std::lock_guard<std::mutex> g(mu);
+    if (copied) return;
+    for (auto& p : back) p.first.copy_(p.second);
+    copied = true;
+  }
+  std::shared_ptr<Work> inner;
+  std::vector<std::pair<at::Tensor, at::Tensor>> back;  // (device tensor, host result)
+  std::mutex mu;
+  bool copied = false;
+};
+
 void set_nonblock(int fd, bool nb) {
   int fl = ::fcntl(fd, F_GETFL, 0);
   ::fcntl(fd, F_SETFL, nb ? (fl | O_NONBLOCK) : (fl & ~O_NONBLOCK));
@@ -78,36 +98,63 @@ class TcpComm : public Comm {
     peers_.assign(size_, -1);
   }
 
+  // Device tensors (gloo's CUDA support): staged through host memory. The device-to-host copy
+  // runs on the caller's current stream (ordered after the producer kernels); the copy back runs
+  // in wait() on the waiter's current stream, so consumers are ordered after it.
   std::shared_ptr<Work> allreduce(at::Tensor t, RedOp op, double premul) override {
-    return enqueue("allreduce", t, {t}, [=]() mutable { do_allreduce(t, op, premul); });
+    if (t.is_cuda()) {
+      auto h = t.cpu();
+      return staged(host_allreduce(h, op, premul), {{t, h}});
+    }
+    return host_allreduce(t, op, premul);
   }
   std::shared_ptr<Work> broadcast(at::Tensor t, int root) override {
-    return enqueue("broadcast", t, {t}, [=]() mutable { do_broadcast(t, root); });
+    if (t.is_cuda()) {
+      auto h = t.cpu();
+      return staged(host_broadcast(h, root), {{t, h}});
+    }
+    return host_broadcast(t, root);
   }
   std::shared_ptr<Work> allgather(at::Tensor out, at::Tensor in) override {
     TORCH_CHECK(out.numel() == in.numel() * size_, "allgather: output must hold size*input elements");
-    return enqueue("allgather", in, {out}, [=]() mutable { do_allgather(out, in); });
+    if (out.is_cuda() || in.is_cuda()) {
+      auto ho = at::empty(out.sizes(), out.options().device(at::kCPU));
+      return staged(host_allgather(ho, in.cpu()), {{out, ho}});
+    }
+    return host_allgather(out, in);
   }
   std::shared_ptr<Work> reduce_scatter(at::Tensor out, at::Tensor in, RedOp op) override {
     TORCH_CHECK(in.numel() == out.numel() * size_, "reduce_scatter: input must hold size*output elements");
-    return enqueue("reduce_scatter", in, {out}, [=]() mutable { do_reduce_scatter(out, in, op); });
+    if (out.is_cuda() || in.is_cuda()) {
+      auto ho = at::empty(out.sizes(), out.options().device(at::kCPU));
+      return staged(host_reduce_scatter(ho, in.cpu(), op), {{out, ho}});
+    }
+    return host_reduce_scatter(out, in, op);
   }
   std::shared_ptr<Work> alltoall(at::Tensor out, at::Tensor in) override {
     TORCH_CHECK(in.numel() == out.numel() && in.numel() % size_ == 0, "alltoall: equal splits required");
-    return enqueue("alltoall", in, {out}, [=]() mutable { do_alltoall(out, in); });
+    if (out.is_cuda() || in.is_cuda()) {
+      auto ho = at::empty(out.sizes(), out.options().device(at::kCPU));
+      return staged(host_alltoall(ho, in.cpu()), {{out, ho}});
+    }
+    return host_alltoall(out, in);
   }
   std::shared_ptr<Work> send(at::Tensor t, int dst) override {
-    return enqueue("send", t, {t}, [=]() mutable {
-      auto c = t.contiguous();
+    auto h = t.is_cuda() ? t.cpu() : t;
+    auto w = enqueue("send", h, {h}, [=]() mutable {
+      auto c = h.contiguous();
       send_all(peers_.at(dst), c.data_ptr(), c.nbytes());
     });
+    return t.is_cuda() ? staged(w, {}) : w;
   }
   std::shared_ptr<Work> recv(at::Tensor t, int src) override {
-    return enqueue("recv", t, {t}, [=]() mutable {
-      auto c = t.is_contiguous() ? t : at::empty_like(t, at::MemoryFormat::Contiguous);
+    auto h = t.is_cuda() ? at::empty(t.sizes(), t.options().device(at::kCPU)) : t;
+    auto w = enqueue("recv", h, {h}, [=]() mutable {
+      auto c = h.is_contiguous() ? h : at::empty_like(h, at::MemoryFormat::Contiguous);
       recv_all(peers_.at(src), c.data_ptr(), c.nbytes());
-      if (!t.is_contiguous()) t.copy_(c);
+      if (!h.is_contiguous()) h.copy_(c);
     });
+    return t.is_cuda() ? staged(w, {{t, h}}) : w;
   }
   std::shared_ptr<Work> barrier() override {
     auto t = at::ones({1}, at::kInt);
@@ -115,6 +162,31 @@ class TcpComm : public Comm {
   }
 
  private:
+  std::shared_ptr<Work> host_allreduce(at::Tensor t, RedOp op, double premul) {
+    return enqueue("allreduce", t, {t}, [=]() mutable { do_allreduce(t, op, premul); });
+  }
+  std::shared_ptr<Work> host_broadcast(at::Tensor t, int root) {
+    return enqueue("broadcast", t, {t}, [=]() mutable { do_broadcast(t, root); });
+  }
+  std::shared_ptr<Work> host_allgather(at::Tensor out, at::Tensor in) {
+    return enqueue("allgather", in, {out}, [=]() mutable { do_allgather(out, in); });
+  }
+  std::shared_ptr<Work> host_reduce_scatter(at::Tensor out, at::Tensor in, RedOp op) {
+    return enqueue("reduce_scatter", in, {out}, [=]() mutable { do_reduce_scatter(out, in, op); });
+  }
+  std::shared_ptr<Work> host_alltoall(at::Tensor out, at::Tensor in) {
+    return enqueue("alltoall", in, {out}, [=]() mutable { do_alltoall(out, in); });
+  }
+
+  std::shared_ptr<Work> staged(std::shared_ptr<Work> inner, std::vector<std::pair<at::Tensor, at::Tensor>> back) {
+    auto w = std::make_shared<StagedWork>();
+    w->inner = std::move(inner);
+    w->back = std::move(back);
+    w->seq = w->inner->seq;
+    for (auto& p : w->back) w->outputs.push_back(p.first);
+    return w;
+  }
+
   // ---------------- mesh setup ----------------
   void connect_mesh(const std::string& host) {
     int lfd = ::socket(AF_INET, SOCK_STREAM, 0);

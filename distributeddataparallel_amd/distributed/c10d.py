@@ -177,8 +177,9 @@ class ProcessGroup:
 
     # -------- collectives (return Work) --------
     def _prep(self, t: torch.Tensor) -> torch.Tensor:
-        if self._backend == "cpu" and t.device.type != "cpu":
-            raise RuntimeError("the cpu backend only handles CPU tensors")
+        # the cpu backend stages device tensors through host memory (gloo-style CUDA support)
+        if self._backend == "cpu" and t.device.type not in ("cpu", "cuda"):
+            raise RuntimeError(f"the cpu backend cannot handle {t.device.type} tensors")
         return t
 
     def allreduce(self, tensor, op=ReduceOp.SUM, premul: float = 1.0) -> Work:

@@ -224,8 +224,8 @@ class DistributedDataParallel(nn.Module, Joinable):
             self.output_device = self.device_ids[0] if output_device is None else torch.device(output_device)
         if self.process_group.backend == "rccl" and self.device_type != "cuda":
             raise ValueError("the rccl backend needs the module on a GPU")
-        if self.process_group.backend == "cpu" and self.device_type != "cpu":
-            raise ValueError("the cpu backend needs the module on the CPU")
+        # backend "cpu" with a GPU module: collectives are staged through host memory (slow;
+        # used to run several DDP ranks on one GPU, where RCCL refuses duplicate devices)
         self._comm_device = self._param_device
 
         env_cap = os.environ.get("XDDP_BUCKET_CAP_MB")
