@@ -525,6 +525,43 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
   return {y, mean, invstd, ss, mask_bits};
 }
 
+// Apply pass only, with coefficients computed elsewhere (e.g. from a conv epilogue's partial
+// statistics): y = [relu](x*scale + shift [+ residual]); optional ReLU bit mask; optional
+// num_batches_tracked += 1. Returns (y, mask_bits).
+std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, const c10::optional<at::Tensor>& residual,
+                                 bool relu, bool save_mask, const c10::optional<at::Tensor>& num_batches_tracked) {
+  check_nhwc(x);
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), Wd = x.size(3);
+  TORCH_CHECK(ss.is_cuda() && ss.scalar_type() == at::kFloat && ss.numel() == 2 * C && ss.is_contiguous(),
+              "bn_apply: scale/shift must be float [2, C]");
+  const bool has_res = residual.has_value() && residual->defined();
+  if (has_res)
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->scalar_type() == x.scalar_type() &&
+                    residual->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "fused residual must match x (shape, dtype, channels_last)");
+  auto y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  at::Tensor mask_bits = (relu && save_mask) ? at::empty({N * H * Wd * C / 8}, x.options().dtype(at::kByte))
+                                             : at::Tensor();
+  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  const int64_t nvec = N * H * Wd * C / 8;
+  int64_t* nbt_inc = (num_batches_tracked.has_value() && num_batches_tracked->defined())
+                         ? num_batches_tracked->data_ptr<int64_t>() : nullptr;
+  uint8_t* mb = mask_bits.defined() ? mask_bits.data_ptr<uint8_t>() : nullptr;
+  dispatch_act(x.scalar_type(), [&](auto tag_t) {
+    using T = decltype(tag_t);
+    const T* res = has_res ? reinterpret_cast<const T*>(residual->data_ptr()) : nullptr;
+    auto launch = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
+                         reinterpret_cast<const T*>(x.data_ptr()), res, reinterpret_cast<T*>(y.data_ptr()), nvec,
+                         (int)C, ss.data_ptr<float>(), ss.data_ptr<float>() + C, nbt_inc, mb);
+    };
+    if (has_res) { if (relu) launch(bn_apply_kernel<T, true, true>); else launch(bn_apply_kernel<T, true, false>); }
+    else { if (relu) launch(bn_apply_kernel<T, false, true>); else launch(bn_apply_kernel<T, false, false>); }
+    XDDP_HIP_CHECK(hipGetLastError());
+  });
+  return {y, mask_bits};
+}
+
 // returns (dx, dweight, dbias, dresidual)
 std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x, const c10::optional<at::Tensor>& y,
                                     const c10::optional<at::Tensor>& weight, const at::Tensor& mean,

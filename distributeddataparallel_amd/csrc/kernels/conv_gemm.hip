@@ -1,0 +1,463 @@
+// 1x1 convolution (NHWC, bf16) as an MFMA GEMM with BatchNorm fused into its prologue and
+// epilogue, for gfx950 / CDNA4.
+//
+//   Y[M, N] = op(X)[M, K] · W[N, K]^T        M = batch·OH·OW pixels, K = Cin, N = Cout
+//   op      = identity, or relu(x·s_k + b_k) per input channel (the PREVIOUS BatchNorm's apply,
+//             so its normalized activation is never written to HBM)
+//   epilogue: bf16 Y plus, per output channel, the batch statistics this conv's own BatchNorm
+//             needs, so BN does not re-read Y for its stats pass.
+//
+// Why this shape (profiles/): at ResNet-50 bs256 the 1x1 convs are
+// HBM-bound (K = 64..2048 is short), and every BN pass over an activation costs as much as the
+// conv itself. Fusing removes whole activation passes; the GEMM itself only has to stream.
+//
+// Structure: 256 threads = 4 waves (2 x 2), block tile BM x BN x 64, each wave (BM/2) x (BN/2)
+// built from mfma_f32_16x16x32_bf16 tiles. Operands are staged global -> VGPR -> LDS (so the BN
+// prologue is applied once per element, in registers), two LDS buffers, the next K-tile's loads
+// issued before the current tile's MFMAs (2-phase pipeline). LDS rows are 128 B (64 bf16) with the
+// 16-B chunk index XOR-swizzled by (row >> 1) & 7, so the 16 lanes of a ds_read_b128 group hit 16
+// distinct bank groups. A block walks several M-tiles of one N-tile (grid sized to the CU count)
+// and merges their statistics in registers (Chan's parallel mean/M2), so the per-channel
+// partials a finalize kernel has to merge are few. Block ids are remapped XCD-contiguously so
+// the blocks sharing an A panel share one L2.
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include "common.h"
+#include "kernels/dev_utils.h"
+
+namespace xddp {
+namespace kernels {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+using dev::f32x4;
+using dev::u32x4;
+
+constexpr int kBK = 64;       // K per tile (one 128-B LDS row per operand row)
+#ifndef XDDP_GEMM_NTSTORE
+#define XDDP_GEMM_NTSTORE 1
+#endif
+constexpr bool NTSTORE = XDDP_GEMM_NTSTORE;  // streaming (non-temporal) output stores
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ ((row >> 1) & 7)); }
+
+// LDS-only workgroup barrier: __syncthreads() also waits vmcnt(0), which would drain the
+// prefetched global loads that are meant to stay in flight across it (guide §5 "Pipelining
+// across barriers"). LDS traffic is ordered by lgkmcnt(0) + s_barrier alone.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ float bf16_round(float v) { return __uint_as_float(dev::pack_bf16x2(v, 0.f) << 16); }
+
+struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every stride-th pixel)
+  int OH, OW, IH, IW, stride;
+  template <bool STRIDED>
+  __device__ __forceinline__ int64_t in_row(int m) const {  // M < 2^31 (host-checked)
+    if (!STRIDED) return m;
+    const int hw = OH * OW;
+    const int n = m / hw, r = m - n * hw;
+    const int oh = r / OW, ow = r - oh * OW;
+    return ((int64_t)n * IH + oh * stride) * IW + (int64_t)ow * stride;
+  }
+};
+
+template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, bool STRIDED>
+__global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
+    const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, int64_t M, int N,
+    int K, RowMap rm, const float* __restrict__ pro_ss, float* __restrict__ part, int mtiles, int ntiles,
+    int groups) {
+  constexpr int NT = 64 * WM * WN, RSTEP = NT / 8;  // threads; rows staged per pass (8 chunks per row)
+  constexpr int AR = BM / RSTEP, BR = BN / RSTEP;    // 16-B loads per thread per operand tile
+  constexpr int WTM = BM / WM, WTN = BN / WN;        // wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;        // 16x16 MFMA tiles per wave
+  constexpr int ABYTES = BM * 128, BBYTES = BN * 128, BUF = ABYTES + BBYTES;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+  const int wg = dev::xcd_remap(blockIdx.x, gridDim.x);
+  const int nt = wg % ntiles, g = wg / ntiles;
+  if (g >= groups) return;
+  const int n0 = nt * BN;
+  const int lc = tid & 7, lr = tid >> 3;  // staging: 16-B chunk (8 k) and first row of this thread
+  const int nk = K / kBK;
+
+  // Statistics are gathered by the C-tile readout: each thread stores a fixed 8-channel chunk
+  // column (cc) of the tiles it visits, and keeps shifted sums of those 8 channels. The shift is
+  // the block's first output row (a sample of the same channel: no cancellation when
+  // |mean| >> std), so partials across tiles simply add; threads merge once, at the end.
+  constexpr int CPR = BN / 8;                         // 16-B chunks per C-tile row
+  static_assert(NT % CPR == 0, "readout mapping needs a fixed chunk column per thread");
+  const int cc = tid % CPR;
+  float st_n = 0.f, st_s[8], st_ss[8];
+  u32x4 st_k = {0, 0, 0, 0};  // the shift, kept as the 8 packed bf16 values it came from
+#pragma unroll
+  for (int e = 0; e < 8; ++e) st_s[e] = st_ss[e] = 0.f;
+
+  const uint16_t* wrow[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) wrow[i] = Wt + (int64_t)(n0 + lr + RSTEP * i) * K + lc * 8;
+
+  u32x4 sa[AR], sb[BR];
+  // PRO: the previous BN's (scale, shift) for all K input channels, staged once into LDS after
+  // the two operand buffers (kept out of the VGPRs that the MFMA phase needs)
+  float* pro_lds = reinterpret_cast<float*>(smem + 2 * BUF);
+  if (PRO) {
+    for (int i = tid; i < 2 * K; i += NT) pro_lds[i] = pro_ss[i];
+    lds_barrier();
+  }
+  const uint16_t* arow[AR];
+  // Rows past M load row M-1 (clamped, branch-free: a per-row "load or zero" select makes hipcc
+  // branch around every load); their outputs are neither stored nor counted in the statistics.
+  auto set_rows = [&](int mt) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = (int)min<int64_t>((int64_t)mt * BM + lr + RSTEP * i, M - 1);
+      arow[i] = X + rm.in_row<STRIDED>(m) * K + lc * 8;
+    }
+  };
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) sa[i] = *reinterpret_cast<const u32x4*>(arow[i] + kt * kBK);
+#pragma unroll
+    for (int i = 0; i < BR; ++i) sb[i] = *reinterpret_cast<const u32x4*>(wrow[i] + kt * kBK);
+  };
+  auto store = [&](int buf, int kt) {
+    uint8_t* A = smem + buf * BUF;
+    uint8_t* B = A + ABYTES;
+    if (PRO) {  // previous BN's apply + ReLU on this thread's 8 input channels
+      const int k0 = kt * kBK + lc * 8;
+      float sc[8], sh[8];
+      dev::Vec8<float>::ld(pro_lds + k0, sc);
+      dev::Vec8<float>::ld(pro_lds + K + k0, sh);
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float lo = fmaxf(fmaf(__uint_as_float(sa[i][q] << 16), sc[2 * q], sh[2 * q]), 0.f);
+          const float hi = fmaxf(fmaf(__uint_as_float(sa[i][q] & 0xffff0000u), sc[2 * q + 1], sh[2 * q + 1]), 0.f);
+          sa[i][q] = dev::pack_bf16x2(lo, hi);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < AR; ++i) *reinterpret_cast<u32x4*>(A + swz(lr + RSTEP * i, lc)) = sa[i];
+#pragma unroll
+    for (int i = 0; i < BR; ++i) *reinterpret_cast<u32x4*>(B + swz(lr + RSTEP * i, lc)) = sb[i];
+  };
+
+  set_rows(g);
+  load(0);
+  for (int mt = g; mt < mtiles; mt += groups) {
+    const int64_t m0 = (int64_t)mt * BM;
+    const int next = mt + groups;
+    store(0, 0);
+    lds_barrier();
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      // issue the next K-tile's loads — or, on the last K-tile, the NEXT M-tile's first loads,
+      // so they are in flight during these MFMAs and the whole epilogue below
+      if (kt + 1 < nk) {
+        load(kt + 1);
+      } else if (next < mtiles) {
+        set_rows(next);
+        load(0);
+      }
+      const uint8_t* A = smem + cur * BUF;
+      const uint8_t* B = A + ABYTES;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int ch = s * 4 + (lane >> 4);
+        bf16x8 a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          a[i] = *reinterpret_cast<const bf16x8*>(A + swz(wm * WTM + i * 16 + (lane & 15), ch));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          b[j] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WTN + j * 16 + (lane & 15), ch));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+      if (kt + 1 < nk) store(cur ^ 1, kt + 1);
+      lds_barrier();
+    }
+
+    // ---- epilogue: round to bf16 (the stored values are what BN normalizes) ----
+    const int rows_valid = (int)min<int64_t>(BM, M - m0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = bf16_round(acc[i][j][r]);
+
+    // ---- store Y through LDS: C tile [BM][BN] bf16, rows padded 16 B, then 16-B global stores ----
+    constexpr int CST = BN * 2 + 16;
+    uint8_t* Cs = smem;  // the K loop ended with a barrier: the operand buffers are free
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+          const int col = wn * WTN + j * 16 + (lane & 15);
+          *reinterpret_cast<uint16_t*>(Cs + row * CST + col * 2) =
+              (uint16_t)(__float_as_uint(acc[i][j][r]) >> 16);  // exact: already bf16-rounded
+        }
+    lds_barrier();
+    if (STATS && mt == g) st_k = *reinterpret_cast<const u32x4*>(Cs + cc * 16);  // row 0: always valid
+#pragma unroll
+    for (int q = tid; q < BM * CPR; q += NT) {
+      const int row = q / CPR;
+      if (row < rows_valid) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
+        if (NTSTORE) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + (m0 + row) * N + n0 + cc * 8));
+        else *reinterpret_cast<u32x4*>(Y + (m0 + row) * N + n0 + cc * 8) = v;
+        if (STATS) {
+          st_n += 1.f;
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const float d0 = __uint_as_float(v[h] << 16) - __uint_as_float(st_k[h] << 16);
+            const float d1 = __uint_as_float(v[h] & 0xffff0000u) - __uint_as_float(st_k[h] & 0xffff0000u);
+            st_s[2 * h] += d0;
+            st_s[2 * h + 1] += d1;
+            st_ss[2 * h] = fmaf(d0, d0, st_ss[2 * h]);
+            st_ss[2 * h + 1] = fmaf(d1, d1, st_ss[2 * h + 1]);
+          }
+        }
+      }
+    }
+    lds_barrier();  // Cs aliases the operand buffers the next tile stores into
+  }
+
+  if (STATS) {
+    // per thread (n, mean, M2) of its 8 channels, Chan-merged over the lanes sharing cc (xor over
+    // the lane bits above log2(CPR)), then over the waves through LDS
+    float mean[8], m2[8], n = st_n;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float k = __uint_as_float((e & 1) ? (st_k[e >> 1] & 0xffff0000u) : (st_k[e >> 1] << 16));
+      mean[e] = n > 0.f ? k + st_s[e] / n : 0.f;
+      m2[e] = n > 0.f ? fmaxf(st_ss[e] - st_s[e] * st_s[e] / n, 0.f) : 0.f;
+    }
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1) {
+      const float nb = __shfl_xor(n, o, 64), nn = n + nb;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float mb = __shfl_xor(mean[e], o, 64), m2b = __shfl_xor(m2[e], o, 64);
+        if (nn > 0.f) {
+          const float d = mb - mean[e];
+          mean[e] += d * (nb / nn);
+          m2[e] += m2b + d * d * (n * nb / nn);
+        }
+      }
+      n = nn;
+    }
+    constexpr int NW = NT / 64;
+    float* red = reinterpret_cast<float*>(smem);  // [NW][3][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wid * 3 + 0) * BN + cc * 8 + e] = n;
+        red[(wid * 3 + 1) * BN + cc * 8 + e] = mean[e];
+        red[(wid * 3 + 2) * BN + cc * 8 + e] = m2[e];
+      }
+    }
+    lds_barrier();
+    for (int c = tid; c < BN; c += NT) {
+      float tn = 0.f, tm = 0.f, t2 = 0.f;
+      for (int w = 0; w < NW; ++w) {
+        const float nb = red[(w * 3 + 0) * BN + c], nn = tn + nb;
+        if (nb > 0.f) {
+          const float d = red[(w * 3 + 1) * BN + c] - tm;
+          tm += d * (nb / nn);
+          t2 += red[(w * 3 + 2) * BN + c] + d * d * (tn * nb / nn);
+        }
+        tn = nn;
+      }
+      part[((int64_t)g * 3 + 0) * N + n0 + c] = tn;
+      part[((int64_t)g * 3 + 1) * N + n0 + c] = tm;
+      part[((int64_t)g * 3 + 2) * N + n0 + c] = t2;
+    }
+  }
+}
+
+// Per channel: Chan-merge the groups' (count, mean, M2), then the BN coefficients and the
+// running-stat update (same outputs as the stats finalize of batch_norm.hip). One 64-lane wave
+// per channel; lanes stride over the groups, then a shuffle butterfly of pairwise merges.
+template <typename W>
+__global__ __launch_bounds__(64) void bn_partial_finalize_kernel(
+    const float* __restrict__ part, int groups, int C, int64_t M, const W* __restrict__ weight,
+    const W* __restrict__ bias, W* running_mean, W* running_var, const int64_t* nbt, float momentum, bool cma,
+    float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale,
+    float* __restrict__ shift) {
+  const int c = blockIdx.x, lane = threadIdx.x;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int gi = lane; gi < groups; gi += 64) {
+    const float nb = part[((int64_t)gi * 3 + 0) * C + c];
+    if (nb <= 0.f) continue;
+    const float mb = part[((int64_t)gi * 3 + 1) * C + c], m2b = part[((int64_t)gi * 3 + 2) * C + c];
+    const float nn = n + nb, d = mb - mean;
+    mean += d * (nb / nn);
+    m2 += m2b + d * d * (n * nb / nn);
+    n = nn;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float nb = __shfl_xor(n, o, 64), mb = __shfl_xor(mean, o, 64), m2b = __shfl_xor(m2, o, 64);
+    const float nn = n + nb;
+    if (nn > 0.f) {
+      const float d = mb - mean;
+      mean += d * (nb / nn);
+      m2 += m2b + d * d * (n * nb / nn);
+    }
+    n = nn;
+  }
+  if (lane != 0) return;
+  const float var = fmaxf(m2 / (float)M, 0.f);
+  const float inv = rsqrtf(var + eps);
+  mean_out[c] = mean;
+  invstd_out[c] = inv;
+  const float gm = weight ? dev::Elem<W, float>::ld(weight, c) : 1.f;
+  const float bb = bias ? dev::Elem<W, float>::ld(bias, c) : 0.f;
+  scale[c] = gm * inv;
+  shift[c] = bb - mean * gm * inv;
+  if (running_mean) {
+    float mom = momentum;
+    if (cma && nbt) mom = 1.f / (float)(nbt[0] + 1);
+    const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
+    dev::Elem<W, float>::st(running_mean, c, (1.f - mom) * dev::Elem<W, float>::ld(running_mean, c) + mom * mean);
+    dev::Elem<W, float>::st(running_var, c, (1.f - mom) * dev::Elem<W, float>::ld(running_var, c) + mom * unbiased);
+  }
+}
+
+int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch_gemm(bool pro, bool stats, dim3 grid, size_t lds, hipStream_t s, const uint16_t* x, const uint16_t* w,
+                 uint16_t* y, int64_t M, int N, int K, RowMap rm, const float* pss, float* part, int mt, int nt,
+                 int groups) {
+  auto go = [&](auto kern) {
+    static size_t lds_set = 0;  // per kernel instantiation: opt in to > 64 KB of dynamic LDS once
+    if (lds > 65536 && lds > lds_set) {
+      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      lds_set = lds;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, s, x, w, y, M, N, K, rm, pss, part, mt, nt, groups);
+  };
+#define XDDP_G(P, S)                                                                                       \
+  if (rm.stride > 1) go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, true>);                                   \
+  else go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, false>)
+  if (pro) { if (stats) XDDP_G(true, true); else XDDP_G(true, false); }
+  else { if (stats) XDDP_G(false, true); else XDDP_G(false, false); }
+#undef XDDP_G
+  XDDP_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace
+
+// x: [B, K, IH, IW] channels_last bf16; w: [N, K, 1, 1] bf16 (contiguous == [N][K]).
+// prologue_ss: optional float [2, K] (scale, shift) -> op(x) = relu(x*scale + shift).
+// Returns (y [B, N, OH, OW] channels_last, partials [groups, 3, N] or undefined).
+std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride,
+                                     const c10::optional<at::Tensor>& prologue_ss, bool stats) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16, "conv1x1_gemm: x must be 4-D bf16 on GPU");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv1x1_gemm: x must be channels_last");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 1 && w.size(3) == 1 && w.scalar_type() == at::kBFloat16,
+              "conv1x1_gemm: w must be [N, K, 1, 1] bf16");
+  TORCH_CHECK(stride >= 1, "conv1x1_gemm: bad stride");
+  const int64_t B = x.size(0), K = x.size(1), IH = x.size(2), IW = x.size(3), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "conv1x1_gemm: channel mismatch");
+  TORCH_CHECK(K % kBK == 0 && N % 64 == 0, "conv1x1_gemm: needs Cin % 64 == 0 and Cout % 64 == 0");
+  auto wc = w.contiguous();  // [N][K] row-major for either weight memory format (1x1: same bytes)
+  const int64_t OH = (IH - 1) / stride + 1, OW = (IW - 1) / stride + 1;
+  const int64_t M = B * OH * OW;
+  TORCH_CHECK(M > 0 && M < (int64_t(1) << 31), "conv1x1_gemm: bad M");
+  const bool pro = prologue_ss.has_value() && prologue_ss->defined();
+  if (pro) TORCH_CHECK(prologue_ss->scalar_type() == at::kFloat && prologue_ss->numel() == 2 * K &&
+                           prologue_ss->is_contiguous(), "conv1x1_gemm: prologue scale/shift must be float [2, K]");
+  auto y = at::empty({B, N, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  const int BM = 128, BN = (N % 128 == 0) ? 128 : 64;
+  const int mtiles = (int)((M + BM - 1) / BM), ntiles = (int)(N / BN);
+  // 2-3 blocks per CU resident (LDS 48-64 KB, <= 128 VGPRs): size the grid to a few rounds
+  static const int blocks_per_cu = [] {
+    const char* e = std::getenv("XDDP_GEMM_BLOCKS_PER_CU");
+    return e ? std::max(1, std::atoi(e)) : 2;  // persistent: one resident round (2 blocks per CU) measured best
+  }();
+  const int target = num_cus() * blocks_per_cu;
+  int groups = std::max(1, std::min(mtiles, (target + ntiles - 1) / ntiles));
+  at::Tensor part = stats ? at::empty({groups, 3, N}, x.options().dtype(at::kFloat)) : at::Tensor();
+  RowMap rm{(int)OH, (int)OW, (int)IH, (int)IW, (int)stride};
+  const dim3 grid(groups * ntiles);
+  const size_t lds = 2 * (size_t)(BM + BN) * 128 + (pro ? 2 * K * sizeof(float) : 0);
+  const auto* xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  const auto* wp = reinterpret_cast<const uint16_t*>(wc.data_ptr());
+  auto* yp = reinterpret_cast<uint16_t*>(y.data_ptr());
+  const float* pss = pro ? prologue_ss->data_ptr<float>() : nullptr;
+  float* pp = stats ? part.data_ptr<float>() : nullptr;
+  if (BN == 128)
+    launch_gemm<128, 128, 4, 2>(pro, stats, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,
+                          groups);
+  else
+    launch_gemm<128, 64, 8, 1>(pro, stats, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,
+                         groups);
+  return {y, part};
+}
+
+// partials [groups, 3, N] -> (mean, invstd, scale_shift [2, N]); updates running stats.
+std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M,
+                                               const c10::optional<at::Tensor>& weight,
+                                               const c10::optional<at::Tensor>& bias,
+                                               const c10::optional<at::Tensor>& running_mean,
+                                               const c10::optional<at::Tensor>& running_var,
+                                               const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
+                                               bool cumulative, double eps) {
+  TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.size(1) == 3 && part.scalar_type() == at::kFloat,
+              "bn_stats_from_partials: partials must be float [groups, 3, C]");
+  const int groups = (int)part.size(0), C = (int)part.size(2);
+  auto fopt = part.options();
+  auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), ss = at::empty({2, C}, fopt);
+  auto stream = c10::hip::getCurrentHIPStream(part.device().index()).stream();
+  auto opt = [](const c10::optional<at::Tensor>& t) { return t.has_value() && t->defined(); };
+  const auto wdt = opt(weight) ? weight->scalar_type() : (opt(running_mean) ? running_mean->scalar_type() : at::kFloat);
+  auto go = [&](auto tag) {
+    using W = decltype(tag);
+    auto P = [&](const c10::optional<at::Tensor>& t) { return opt(t) ? reinterpret_cast<W*>(t->data_ptr()) : nullptr; };
+    hipLaunchKernelGGL((bn_partial_finalize_kernel<W>), dim3(C), dim3(64), 0, stream, part.data_ptr<float>(), groups,
+                       C, M, P(weight), P(bias), P(running_mean), P(running_var),
+                       opt(num_batches_tracked) ? num_batches_tracked->data_ptr<int64_t>() : nullptr, (float)momentum,
+                       cumulative, (float)eps, mean.data_ptr<float>(), invstd.data_ptr<float>(), ss.data_ptr<float>(),
+                       ss.data_ptr<float>() + C);
+    XDDP_HIP_CHECK(hipGetLastError());
+  };
+  switch (wdt) {
+    case at::kFloat: go(float{}); break;
+    case at::kBFloat16: go(dev::bf16_t{}); break;
+    case at::kHalf: go(dev::f16_t{}); break;
+    default: TORCH_CHECK(false, "bn_stats_from_partials: unsupported weight dtype");
+  }
+  return {mean, invstd, ss};
+}
+
+}  // namespace kernels
+}  // namespace xddp

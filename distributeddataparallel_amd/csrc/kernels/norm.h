@@ -20,6 +20,18 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy, const at::Tensor& x, c
                                     const at::Tensor& invstd, const c10::optional<at::Tensor>& ss, bool relu,
                                     bool need_dres, bool need_dweight, const c10::optional<at::Tensor>& dy2,
                                     const c10::optional<at::Tensor>& mask_bits);
+std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, const c10::optional<at::Tensor>& residual,
+                                 bool relu, bool save_mask, const c10::optional<at::Tensor>& num_batches_tracked);
+// 1x1 conv as an MFMA GEMM with BN prologue (previous BN's apply+ReLU) / epilogue (stats partials)
+std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride,
+                                     const c10::optional<at::Tensor>& prologue_ss, bool stats);
+std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M,
+                                               const c10::optional<at::Tensor>& weight,
+                                               const c10::optional<at::Tensor>& bias,
+                                               const c10::optional<at::Tensor>& running_mean,
+                                               const c10::optional<at::Tensor>& running_var,
+                                               const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
+                                               bool cumulative, double eps);
 std::vector<at::Tensor> ln_forward(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
                                    const c10::optional<at::Tensor>& beta, double eps, bool rms);
 std::vector<at::Tensor> ln_backward(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& gamma,

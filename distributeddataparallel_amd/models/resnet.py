@@ -26,6 +26,13 @@ def conv1x1(i, o, stride=1):
     return nn.Conv2d(i, o, 1, stride=stride, bias=False)
 
 
+def _conv_bn_fusion() -> bool:
+    """XDDP_CONV_BN_FUSION=0 turns off the 1x1-conv + BN-statistics fusion (A/B switch)."""
+    import os
+
+    return os.environ.get("XDDP_CONV_BN_FUSION", "1") != "0"
+
+
 def _bn_relu(norm_layer, c):
     """Return (bn, act). A fused norm layer (``fuses_relu``) absorbs the ReLU."""
     bn = norm_layer(c)
@@ -84,6 +91,14 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         x, xr = x if isinstance(x, tuple) else (x, x)  # (main, residual-path alias) from a fused producer
+        if self._fused_add and _conv_bn_fusion() and self.training:
+            # 1x1 convs with the BN statistics in the conv's MFMA epilogue (ops/conv_bn.py)
+            from ..ops.conv_bn import conv1x1_bn_act
+
+            identity = xr if self.downsample is None else conv1x1_bn_act(xr, self.downsample[0], self.downsample[1])
+            out = conv1x1_bn_act(x, self.conv1, self.bn1, relu=True)
+            out = self.act2(self.bn2(self.conv2(out)))
+            return conv1x1_bn_act(out, self.conv3, self.bn3, residual=identity, relu=True, dual_output=True)
         identity = xr if self.downsample is None else self.downsample(xr)
         out = self.act1(self.bn1(self.conv1(x)))
         out = self.act2(self.bn2(self.conv2(out)))

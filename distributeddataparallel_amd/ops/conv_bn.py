@@ -1,0 +1,81 @@
+"""1x1 convolution + BatchNorm(+residual)(+ReLU) with the BN statistics computed in the conv's
+epilogue (``csrc/kernels/conv_gemm.hip``: an MFMA GEMM on gfx950).
+
+In the reference stack every BatchNorm after a conv re-reads the conv output for its batch
+statistics. For the ResNet-50 1x1 convs the GEMM that produces the
+output also reduces it per channel, so the stats pass disappears; the apply pass (scale/shift,
+residual, ReLU, ReLU bit mask) and the whole backward reuse the fused-BN kernels. The conv
+backward (dgrad, wgrad) goes to MIOpen through ``aten::convolution_backward``.
+
+Parameters and buffers stay in the original ``nn.Conv2d`` / ``FusedBatchNorm2d`` modules, so
+state_dict layout and DDP bucketing are unchanged.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from .._native import load
+
+__all__ = ["conv1x1_bn_act", "conv_bn_supported"]
+
+
+class _Conv1x1BN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, residual, relu, dual,
+                stride):
+        C = load()
+        ctx.set_materialize_grads(False)
+        y, part = C.conv1x1_gemm(x, w, stride, None, True)
+        M = y.numel() // y.size(1)
+        mean, invstd, ss = C.bn_stats_from_partials(part, M, weight, bias, running_mean, running_var, nbt, momentum,
+                                                    cma, eps)
+        keep_mask = relu and residual is not None
+        out, bits = C.bn_apply(y, ss, residual, relu, keep_mask, nbt)
+        ctx.relu, ctx.has_res, ctx.stride = relu, residual is not None, stride
+        ctx.save_for_backward(x, w, y, bits if keep_mask else None, weight, mean, invstd, ss)
+        if dual:  # two consumers: gradients arrive separately and are summed in the BN backward kernel
+            return out, out.view_as(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout, dout2=None):
+        C = load()
+        x, w, y, bits, weight, mean, invstd, ss = ctx.saved_tensors
+        if dout is None:
+            dout, dout2 = dout2, None
+        if dout is None:
+            return (None,) * 14
+        need_bn_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        dy, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu,
+                                               ctx.has_res and ctx.needs_input_grad[10], need_bn_w, dout2, bits)
+        s = ctx.stride
+        dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
+                                                        [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+        return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
+                None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None)
+
+
+def conv_bn_supported(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module) -> bool:
+    """Whether the fused kernel covers this (input, conv, bn) triple; otherwise use conv then bn."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0
+            and conv.kernel_size == (1, 1) and conv.padding == (0, 0) and conv.dilation == (1, 1)
+            and conv.groups == 1 and conv.bias is None and conv.stride[0] == conv.stride[1]
+            and conv.weight.dtype == torch.bfloat16 and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0
+            and bn.training and bn.track_running_stats and bn.momentum is not None
+            and getattr(bn, "fuses_relu", False))
+
+
+def conv1x1_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, residual: Optional[torch.Tensor] = None,
+                   relu: bool = False, dual_output: bool = False):
+    """``relu(bn(conv(x)) [+ residual])`` with BN statistics from the conv epilogue when supported."""
+    if not conv_bn_supported(x, conv, bn) or (residual is not None and not (
+            residual.shape[0] == x.shape[0] and residual.dtype == x.dtype
+            and residual.is_contiguous(memory_format=torch.channels_last))):
+        return bn(conv(x), residual=residual, relu=relu, dual_output=dual_output)
+    return _Conv1x1BN.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                            bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), residual, relu,
+                            dual_output, int(conv.stride[0]))

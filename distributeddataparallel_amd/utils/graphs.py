@@ -31,6 +31,13 @@ class GraphedTrainStep:
         # a stream is capturing; with benchmark mode torch resolves each conv once through the
         # Find API during warmup and replays the cached algorithm inside the capture.
         torch.backends.cudnn.benchmark = True
+        # Deterministic algorithms only inside the graph: MIOpen's split-K weight-gradient kernels
+        # accumulate with atomics into an output that a separate zero-fill prepares; on some boxes
+        # Find picked such a solution and replays accumulated into stale values (inf updates in
+        # tests/test_ddp_gpu.py::test_graphed_train_step_matches_eager). The flag is part of torch's
+        # algorithm-cache key, so it only has to hold for warmup + capture.
+        prev_det = torch.backends.cudnn.deterministic
+        torch.backends.cudnn.deterministic = True
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         if hasattr(model, "_rebind_grad_accumulators"):
@@ -47,10 +54,13 @@ class GraphedTrainStep:
         optimizer.zero_grad(set_to_none=set_to_none)
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: the communicator's watchdog thread keeps polling live (non-captured) work
-        with torch.cuda.graph(self.graph, stream=side, capture_error_mode="thread_local"):
-            self.static_loss = loss_fn(model(self.static_input), self.static_target)
-            self.static_loss.backward()
-            optimizer.step()
+        try:
+            with torch.cuda.graph(self.graph, stream=side, capture_error_mode="thread_local"):
+                self.static_loss = loss_fn(model(self.static_input), self.static_target)
+                self.static_loss.backward()
+                optimizer.step()
+        finally:
+            torch.backends.cudnn.deterministic = prev_det
 
     def __call__(self, inputs: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         if inputs.data_ptr() != self.static_input.data_ptr():
