@@ -31,6 +31,9 @@ using dev::Vec8;
 namespace {
 
 constexpr int kBlock = 256;
+#ifndef XDDP_BN_NT
+#define XDDP_BN_NT 1  // non-temporal (streaming) stores for the activation-sized outputs
+#endif
 
 struct Geo {
   int tx, ty;       // lanes across channel-vectors, lanes down rows
@@ -236,7 +239,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
       }
       a[j] = o;
     }
-    Vec8<T>::st(y + e, a);
+    if (XDDP_BN_NT) dev::st8_stream(y + e, a); else Vec8<T>::st(y + e, a);
     if (RELU && mbits) mbits[v] = (uint8_t)bits;
   }
 }
@@ -299,7 +302,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
       for (int j = 0; j < 8; ++j) g[j] = ((b >> j) & 1u) ? g[j] : 0.f;
     }
     if (WG) {
-      Vec8<T>::st(gout + r * C + c0, g);
+      if (XDDP_BN_NT) dev::st8_stream(gout + r * C + c0, g); else Vec8<T>::st(gout + r * C + c0, g);
       Vec8<T>::rt(g);  // the elementwise pass sees g at storage precision: keep the sums consistent
     }
 #pragma unroll
@@ -404,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_elem_kernel(const T* __restrict
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = ((b >> j) & 1u) ? g[j] : 0.f;
     }
-    if (DRES) Vec8<T>::st(dres + e, g);
+    if (DRES) { if (XDDP_BN_NT) dev::st8_stream(dres + e, g); else Vec8<T>::st(dres + e, g); }
     // per-channel coefficients as 16-B vector loads (L1/L2 resident; C*16 B per array)
     float k1[8], k2[8], k3[8], mu[8], out[8];
     Vec8<float>::ld(coef + c0, k1);
@@ -413,7 +416,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_elem_kernel(const T* __restrict
     Vec8<float>::ld(mean + c0, mu);
 #pragma unroll
     for (int j = 0; j < 8; ++j) out[j] = fmaf(k1[j], g[j], fmaf(k2[j], a[j] - mu[j], k3[j]));
-    Vec8<T>::st(dx + e, out);
+    if (XDDP_BN_NT) dev::st8_stream(dx + e, out); else Vec8<T>::st(dx + e, out);
   }
 }
 

@@ -126,6 +126,14 @@ struct Vec8<bf16_t> {
     for (int j = 0; j < 4; ++j) a[j] = pack_bf16x2((float)v[2 * j], (float)v[2 * j + 1]);
     *reinterpret_cast<u32x4*>(p) = a;
   }
+  // streaming store: a write-once activation does not displace re-read data from L2 / MALL
+  template <typename C>
+  static __device__ __forceinline__ void st_nt(bf16_t* p, const C (&v)[8]) {
+    u32x4 a;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = pack_bf16x2((float)v[2 * j], (float)v[2 * j + 1]);
+    __builtin_nontemporal_store(a, reinterpret_cast<u32x4*>(p));
+  }
   static __device__ __forceinline__ void rt(float (&v)[8]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -163,6 +171,13 @@ struct Vec8<f16_t> {
     }
   }
 };
+
+// Non-temporal store where the dtype has one (bf16: the activation dtype of the hot path).
+template <typename T, typename C>
+__device__ __forceinline__ void st8_stream(T* p, const C (&v)[8]) {
+  if constexpr (__is_same(T, bf16_t)) Vec8<bf16_t>::st_nt(p, v);
+  else Vec8<T>::st(p, v);
+}
 
 // ---- reductions over a 64-lane wavefront ------------------------------------------
 template <typename T>
