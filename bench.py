@@ -45,6 +45,20 @@ def _install_miopen_tuning():
 
 _install_miopen_tuning()
 
+
+def _graph_safe_miopen():
+    """--graphs 1: MIOpen's implicit-GEMM solvers are not replay-safe for the captured stem conv on
+    ROCm 7.0 (utils/graphs.py); MIOpen reads the switch once, so set it before torch loads."""
+    argv = sys.argv[1:]
+    for i, a in enumerate(argv):
+        v = a.split("=", 1)[1] if a.startswith("--graphs=") else (argv[i + 1] if a == "--graphs" and i + 1 < len(argv)
+                                                                   else None)
+        if v is not None and v != "0":
+            os.environ.setdefault("MIOPEN_DEBUG_CONV_IMPLICIT_GEMM", "0")
+
+
+_graph_safe_miopen()
+
 import torch  # noqa: E402
 import torch.nn as nn  # noqa: E402
 import torch.nn.functional as F  # noqa: E402

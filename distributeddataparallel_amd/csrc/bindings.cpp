@@ -325,6 +325,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       }, py::arg("params"), py::arg("grads"), py::arg("momentum_bufs"), py::arg("lr"), py::arg("momentum"),
       py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"), py::arg("maximize"),
       py::arg("first_step"), py::arg("grad_scale") = py::none());
+  m.def("fused_sgd_master", [](const std::vector<at::Tensor>& p, const std::vector<at::Tensor>& g,
+                               const std::vector<at::Tensor>& b, const std::vector<at::Tensor>& q, double lr,
+                               double momentum, double dampening, double wd, bool nesterov, bool maximize, bool first,
+                               c10::optional<at::Tensor> gs) {
+        if (p.empty()) return;
+        kernels::fused_sgd_master(p, g, b, q, lr, momentum, dampening, wd, nesterov, maximize, first, gs,
+                                  stream_of(p[0]));
+      }, py::arg("masters"), py::arg("grads"), py::arg("momentum_bufs"), py::arg("model_params"), py::arg("lr"),
+      py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"), py::arg("maximize"),
+      py::arg("first_step"), py::arg("grad_scale") = py::none());
   m.def("fused_adam", [](const std::vector<at::Tensor>& p, const std::vector<at::Tensor>& g,
                          const std::vector<at::Tensor>& m1, const std::vector<at::Tensor>& m2,
                          const std::vector<at::Tensor>& masters, double lr, double b1, double b2, double eps,

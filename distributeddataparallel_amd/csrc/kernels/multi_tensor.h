@@ -37,6 +37,10 @@ void mt_l2norm(const std::vector<at::Tensor>& tensors, const at::Tensor& out, do
 void mt_nonfinite(const std::vector<at::Tensor>& tensors, const at::Tensor& out, hipStream_t stream);
 
 // Fused SGD over a tensor list (torch.optim.SGD semantics).
+void fused_sgd_master(const std::vector<at::Tensor>& masters, const std::vector<at::Tensor>& grads,
+                      const std::vector<at::Tensor>& momentum_bufs, const std::vector<at::Tensor>& model_params,
+                      double lr, double momentum, double dampening, double weight_decay, bool nesterov, bool maximize,
+                      bool first_step, const c10::optional<at::Tensor>& grad_scale, hipStream_t stream);
 void fused_sgd(const std::vector<at::Tensor>& params, const std::vector<at::Tensor>& grads,
                const std::vector<at::Tensor>& momentum_bufs, double lr, double momentum, double dampening,
                double weight_decay, bool nesterov, bool maximize, bool first_step,

@@ -428,6 +428,102 @@ __global__ __launch_bounds__(kThreads) void sgd_kernel(SegTable<3> t, float lr, 
   }
 }
 
+// Master-weight SGD: slots {fp32 master, grad, fp32 momentum, low-precision model param}. The
+// updated master is rounded into the model's param in the same pass (no second launch that
+// re-reads the masters).
+template <typename G, typename Mdl, bool VEC, bool MOM>
+__global__ __launch_bounds__(kThreads) void sgd_master_kernel(SegTable<4> t, float lr, float momentum,
+                                                              float dampening, float wd, bool nesterov,
+                                                              bool maximize, bool first, const float* gs) {
+  const int s = find_seg(t, blockIdx.x);
+  const int64_t blk = blockIdx.x - (s ? t.blk_end[s - 1] : 0);
+  float* p = reinterpret_cast<float*>(t.ptr[0][s]);
+  const G* g = reinterpret_cast<const G*>(t.ptr[1][s]);
+  float* buf = reinterpret_cast<float*>(t.ptr[2][s]);
+  Mdl* q = reinterpret_cast<Mdl*>(t.ptr[3][s]);
+  const int64_t n = t.numel[s];
+  const float gscale = (gs ? *gs : 1.f) * (maximize ? -1.f : 1.f);
+  const int64_t base = blk * kChunk;
+  auto upd = [&](float& pv, float gv, float& bv) {
+    float d = gv * gscale;
+    if (wd != 0.f) d = fmaf(wd, pv, d);
+    if (MOM) {
+      bv = first ? d : fmaf(momentum, bv, (1.f - dampening) * d);
+      d = nesterov ? fmaf(momentum, bv, d) : bv;
+    }
+    pv = fmaf(-lr, d, pv);
+  };
+#pragma unroll
+  for (int it = 0; it < kIters; ++it) {
+    const int64_t i = base + ((int64_t)it * kThreads + threadIdx.x) * 8;
+    if (VEC && i + 8 <= n) {
+      float pv[8], gv[8], bv[8];
+      Vec8<float>::ld(p + i, pv);
+      Vec8<G>::ld(g + i, gv);
+      if (MOM && !first) Vec8<float>::ld(buf + i, bv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) upd(pv[j], gv[j], bv[j]);
+      Vec8<float>::st(p + i, pv);
+      if (MOM) Vec8<float>::st(buf + i, bv);
+      Vec8<Mdl>::st(q + i, pv);
+    } else {
+      for (int64_t k = i; k < i + 8 && k < n; ++k) {
+        float pv = p[k], gv = Elem<G, float>::ld(g, k), bv = 0.f;
+        if (MOM && !first) bv = buf[k];
+        upd(pv, gv, bv);
+        p[k] = pv;
+        if (MOM) buf[k] = bv;
+        Elem<Mdl, float>::st(q, k, pv);
+      }
+    }
+  }
+}
+
+void fused_sgd_master(const std::vector<at::Tensor>& masters, const std::vector<at::Tensor>& grads,
+                      const std::vector<at::Tensor>& momentum_bufs, const std::vector<at::Tensor>& model_params,
+                      double lr, double momentum, double dampening, double weight_decay, bool nesterov, bool maximize,
+                      bool first_step, const c10::optional<at::Tensor>& grad_scale, hipStream_t stream) {
+  TORCH_CHECK(masters.size() == grads.size() && masters.size() == model_params.size(), "SGD list length mismatch");
+  const bool mom = momentum != 0.0;
+  TORCH_CHECK(!mom || momentum_bufs.size() == masters.size(), "momentum buffers missing");
+  if (masters.empty()) return;
+  const auto gt = grads[0].scalar_type(), mt = model_params[0].scalar_type();
+  std::vector<std::array<void*, 4>> ptrs;
+  std::vector<int64_t> numels;
+  bool vec = true;
+  for (size_t i = 0; i < masters.size(); ++i) {
+    TORCH_CHECK(masters[i].scalar_type() == at::kFloat, "master weights must be fp32");
+    TORCH_CHECK(grads[i].scalar_type() == gt && model_params[i].scalar_type() == mt, "mixed dtypes in SGD list");
+    check_dense_pair(masters[i], grads[i]);
+    check_dense_pair(masters[i], model_params[i]);
+    void* b = nullptr;
+    if (mom) {
+      TORCH_CHECK(momentum_bufs[i].scalar_type() == at::kFloat, "momentum buffers must be fp32");
+      check_dense_pair(masters[i], momentum_bufs[i]);
+      b = momentum_bufs[i].data_ptr();
+    }
+    vec = vec && aligned16(masters[i].data_ptr()) && aligned16(grads[i].data_ptr()) && (!mom || aligned16(b)) &&
+          aligned16(model_params[i].data_ptr());
+    ptrs.push_back({masters[i].data_ptr(), const_cast<void*>(grads[i].data_ptr()), b, model_params[i].data_ptr()});
+    numels.push_back(masters[i].numel());
+  }
+  const float* gs = scale_ptr(grad_scale);
+  TORCH_CHECK(mt == at::kBFloat16 || mt == at::kHalf, "master-weight SGD: model params must be bf16/fp16");
+  XDDP_DISPATCH_FLOAT(gt, G, {
+    auto go = [&](auto tag) {
+      using Mdl = decltype(tag);
+      for_each_table<4>(ptrs, numels, [&](const SegTable<4>& t, int32_t nb) {
+        auto k = vec ? (mom ? sgd_master_kernel<G, Mdl, true, true> : sgd_master_kernel<G, Mdl, true, false>)
+                     : (mom ? sgd_master_kernel<G, Mdl, false, true> : sgd_master_kernel<G, Mdl, false, false>);
+        hipLaunchKernelGGL(k, dim3(nb), dim3(kThreads), 0, stream, t, (float)lr, (float)momentum, (float)dampening,
+                           (float)weight_decay, nesterov, maximize, first_step, gs);
+        XDDP_HIP_CHECK(hipGetLastError());
+      });
+    };
+    if (mt == at::kBFloat16) go(bf16_t{}); else go(f16_t{});
+  });
+}
+
 void fused_sgd(const std::vector<at::Tensor>& params, const std::vector<at::Tensor>& grads,
                const std::vector<at::Tensor>& momentum_bufs, double lr, double momentum, double dampening,
                double weight_decay, bool nesterov, bool maximize, bool first_step,

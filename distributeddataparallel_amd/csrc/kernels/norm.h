@@ -42,6 +42,11 @@ std::vector<at::Tensor> maxpool_forward(const at::Tensor& x, int64_t k, int64_t 
 at::Tensor maxpool_backward(const at::Tensor& dy, const at::Tensor& idx, const at::Tensor& x_like, int64_t k,
                             int64_t stride, int64_t pad, const c10::optional<at::Tensor>& dy2);
 
+// transformer elementwise kernels (csrc/kernels/transformer.hip)
+at::Tensor rope(const at::Tensor& x, const at::Tensor& cosv, const at::Tensor& sinv, bool backward);
+at::Tensor swiglu_forward(const at::Tensor& a, const at::Tensor& b);
+std::vector<at::Tensor> swiglu_backward(const at::Tensor& g, const at::Tensor& a, const at::Tensor& b);
+
 void bind_norm_kernels(pybind11::module_& m);
 
 }  // namespace kernels

@@ -21,6 +21,9 @@ void bind_norm_kernels(py::module_& m) {
   m.def("bn_stats_from_partials", &bn_stats_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"),
         py::arg("momentum"), py::arg("cumulative"), py::arg("eps"));
+  m.def("rope", &rope, py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("backward") = false);
+  m.def("swiglu_forward", &swiglu_forward, py::arg("a"), py::arg("b"));
+  m.def("swiglu_backward", &swiglu_backward, py::arg("grad"), py::arg("a"), py::arg("b"));
   m.def("maxpool_forward", &maxpool_forward, py::arg("x"), py::arg("kernel"), py::arg("stride"), py::arg("pad"));
   m.def("maxpool_backward", &maxpool_backward, py::arg("dy"), py::arg("idx"), py::arg("x_like"), py::arg("kernel"),
         py::arg("stride"), py::arg("pad"), py::arg("dy2") = py::none());

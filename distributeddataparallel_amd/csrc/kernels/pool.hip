@@ -115,6 +115,71 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
   }
 }
 
+// ResNet stem specialisation (k=3, s=2, p=1): one lane per 2x2 input quad (h = 2t, 2t+1;
+// w = 2u, 2u+1) x 8 channels. The quad is covered by exactly the windows (t|t+1, u|u+1), so each
+// window's dy/argmax is read once per quad instead of once per covered pixel (2.25x fewer gathered
+// reads than the per-pixel gather above).
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_bwd_k3s2p1_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                                 const uint8_t* __restrict__ idx,
+                                                                 T* __restrict__ dx, int N, int H, int W, int C,
+                                                                 int OH, int OW) {
+  const int cv = C / 8;
+  const int QH = (H + 1) / 2, QW = (W + 1) / 2;
+  const int64_t total = (int64_t)N * QH * QW * cv;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(q % cv) * 8;
+    int64_t r = q / cv;
+    const int u = (int)(r % QW);
+    r /= QW;
+    const int t = (int)(r % QH);
+    const int n = (int)(r / QH);
+    float acc[4][8];  // [h1*2 + w1][channel]
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[a][j] = 0.f;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const int oh = t + dh, ow = u + dw;
+        if (oh >= OH || ow >= OW) continue;
+        const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c0;
+        const uint64_t packed = *reinterpret_cast<const uint64_t*>(idx + o);
+        float g[8];
+        Vec8<T>::ld(dy + o, g);
+        if (dy2) {
+          float g2[8];
+          Vec8<T>::ld(dy2 + o, g2);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] += g2[j];
+        }
+        // input (2t + a, 2u + b) sits at window offset kh = 1 + a - 2*dh, kw = 1 + b - 2*dw
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int kh = 1 + a - 2 * dh, kw = 1 + b - 2 * dw;
+            if (kh < 0 || kw < 0) continue;  // compile-time after unrolling
+            const int pos = kh * 3 + kw;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if ((int)((packed >> (8 * j)) & 0xff) == pos) acc[a * 2 + b][j] += g[j];
+          }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int h = 2 * t + a, w = 2 * u + b;
+        if (h < H && w < W) dev::st8_stream(dx + (((int64_t)n * H + h) * W + w) * C + c0, acc[a * 2 + b]);
+      }
+  }
+}
+
 template <typename F>
 void dispatch_pool(at::ScalarType st, F&& f) {
   switch (st) {
@@ -169,6 +234,15 @@ at::Tensor maxpool_backward(const at::Tensor& dy_in, const at::Tensor& idx, cons
   if (total == 0) return dx;
   dispatch_pool(dy.scalar_type(), [&](auto tag) {
     using T = decltype(tag);
+    if (k == 3 && stride == 2 && pad == 1) {
+      const int64_t quads = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+      hipLaunchKernelGGL((maxpool_bwd_k3s2p1_kernel<T>), dim3(grid_for(quads)), dim3(256), 0, stream,
+                         reinterpret_cast<const T*>(dy.data_ptr()),
+                         dy2.defined() ? reinterpret_cast<const T*>(dy2.data_ptr()) : nullptr,
+                         idx.data_ptr<uint8_t>(), reinterpret_cast<T*>(dx.data_ptr()), N, H, W, C, OH, OW);
+      XDDP_HIP_CHECK(hipGetLastError());
+      return;
+    }
     hipLaunchKernelGGL((maxpool_bwd_kernel<T>), dim3(grid_for(total)), dim3(256), 0, stream,
                        reinterpret_cast<const T*>(dy.data_ptr()),
                        dy2.defined() ? reinterpret_cast<const T*>(dy2.data_ptr()) : nullptr, idx.data_ptr<uint8_t>(),

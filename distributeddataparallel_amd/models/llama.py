@@ -1,13 +1,16 @@
 """Llama-3 decoder (8B config) — BASELINE.json config 5 (Llama-3-8B bf16 pure DDP).
 
-RMSNorm on xddp's fused kernel, rotary embeddings from a precomputed cos/sin table,
-grouped-query attention through ``F.scaled_dot_product_attention`` (causal), SwiGLU MLP.
-Pure DDP sizing on MI355X: 8.03B params → 16 GB bf16 params + 16 GB bf16
-grads (bucket views) + 96 GB fp32 master/Adam ≈ 128 GB of the 288 GB HBM3E, leaving room
-for activations (optionally checkpointed per layer).
+RMSNorm on xddp's fused kernel, rotary embeddings and the SwiGLU gate on fused HIP kernels
+(``ops/transformer.py``: one pass each instead of ~10 / 3 PyTorch ops), grouped-query attention
+through ``F.scaled_dot_product_attention`` (causal; K/V heads are shared by ``enable_gqa`` rather
+than materialised by ``repeat_interleave``). Pure DDP sizing on MI355X: 8.03B
+params → 16 GB bf16 params + 16 GB bf16 grads (bucket views) + 96 GB fp32 master/Adam ≈ 128 GB
+of the 288 GB HBM3E, leaving room for activations (optionally checkpointed per layer).
+``XDDP_FUSED_TRANSFORMER=0`` selects the PyTorch reference ops (A/B and parity tests).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -15,6 +18,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.layer_norm import FusedRMSNorm
+from ..ops.transformer import rope, rope_reference, swiglu
 
 __all__ = ["LlamaConfig", "Llama", "llama3_8b", "llama_tiny"]
 
@@ -33,19 +37,15 @@ class LlamaConfig:
     checkpoint_activations: bool = False
 
 
+def _fused() -> bool:
+    return os.environ.get("XDDP_FUSED_TRANSFORMER", "1") != "0"
+
+
 def _rope_table(head_dim, max_len, theta, device=None):
     inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float32, device=device) / head_dim))
     t = torch.arange(max_len, dtype=torch.float32, device=device)
     f = torch.outer(t, inv)
     return torch.cos(f), torch.sin(f)
-
-
-def _apply_rope(x, cos, sin):
-    # x: [B, H, S, Dh]; rotate pairs (even, odd)
-    x1, x2 = x[..., 0::2].float(), x[..., 1::2].float()
-    c, s = cos[None, None], sin[None, None]
-    out = torch.stack([x1 * c - x2 * s, x1 * s + x2 * c], dim=-1).flatten(-2)
-    return out.to(x.dtype)
 
 
 class Attention(nn.Module):
@@ -60,15 +60,18 @@ class Attention(nn.Module):
 
     def forward(self, x, cos, sin):
         B, S, _ = x.shape
-        q = self.wq(x).view(B, S, self.h, self.hd).transpose(1, 2)
-        k = self.wk(x).view(B, S, self.kvh, self.hd).transpose(1, 2)
+        rot = rope if _fused() else rope_reference
+        # rotate in the projection's [B, S, H, Dh] layout, then move heads forward for attention
+        q = rot(self.wq(x).view(B, S, self.h, self.hd), cos, sin).transpose(1, 2)
+        k = rot(self.wk(x).view(B, S, self.kvh, self.hd), cos, sin).transpose(1, 2)
         v = self.wv(x).view(B, S, self.kvh, self.hd).transpose(1, 2)
-        q, k = _apply_rope(q, cos, sin), _apply_rope(k, cos, sin)
-        if self.kvh != self.h:
+        if self.kvh != self.h and not _fused():
             rep = self.h // self.kvh
             k = k.repeat_interleave(rep, dim=1)
             v = v.repeat_interleave(rep, dim=1)
-        o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+            o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        else:
+            o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=self.kvh != self.h)
         return self.wo(o.transpose(1, 2).reshape(B, S, -1))
 
 
@@ -80,6 +83,8 @@ class FeedForward(nn.Module):
         self.w3 = nn.Linear(cfg.dim, cfg.ffn_dim, bias=False)
 
     def forward(self, x):
+        if _fused():
+            return self.w2(swiglu(self.w1(x), self.w3(x)))
         return self.w2(F.silu(self.w1(x)) * self.w3(x))
 
 
@@ -104,16 +109,24 @@ class Llama(nn.Module):
         self.layers = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layers)])
         self.norm = FusedRMSNorm(cfg.dim, eps=cfg.norm_eps)
         self.output = nn.Linear(cfg.dim, cfg.vocab_size, bias=False)
-        cos, sin = _rope_table(cfg.dim // cfg.n_heads, cfg.max_seq_len, cfg.rope_theta)
-        self.register_buffer("rope_cos", cos, persistent=False)
-        self.register_buffer("rope_sin", sin, persistent=False)
+        # rotary tables stay fp32 whatever dtype the model is cast to: a plain attribute cache
+        # per device, not a buffer (``.to(bfloat16)`` would round the angles' cos/sin, and DDP
+        # would broadcast the tables before every forward)
+        self._rope = {}
         for m in self.modules():
             if isinstance(m, (nn.Linear, nn.Embedding)):
                 nn.init.normal_(m.weight, std=0.02)
 
+    def _tables(self, device):
+        key = str(device)
+        if key not in self._rope:
+            cos, sin = _rope_table(self.cfg.dim // self.cfg.n_heads, self.cfg.max_seq_len, self.cfg.rope_theta,
+                                   device=device)
+            self._rope[key] = (cos.contiguous(), sin.contiguous())
+        return self._rope[key]
+
     def forward(self, tokens):
-        S = tokens.shape[1]
-        cos, sin = self.rope_cos[:S].float(), self.rope_sin[:S].float()
+        cos, sin = self._tables(tokens.device)
         h = self.tok_embeddings(tokens)
         for blk in self.layers:
             if self.cfg.checkpoint_activations and self.training:

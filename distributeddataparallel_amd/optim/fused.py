@@ -73,11 +73,12 @@ class FusedSGD(Optimizer):
             for (dev, pdt, gdt, first, use_master), (ps, gs, bufs, orig) in buckets.items():
                 mom = group["momentum"]
                 bufs = bufs if mom != 0 else []
-                if dev.type == "cuda":
+                if dev.type == "cuda" and use_master:  # one pass: update fp32 masters, round into the params
+                    C.fused_sgd_master(ps, gs, bufs, orig, group["lr"], mom, group["dampening"],
+                                       group["weight_decay"], group["nesterov"], group["maximize"], first, grad_scale)
+                elif dev.type == "cuda":
                     C.fused_sgd(ps, gs, bufs, group["lr"], mom, group["dampening"], group["weight_decay"],
                                 group["nesterov"], group["maximize"], first, grad_scale)
-                    if use_master:
-                        C.mt_scale_copy(ps, orig, 1.0)
                 else:
                     self._cpu_step(ps, gs, bufs, group, first, grad_scale)
                     if use_master:

@@ -10,10 +10,17 @@ Requirements (checked where possible):
   * buckets already rebuilt — done by the eager warmup steps run here before capture;
   * an optimizer whose step is pure device work (``FusedSGD``, torch SGD/momentum);
   * the Reducer's collectives go to the RCCL comm stream, which joins the capture through an
-    event wait and rejoins the compute stream before the end of the step.
+    event wait and rejoins the compute stream before the end of the step;
+  * ``MIOPEN_DEBUG_CONV_IMPLICIT_GEMM=0`` in the process environment: with MIOpen's implicit-GEMM
+    solvers a captured ResNet stem conv (3 input channels) gave NaN weight gradients from the
+    second replay on, on some MI355X boxes — reproduced with a plain torch model, torch SGD and
+    ``torch.cuda.graph`` (no xddp code), and not narrowed to one solver switch
+    (scripts/dbg/graph_dbg.py, scripts/dbg/gpu_graph_env.sh).
 """
 from __future__ import annotations
 
+import os
+import warnings
 from typing import Callable
 
 import torch
@@ -31,13 +38,11 @@ class GraphedTrainStep:
         # a stream is capturing; with benchmark mode torch resolves each conv once through the
         # Find API during warmup and replays the cached algorithm inside the capture.
         torch.backends.cudnn.benchmark = True
-        # Deterministic algorithms only inside the graph: MIOpen's split-K weight-gradient kernels
-        # accumulate with atomics into an output that a separate zero-fill prepares; on some boxes
-        # Find picked such a solution and replays accumulated into stale values (inf updates in
-        # tests/test_ddp_gpu.py::test_graphed_train_step_matches_eager). The flag is part of torch's
-        # algorithm-cache key, so it only has to hold for warmup + capture.
-        prev_det = torch.backends.cudnn.deterministic
-        torch.backends.cudnn.deterministic = True
+        if os.environ.get("MIOPEN_DEBUG_CONV_IMPLICIT_GEMM") != "0":
+            warnings.warn("HIP-graph capture with MIOpen implicit-GEMM conv solvers enabled: on ROCm 7.0 a "
+                          "captured ResNet stem conv returned NaN gradients from the second replay on "
+                          "(reproduced without xddp). Set MIOPEN_DEBUG_CONV_IMPLICIT_GEMM=0 before the process "
+                          "starts (bench.py --graphs 1 does).")
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         if hasattr(model, "_rebind_grad_accumulators"):
@@ -54,13 +59,10 @@ class GraphedTrainStep:
         optimizer.zero_grad(set_to_none=set_to_none)
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: the communicator's watchdog thread keeps polling live (non-captured) work
-        try:
-            with torch.cuda.graph(self.graph, stream=side, capture_error_mode="thread_local"):
-                self.static_loss = loss_fn(model(self.static_input), self.static_target)
-                self.static_loss.backward()
-                optimizer.step()
-        finally:
-            torch.backends.cudnn.deterministic = prev_det
+        with torch.cuda.graph(self.graph, stream=side, capture_error_mode="thread_local"):
+            self.static_loss = loss_fn(model(self.static_input), self.static_target)
+            self.static_loss.backward()
+            optimizer.step()
 
     def __call__(self, inputs: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         if inputs.data_ptr() != self.static_input.data_ptr():

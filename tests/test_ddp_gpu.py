@@ -127,7 +127,28 @@ def test_resnet50_fused_bn_matches_torch_bn(pg):
         torch.backends.cudnn.deterministic = False
 
 
-def test_graphed_train_step_matches_eager(pg):
+def test_graphed_train_step_matches_eager():
+    """Runs _graphed_train_step_check in a fresh process with MIOPEN_DEBUG_CONV_IMPLICIT_GEMM=0
+    (MIOpen reads it once per process; its implicit-GEMM solvers gave NaN stem-conv gradients on
+    replay, without any xddp code involved — utils/graphs.py)."""
+    import subprocess
+    import sys
+
+    code = ("import tests.test_ddp_gpu as t, os\n"
+            "from distributeddataparallel_amd import distributed as dist\n"
+            "from distributeddataparallel_amd.utils.spawn import free_port\n"
+            "os.environ['MASTER_ADDR'] = '127.0.0.1'; os.environ['MASTER_PORT'] = str(free_port())\n"
+            "dist.init_process_group('rccl', rank=0, world_size=1, device_id=0)\n"
+            "t._graphed_train_step_check()\n"
+            "dist.destroy_process_group()\n"
+            "print('graphed ok')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MIOPEN_DEBUG_CONV_IMPLICIT_GEMM="0", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "graphed ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def _graphed_train_step_check():
     """HIP-graph capture of the whole DDP step (fwd, bwd + bucket all-reduce, FusedSGD): every
     replayed step equals an eager step taken from the same state (the eager model is re-synced
     from the graphed one before each step, in place, so MIOpen's run-to-run nondeterminism does
