@@ -45,20 +45,6 @@ def _install_miopen_tuning():
 
 _install_miopen_tuning()
 
-
-def _graph_safe_miopen():
-    """--graphs 1: MIOpen's implicit-GEMM solvers are not replay-safe for the captured stem conv on
-    ROCm 7.0 (utils/graphs.py); MIOpen reads the switch once, so set it before torch loads."""
-    argv = sys.argv[1:]
-    for i, a in enumerate(argv):
-        v = a.split("=", 1)[1] if a.startswith("--graphs=") else (argv[i + 1] if a == "--graphs" and i + 1 < len(argv)
-                                                                   else None)
-        if v is not None and v != "0":
-            os.environ.setdefault("MIOPEN_DEBUG_CONV_IMPLICIT_GEMM", "0")
-
-
-_graph_safe_miopen()
-
 import torch  # noqa: E402
 import torch.nn as nn  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
@@ -271,7 +257,8 @@ def main():
                 "parallelism": f"dp{world}",
                 "impl": args.impl,
                 "norm": args.norm,
-                "optimizer": ("SGD(momentum=0.9, wd=1e-4) fp32 master weights" if args.model.startswith("resnet")
+                "optimizer": ("SGD(momentum=0.9, wd=1e-4) fp32 master weights"
+                              if args.model.startswith("resnet") or args.model == "simplecnn"
                               else "AdamW(wd=0.1) fp32 master weights"),
                 "channels_last": bool(args.channels_last),
                 "comm_dtype": args.comm_dtype,

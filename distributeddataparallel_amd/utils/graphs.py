@@ -11,16 +11,17 @@ Requirements (checked where possible):
   * an optimizer whose step is pure device work (``FusedSGD``, torch SGD/momentum);
   * the Reducer's collectives go to the RCCL comm stream, which joins the capture through an
     event wait and rejoins the compute stream before the end of the step;
-  * ``MIOPEN_DEBUG_CONV_IMPLICIT_GEMM=0`` in the process environment: with MIOpen's implicit-GEMM
-    solvers a captured ResNet stem conv (3 input channels) gave NaN weight gradients from the
-    second replay on, on some MI355X boxes — reproduced with a plain torch model, torch SGD and
-    ``torch.cuda.graph`` (no xddp code), and not narrowed to one solver switch
-    (scripts/dbg/graph_dbg.py, scripts/dbg/gpu_graph_env.sh).
+  * MIOpen in immediate mode (``cudnn.benchmark`` off during warmup + capture; the solutions are
+    compiled by the eager warmup steps and replayed from the graph). With Find/benchmark mode a
+    captured ResNet stem conv (3 input channels) got MIOpen's ASM V4R1 implicit-GEMM solver on
+    some MI355X boxes and returned NaN weight gradients from the second replay on — reproduced with
+    a plain torch model, torch SGD and ``torch.cuda.graph`` (no xddp code); disabling those
+    solvers or benchmark mode fixes it (scripts/dbg/graph_dbg.py, scripts/dbg/gpu_graph_env.sh).
+    ``XDDP_GRAPH_CUDNN_BENCHMARK=1`` opts back into Find mode.
 """
 from __future__ import annotations
 
 import os
-import warnings
 from typing import Callable
 
 import torch
@@ -34,15 +35,8 @@ class GraphedTrainStep:
         self.model, self.optimizer, self.loss_fn = model, optimizer, loss_fn
         self.static_input = example_input.clone()
         self.static_target = example_target.clone()
-        # MIOpen's immediate-mode path compiles/looks up solutions per call, which is illegal while
-        # a stream is capturing; with benchmark mode torch resolves each conv once through the
-        # Find API during warmup and replays the cached algorithm inside the capture.
-        torch.backends.cudnn.benchmark = True
-        if os.environ.get("MIOPEN_DEBUG_CONV_IMPLICIT_GEMM") != "0":
-            warnings.warn("HIP-graph capture with MIOpen implicit-GEMM conv solvers enabled: on ROCm 7.0 a "
-                          "captured ResNet stem conv returned NaN gradients from the second replay on "
-                          "(reproduced without xddp). Set MIOPEN_DEBUG_CONV_IMPLICIT_GEMM=0 before the process "
-                          "starts (bench.py --graphs 1 does).")
+        prev_bench = torch.backends.cudnn.benchmark
+        torch.backends.cudnn.benchmark = os.environ.get("XDDP_GRAPH_CUDNN_BENCHMARK", "0") == "1"
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         if hasattr(model, "_rebind_grad_accumulators"):
@@ -59,10 +53,13 @@ class GraphedTrainStep:
         optimizer.zero_grad(set_to_none=set_to_none)
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: the communicator's watchdog thread keeps polling live (non-captured) work
-        with torch.cuda.graph(self.graph, stream=side, capture_error_mode="thread_local"):
-            self.static_loss = loss_fn(model(self.static_input), self.static_target)
-            self.static_loss.backward()
-            optimizer.step()
+        try:
+            with torch.cuda.graph(self.graph, stream=side, capture_error_mode="thread_local"):
+                self.static_loss = loss_fn(model(self.static_input), self.static_target)
+                self.static_loss.backward()
+                optimizer.step()
+        finally:
+            torch.backends.cudnn.benchmark = prev_bench
 
     def __call__(self, inputs: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         if inputs.data_ptr() != self.static_input.data_ptr():
