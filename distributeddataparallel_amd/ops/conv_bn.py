@@ -4,14 +4,16 @@ epilogue (``csrc/kernels/conv_gemm.hip``: an MFMA GEMM on gfx950).
 In the reference stack every BatchNorm after a conv re-reads the conv output for its batch
 statistics. For the ResNet-50 1x1 convs the GEMM that produces the
 output also reduces it per channel, so the stats pass disappears; the apply pass (scale/shift,
-residual, ReLU, ReLU bit mask) and the whole backward reuse the fused-BN kernels. The conv
-backward (dgrad, wgrad) goes to MIOpen through ``aten::convolution_backward``.
+residual, ReLU, ReLU bit mask) and the BN backward reuse the fused-BN kernels. The conv input
+gradient of stride-1 convs is the same MFMA GEMM on (dY, Wᵀ); the weight gradient (and strided
+input gradients) go to MIOpen through ``aten::convolution_backward``.
 
 Parameters and buffers stay in the original ``nn.Conv2d`` / ``FusedBatchNorm2d`` modules, so
 state_dict layout and DDP bucketing are unchanged.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -52,10 +54,27 @@ class _Conv1x1BN(torch.autograd.Function):
         dy, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu,
                                                ctx.has_res and ctx.needs_input_grad[10], need_bn_w, dout2, bits)
         s = ctx.stride
-        dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
-                                                        [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = None
+        if need_x and s == 1 and _dgrad_gemm():
+            # dX[M, K] = dY[M, N] · W[N, K] is the same NT GEMM on (dY, Wᵀ): 35 % less time than
+            # MIOpen's 1x1 dgrad over the ResNet-50 shapes (scripts/dgrad_bench.py)
+            n_out, k_in = w.shape[0], w.shape[1]
+            wt = w.reshape(n_out, k_in).t().contiguous().view(k_in, n_out, 1, 1)
+            dx = C.conv1x1_gemm(dy, wt, 1, None, False)[0]
+            need_x = False
+        if need_x or need_w:
+            gx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
+                                                            [need_x, need_w, False])
+            dx = gx if need_x else dx
+            dw = gw if need_w else None
         return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
                 None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None)
+
+
+def _dgrad_gemm() -> bool:
+    """XDDP_CONV_DGRAD_GEMM=0 sends the stride-1 input gradient back to MIOpen (A/B switch)."""
+    return os.environ.get("XDDP_CONV_DGRAD_GEMM", "1") != "0"
 
 
 def conv_bn_supported(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module) -> bool:
