@@ -342,6 +342,167 @@ __global__ __launch_bounds__(64) void bn_partial_finalize_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Weight gradient of the 1x1 conv: dW[N, K] = sum_m dY[m, n] · X[m, k]  (a "TN" GEMM whose
+// reduction runs over the M = batch·OH·OW pixel rows). Both operands are staged row-major
+// ([64 pixel rows][n or k], as they lie in HBM) and read into MFMA fragments with gfx950's
+// transposing LDS read ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group, each lane
+// receiving one column), so no register or LDS transposition pass is needed. The reduction is
+// split over M across blocks (fp32 slabs), then one small kernel sums the slabs into dW.
+// LDS rows are padded by 32 B so the 4 rows of a transposed read fall on distinct banks.
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
+template <int TN, int TK, bool STRIDED>
+__global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* __restrict__ dY,
+                                                                const uint16_t* __restrict__ X,
+                                                                float* __restrict__ ws, int M, int N, int K,
+                                                                RowMap rm, int ntiles, int ktiles, int mchunk) {
+  constexpr int BM = 64;                       // pixel rows per step (two 32-deep MFMA k-steps)
+  constexpr int SA = TN * 2 + 32, SB = TK * 2 + 32;
+  constexpr int ABYTES = BM * SA, BUF = ABYTES + BM * SB;
+  constexpr int CA = TN / 8, CB = TK / 8;      // 16-B chunks per staged row
+  constexpr int LA = BM * CA / 256, LB = BM * CB / 256;
+  constexpr int WTN = TN / 2, WTK = TK / 2, FN = WTN / 16, FK = WTK / 16;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wn = wid >> 1, wk = wid & 1;
+  const int tiles = ntiles * ktiles;
+  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
+  const int sidx = bid / tiles, tile = bid % tiles;  // neighbours share the pixel range (L2 reuse)
+  const int n0 = (tile % ntiles) * TN, k0 = (tile / ntiles) * TK;
+  const int m_begin = sidx * mchunk, m_end = min(M, m_begin + mchunk);
+
+  u32x4 sa[LA], sb[LB];
+  auto load = [&](int m) {
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int q = tid + 256 * i, row = q / CA, c = q - (q / CA) * CA;
+      const int mm = m + row;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(dY + (int64_t)min(mm, M - 1) * N + n0 + c * 8);
+      sa[i] = mm < m_end ? v : u32x4{0, 0, 0, 0};  // rows past the range contribute zero
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int q = tid + 256 * i, row = q / CB, c = q - (q / CB) * CB;
+      const int mm = m + row;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(X + rm.in_row<STRIDED>(min(mm, M - 1)) * K + k0 + c * 8);
+      sb[i] = mm < m_end ? v : u32x4{0, 0, 0, 0};
+    }
+  };
+  auto store = [&](int buf) {
+    uint8_t* A = smem + buf * BUF;
+    uint8_t* B = A + ABYTES;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int q = tid + 256 * i, row = q / CA, c = q - (q / CA) * CA;
+      *reinterpret_cast<u32x4*>(A + row * SA + c * 16) = sa[i];
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int q = tid + 256 * i, row = q / CB, c = q - (q / CB) * CB;
+      *reinterpret_cast<u32x4*>(B + row * SB + c * 16) = sb[i];
+    }
+  };
+
+  f32x4 acc[FN][FK];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read addressing: lane (4q + p) of its 16-lane group addresses row q, columns 4p..4p+3
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  if (m_begin < m_end) {
+    load(m_begin);
+    store(0);
+    lds_barrier();
+    int cur = 0;
+    for (int m = m_begin; m < m_end; m += BM) {
+      const bool more = m + BM < m_end;
+      if (more) load(m + BM);  // in flight during the MFMAs below
+      const uint8_t* A = smem + cur * BUF;
+      const uint8_t* B = A + ABYTES;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int r0 = s2 * 32 + 8 * g + q4;
+        bf16x8 a[FN], b[FK];
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const int col = wn * WTN + i * 16 + 4 * p4;
+          const v4s lo = lds_tr16(A + r0 * SA + col * 2), hi = lds_tr16(A + (r0 + 4) * SA + col * 2);
+          const v4s v8[2] = {lo, hi};
+          a[i] = __builtin_bit_cast(bf16x8, v8);
+        }
+#pragma unroll
+        for (int j = 0; j < FK; ++j) {
+          const int col = wk * WTK + j * 16 + 4 * p4;
+          const v4s lo = lds_tr16(B + r0 * SB + col * 2), hi = lds_tr16(B + (r0 + 4) * SB + col * 2);
+          const v4s v8[2] = {lo, hi};
+          b[j] = __builtin_bit_cast(bf16x8, v8);
+        }
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+      if (more) store(cur ^ 1);
+      lds_barrier();
+      cur ^= 1;
+    }
+  }
+  // fp32 slab of this pixel range: ws[sidx][n][k]; lane holds rows n = (lane>>4)*4 + r, col k = lane&15
+  float* out = ws + (int64_t)sidx * N * K;
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4 + r;
+        const int k = k0 + wk * WTK + j * 16 + (lane & 15);
+        out[(int64_t)n * K + k] = acc[i][j][r];
+      }
+}
+
+// dW = sum over the S slabs, cast to the weight dtype; 4 elements per lane.
+template <typename W>
+__global__ __launch_bounds__(512) void wgrad_reduce_kernel(const float* __restrict__ ws, int S, int64_t nk,
+                                                           W* __restrict__ dw) {
+  // block = 64 float4 columns x 8 slab groups: the slab sum is split 8 ways (4 independent
+  // accumulators each) so a small weight with hundreds of slabs is not one long dependent chain
+  __shared__ f32x4 red[8][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t v = (int64_t)blockIdx.x * 64 + c;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+  if (v * 4 < nk) {
+    const float* p = ws + v * 4;
+    int s = g;
+    for (; s + 24 < S; s += 32) {
+      a0 += *reinterpret_cast<const f32x4*>(p + (int64_t)s * nk);
+      a1 += *reinterpret_cast<const f32x4*>(p + (int64_t)(s + 8) * nk);
+      a2 += *reinterpret_cast<const f32x4*>(p + (int64_t)(s + 16) * nk);
+      a3 += *reinterpret_cast<const f32x4*>(p + (int64_t)(s + 24) * nk);
+    }
+    for (; s < S; s += 8) a0 += *reinterpret_cast<const f32x4*>(p + (int64_t)s * nk);
+  }
+  red[g][c] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (g == 0 && v * 4 < nk) {
+    f32x4 acc = red[0][c];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) acc += red[i][c];
+    dev::Elem<W, float>::st(dw, v * 4 + 0, acc.x);
+    dev::Elem<W, float>::st(dw, v * 4 + 1, acc.y);
+    dev::Elem<W, float>::st(dw, v * 4 + 2, acc.z);
+    dev::Elem<W, float>::st(dw, v * 4 + 3, acc.w);
+  }
+}
+
 int num_cus() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -422,6 +583,68 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
     launch_gemm<128, 64, 8, 1>(pro, stats, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,
                          groups);
   return {y, part};
+}
+
+
+// dY: [B, N, OH, OW] channels_last bf16; x: [B, K, IH, IW] channels_last bf16 (the conv input);
+// returns dW [N, K, 1, 1] in w_like's dtype (fp32 accumulation, split over pixel rows).
+at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like) {
+  const auto wdtype = w_like.scalar_type();
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16,
+              "conv1x1_wgrad: bf16 GPU tensors expected");
+  TORCH_CHECK(dy.dim() == 4 && x.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv1x1_wgrad: channels_last 4-D tensors expected");
+  const int64_t B = x.size(0), K = x.size(1), IH = x.size(2), IW = x.size(3), N = dy.size(1);
+  const int64_t OH = (IH - 1) / stride + 1, OW = (IW - 1) / stride + 1;
+  TORCH_CHECK(dy.size(0) == B && dy.size(2) == OH && dy.size(3) == OW, "conv1x1_wgrad: dy/x shape mismatch");
+  TORCH_CHECK(N % 64 == 0 && K % 64 == 0, "conv1x1_wgrad: channel counts must be multiples of 64");
+  const int64_t M = B * OH * OW;
+  TORCH_CHECK(M > 0 && M < (int64_t(1) << 31), "conv1x1_wgrad: bad M");
+  const int TN = N % 128 == 0 ? 128 : 64, TK = K % 128 == 0 ? 128 : 64;
+  const int ntiles = (int)(N / TN), ktiles = (int)(K / TK), tiles = ntiles * ktiles;
+  const int64_t steps = (M + 63) / 64;
+  int S = (int)std::max<int64_t>(1, std::min<int64_t>(steps, (int64_t)num_cus() * 2 / tiles));
+  const int64_t mchunk = ((steps + S - 1) / S) * 64;
+  S = (int)((M + mchunk - 1) / mchunk);
+  auto ws = at::empty({S, N, K}, dy.options().dtype(at::kFloat));
+  auto dw = at::empty({N, K, 1, 1}, dy.options().dtype(wdtype));
+  auto stream = c10::hip::getCurrentHIPStream(dy.device().index()).stream();
+  RowMap rm{(int)OH, (int)OW, (int)IH, (int)IW, (int)stride};
+  const size_t lds = 2 * (size_t)64 * ((TN * 2 + 32) + (TK * 2 + 32));
+  auto go = [&](auto kern) {
+    static size_t lds_set = 0;
+    if (lds > 65536 && lds > lds_set) {
+      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      lds_set = lds;
+    }
+    hipLaunchKernelGGL(kern, dim3(S * tiles), dim3(256), lds, stream,
+                       reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                       ws.data_ptr<float>(), (int)M, (int)N, (int)K, rm, ntiles, ktiles, (int)mchunk);
+    XDDP_HIP_CHECK(hipGetLastError());
+  };
+  const bool strided = stride > 1;
+#define XDDP_W(A, Bk) \
+  if (strided) go(conv1x1_wgrad_kernel<A, Bk, true>); else go(conv1x1_wgrad_kernel<A, Bk, false>)
+  if (TN == 128 && TK == 128) { XDDP_W(128, 128); }
+  else if (TN == 128) { XDDP_W(128, 64); }
+  else if (TK == 128) { XDDP_W(64, 128); }
+  else { XDDP_W(64, 64); }
+#undef XDDP_W
+  const int64_t nk = N * K;
+  const int grid = (int)((nk / 4 + 63) / 64);
+  auto red = [&](auto tag) {
+    using W = decltype(tag);
+    hipLaunchKernelGGL((wgrad_reduce_kernel<W>), dim3(grid), dim3(512), 0, stream, ws.data_ptr<float>(), S, nk,
+                       reinterpret_cast<W*>(dw.data_ptr()));
+    XDDP_HIP_CHECK(hipGetLastError());
+  };
+  switch (wdtype) {
+    case at::kBFloat16: red(dev::bf16_t{}); break;
+    case at::kFloat: red(float{}); break;
+    case at::kHalf: red(dev::f16_t{}); break;
+    default: TORCH_CHECK(false, "conv1x1_wgrad: unsupported weight dtype");
+  }
+  return dw;
 }
 
 // partials [groups, 3, N] -> (mean, invstd, scale_shift [2, N]); updates running stats.

@@ -38,6 +38,27 @@ def test_conv1x1_gemm_matches_conv2d(b, cin, h, w, cout, s):
     torch.testing.assert_close(yp.float(), refp, rtol=1e-2, atol=1e-2 * refp.abs().max().item())
 
 
+@pytest.mark.parametrize("b,cin,h,w,cout,s,wdt", [
+    (2, 64, 14, 14, 256, 1, torch.bfloat16),    # M = 392: partial last pixel step
+    (3, 128, 9, 7, 64, 1, torch.float32),       # 64-wide tiles, fp32 weight output
+    (2, 256, 15, 15, 512, 2, torch.bfloat16),   # strided (downsample) rows, odd input size
+    (8, 64, 28, 28, 64, 1, torch.bfloat16),     # one tile, many M slabs (reduce split)
+])
+def test_conv1x1_wgrad_matches_fp32(b, cin, h, w, cout, s, wdt):
+    """dW[n, k] = sum_m dY[m, n] X[m, k] (strided pixel rows for s = 2) against fp32 torch."""
+    torch.manual_seed(2)
+    x = _x(b, cin, h, w)
+    oh, ow = (h - 1) // s + 1, (w - 1) // s + 1
+    dy = _x(b, cout, oh, ow)
+    like = torch.empty(cout, cin, 1, 1, device="cuda", dtype=wdt)
+    dw = C.conv1x1_wgrad(dy, x, s, like)
+    xs = x.float()[:, :, ::s, ::s]
+    ref = torch.einsum("bnhw,bkhw->nk", dy.float(), xs).view(cout, cin, 1, 1)
+    assert dw.shape == ref.shape and dw.dtype == wdt
+    tol = 1e-2 if wdt == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(dw.float(), ref, rtol=tol, atol=tol * ref.abs().max().item())
+
+
 @pytest.mark.parametrize("offset", [0.0, 300.0])
 def test_epilogue_stats_match_torch(offset):
     """Epilogue partials -> mean/var equal torch's over the stored bf16 output, also when
