@@ -294,24 +294,30 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
 }
 
 // Per channel: Chan-merge the groups' (count, mean, M2), then the BN coefficients and the
-// running-stat update (same outputs as the stats finalize of batch_norm.hip). One 64-lane wave
-// per channel; lanes stride over the groups, then a shuffle butterfly of pairwise merges.
+// running-stat update (same outputs as the stats finalize of batch_norm.hip). One 256-thread
+// block per channel: threads stride over the groups (element (g, q, c) at g*gs + q*ks + c*cs, so
+// both the [groups][3][C] and the group-minor [3][C][groups] layouts are read), then a shuffle
+// butterfly of pairwise merges per wave and a 4-way merge through LDS.
 template <typename W>
-__global__ __launch_bounds__(64) void bn_partial_finalize_kernel(
-    const float* __restrict__ part, int groups, int C, int64_t M, const W* __restrict__ weight,
-    const W* __restrict__ bias, W* running_mean, W* running_var, const int64_t* nbt, float momentum, bool cma,
-    float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale,
-    float* __restrict__ shift) {
-  const int c = blockIdx.x, lane = threadIdx.x;
+__global__ __launch_bounds__(256) void bn_partial_finalize_kernel(
+    const float* __restrict__ part, int groups, int C, int64_t gs, int64_t ks, int64_t cs, int64_t M,
+    const W* __restrict__ weight, const W* __restrict__ bias, W* running_mean, W* running_var, const int64_t* nbt,
+    float momentum, bool cma, float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out,
+    float* __restrict__ scale, float* __restrict__ shift) {
+  __shared__ float red[3][4];
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float* pc = part + (int64_t)c * cs;
   float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int gi = lane; gi < groups; gi += 64) {
-    const float nb = part[((int64_t)gi * 3 + 0) * C + c];
-    if (nb <= 0.f) continue;
-    const float mb = part[((int64_t)gi * 3 + 1) * C + c], m2b = part[((int64_t)gi * 3 + 2) * C + c];
-    const float nn = n + nb, d = mb - mean;
-    mean += d * (nb / nn);
-    m2 += m2b + d * d * (n * nb / nn);
-    n = nn;
+  for (int gi = tid; gi < groups; gi += 256) {
+    const float* q = pc + (int64_t)gi * gs;
+    const float nb = q[0], mb = q[ks], m2b = q[2 * ks];
+    const float nn = n + nb;
+    if (nb > 0.f) {
+      const float d = mb - mean;
+      mean += d * (nb / nn);
+      m2 += m2b + d * d * (n * nb / nn);
+      n = nn;
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -324,7 +330,23 @@ __global__ __launch_bounds__(64) void bn_partial_finalize_kernel(
     }
     n = nn;
   }
-  if (lane != 0) return;
+  if (lane == 0) {
+    red[0][wid] = n;
+    red[1][wid] = mean;
+    red[2][wid] = m2;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  n = mean = m2 = 0.f;
+  for (int w = 0; w < 4; ++w) {
+    const float nb = red[0][w], nn = n + nb;
+    if (nb > 0.f) {
+      const float d = red[1][w] - mean;
+      mean += d * (nb / nn);
+      m2 += red[2][w] + d * d * (n * nb / nn);
+      n = nn;
+    }
+  }
   const float var = fmaxf(m2 / (float)M, 0.f);
   const float inv = rsqrtf(var + eps);
   mean_out[c] = mean;
@@ -647,17 +669,21 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stri
   return dw;
 }
 
-// partials [groups, 3, N] -> (mean, invstd, scale_shift [2, N]); updates running stats.
+// partials [groups, 3, N] (or [3, N, groups] when group_minor) -> (mean, invstd, scale_shift
+// [2, N]); updates running stats.
 std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M,
                                                const c10::optional<at::Tensor>& weight,
                                                const c10::optional<at::Tensor>& bias,
                                                const c10::optional<at::Tensor>& running_mean,
                                                const c10::optional<at::Tensor>& running_var,
                                                const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
-                                               bool cumulative, double eps) {
-  TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.size(1) == 3 && part.scalar_type() == at::kFloat,
-              "bn_stats_from_partials: partials must be float [groups, 3, C]");
-  const int groups = (int)part.size(0), C = (int)part.size(2);
+                                               bool cumulative, double eps, bool group_minor) {
+  TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.size(group_minor ? 0 : 1) == 3 &&
+                  part.scalar_type() == at::kFloat && part.is_contiguous(),
+              "bn_stats_from_partials: partials must be float [groups, 3, C] (or [3, C, groups])");
+  const int groups = (int)part.size(group_minor ? 2 : 0), C = (int)part.size(group_minor ? 1 : 2);
+  const int64_t gs = group_minor ? 1 : 3 * C, ks = group_minor ? (int64_t)C * groups : C,
+                cs = group_minor ? groups : 1;
   auto fopt = part.options();
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), ss = at::empty({2, C}, fopt);
   auto stream = c10::hip::getCurrentHIPStream(part.device().index()).stream();
@@ -666,8 +692,8 @@ std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M
   auto go = [&](auto tag) {
     using W = decltype(tag);
     auto P = [&](const c10::optional<at::Tensor>& t) { return opt(t) ? reinterpret_cast<W*>(t->data_ptr()) : nullptr; };
-    hipLaunchKernelGGL((bn_partial_finalize_kernel<W>), dim3(C), dim3(64), 0, stream, part.data_ptr<float>(), groups,
-                       C, M, P(weight), P(bias), P(running_mean), P(running_var),
+    hipLaunchKernelGGL((bn_partial_finalize_kernel<W>), dim3(C), dim3(256), 0, stream, part.data_ptr<float>(), groups,
+                       C, gs, ks, cs, M, P(weight), P(bias), P(running_mean), P(running_var),
                        opt(num_batches_tracked) ? num_batches_tracked->data_ptr<int64_t>() : nullptr, (float)momentum,
                        cumulative, (float)eps, mean.data_ptr<float>(), invstd.data_ptr<float>(), ss.data_ptr<float>(),
                        ss.data_ptr<float>() + C);

@@ -25,6 +25,9 @@ std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, cons
 // 1x1 conv as an MFMA GEMM with BN prologue (previous BN's apply+ReLU) / epilogue (stats partials)
 std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride,
                                      const c10::optional<at::Tensor>& prologue_ss, bool stats);
+// 3x3 pad-1 conv (stride 1/2) as an implicit MFMA GEMM (csrc/kernels/conv3x3.hip)
+std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats);
+at::Tensor conv3x3_rot_weight(const at::Tensor& w);
 at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like);
 std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M,
                                                const c10::optional<at::Tensor>& weight,
@@ -32,7 +35,7 @@ std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M
                                                const c10::optional<at::Tensor>& running_mean,
                                                const c10::optional<at::Tensor>& running_var,
                                                const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
-                                               bool cumulative, double eps);
+                                               bool cumulative, double eps, bool group_minor);
 std::vector<at::Tensor> ln_forward(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
                                    const c10::optional<at::Tensor>& beta, double eps, bool rms);
 std::vector<at::Tensor> ln_backward(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& gamma,

@@ -18,10 +18,12 @@ void bind_norm_kernels(py::module_& m) {
         py::arg("save_mask"), py::arg("num_batches_tracked"));
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("prologue_ss"),
         py::arg("stats"));
+  m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"));
+  m.def("conv3x3_rot_weight", &conv3x3_rot_weight, py::arg("w"));
   m.def("conv1x1_wgrad", &conv1x1_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"));
   m.def("bn_stats_from_partials", &bn_stats_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"),
-        py::arg("momentum"), py::arg("cumulative"), py::arg("eps"));
+        py::arg("momentum"), py::arg("cumulative"), py::arg("eps"), py::arg("group_minor") = false);
   m.def("rope", &rope, py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("backward") = false);
   m.def("swiglu_forward", &swiglu_forward, py::arg("a"), py::arg("b"));
   m.def("swiglu_backward", &swiglu_backward, py::arg("grad"), py::arg("a"), py::arg("b"));

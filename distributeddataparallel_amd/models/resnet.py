@@ -93,11 +93,11 @@ class Bottleneck(nn.Module):
         x, xr = x if isinstance(x, tuple) else (x, x)  # (main, residual-path alias) from a fused producer
         if self._fused_add and _conv_bn_fusion() and self.training:
             # 1x1 convs with the BN statistics in the conv's MFMA epilogue (ops/conv_bn.py)
-            from ..ops.conv_bn import conv1x1_bn_act
+            from ..ops.conv_bn import conv1x1_bn_act, conv3x3_bn_relu
 
             identity = xr if self.downsample is None else conv1x1_bn_act(xr, self.downsample[0], self.downsample[1])
             out = conv1x1_bn_act(x, self.conv1, self.bn1, relu=True)
-            out = self.act2(self.bn2(self.conv2(out)))
+            out = self.act2(conv3x3_bn_relu(out, self.conv2, self.bn2))
             return conv1x1_bn_act(out, self.conv3, self.bn3, residual=identity, relu=True, dual_output=True)
         identity = xr if self.downsample is None else self.downsample(xr)
         out = self.act1(self.bn1(self.conv1(x)))

@@ -10,6 +10,11 @@ GEMM over the pixel dimension (``conv1x1_wgrad``: dYᵀ·X with transposed LDS r
 split over pixels and summed by a second kernel). Only strided input gradients go to MIOpen
 through ``aten::convolution_backward``.
 
+The ResNet bottleneck's 3x3 conv + BN + ReLU (``conv3x3_bn_relu``) runs on the implicit-GEMM
+kernel of ``csrc/kernels/conv3x3.hip`` with the same statistics epilogue; its stride-1 input
+gradient is that kernel on (dY, rot180(W)ᵀ), its weight gradient (and strided input gradient)
+stay on MIOpen.
+
 Parameters and buffers stay in the original ``nn.Conv2d`` / ``FusedBatchNorm2d`` modules, so
 state_dict layout and DDP bucketing are unchanged.
 """
@@ -23,7 +28,7 @@ import torch.nn as nn
 
 from .._native import load
 
-__all__ = ["conv1x1_bn_act", "conv_bn_supported"]
+__all__ = ["conv1x1_bn_act", "conv3x3_bn_relu", "conv_bn_supported"]
 
 
 class _Conv1x1BN(torch.autograd.Function):
@@ -79,6 +84,50 @@ class _Conv1x1BN(torch.autograd.Function):
                 None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None)
 
 
+class _Conv3x3BNReLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, stride):
+        C = load()
+        ctx.set_materialize_grads(False)
+        y, part = C.conv3x3_forward(x, w, stride, True)
+        M = y.numel() // y.size(1)
+        mean, invstd, ss = C.bn_stats_from_partials(part, M, weight, bias, running_mean, running_var, nbt, momentum,
+                                                    cma, eps, True)
+        out, _ = C.bn_apply(y, ss, None, True, False, nbt)
+        ctx.stride = stride
+        ctx.save_for_backward(x, w, y, weight, mean, invstd, ss)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        if dout is None:
+            return (None,) * 11
+        C = load()
+        x, w, y, weight, mean, invstd, ss = ctx.saved_tensors
+        need_bn_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        # ReLU mask recomputed from y·scale + shift inside the BN backward (no mask tensor kept)
+        dy, dw_bn, db_bn, _ = C.bn_backward(dout.contiguous(memory_format=torch.channels_last), y, None, weight,
+                                            mean, invstd, ss, True, False, need_bn_w, None, None)
+        s = ctx.stride
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = None
+        if need_x and s == 1:
+            dx = C.conv3x3_forward(dy, C.conv3x3_rot_weight(w), 1, False)[0]
+            need_x = False
+        if need_x or need_w:
+            gx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
+                                                            [need_x, need_w, False])
+            dx = gx if need_x else dx
+            dw = gw if need_w else None
+        return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
+                None, None, None, None, None, None, None)
+
+
+def _conv3x3() -> bool:
+    """XDDP_CONV3X3=0 sends the bottleneck 3x3 conv back to MIOpen + separate BN (A/B switch)."""
+    return os.environ.get("XDDP_CONV3X3", "1") != "0"
+
+
 def _dgrad_gemm() -> bool:
     """XDDP_CONV_DGRAD_GEMM=0 sends the stride-1 input gradient back to MIOpen (A/B switch)."""
     return os.environ.get("XDDP_CONV_DGRAD_GEMM", "1") != "0"
@@ -90,20 +139,32 @@ def _wgrad_gemm() -> bool:
 
 
 def conv_bn_supported(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module) -> bool:
-    """Whether the fused kernel covers this (input, conv, bn) triple; otherwise use conv then bn."""
+    """Whether the fused kernels cover this (input, conv, bn) triple; otherwise use conv then bn."""
+    k = conv.kernel_size
+    geometry = ((k == (1, 1) and conv.padding == (0, 0))
+                or (k == (3, 3) and conv.padding == (1, 1) and conv.stride[0] in (1, 2)
+                    and conv.weight.is_contiguous(memory_format=torch.channels_last)))
     return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
             and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0
-            and conv.kernel_size == (1, 1) and conv.padding == (0, 0) and conv.dilation == (1, 1)
+            and geometry and conv.dilation == (1, 1)
             and conv.groups == 1 and conv.bias is None and conv.stride[0] == conv.stride[1]
             and conv.weight.dtype == torch.bfloat16 and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0
             and bn.training and bn.track_running_stats and bn.momentum is not None
             and getattr(bn, "fuses_relu", False))
 
 
+def conv3x3_bn_relu(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module):
+    """``relu(bn(conv3x3(x)))`` on the implicit-GEMM kernel with BN statistics from its epilogue."""
+    if not (_conv3x3() and conv.kernel_size == (3, 3) and conv_bn_supported(x, conv, bn)):
+        return bn(conv(x), relu=True)
+    return _Conv3x3BNReLU.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), int(conv.stride[0]))
+
+
 def conv1x1_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, residual: Optional[torch.Tensor] = None,
                    relu: bool = False, dual_output: bool = False):
     """``relu(bn(conv(x)) [+ residual])`` with BN statistics from the conv epilogue when supported."""
-    if not conv_bn_supported(x, conv, bn) or (residual is not None and not (
+    if conv.kernel_size != (1, 1) or not conv_bn_supported(x, conv, bn) or (residual is not None and not (
             residual.shape[0] == x.shape[0] and residual.dtype == x.dtype
             and residual.is_contiguous(memory_format=torch.channels_last))):
         return bn(conv(x), residual=residual, relu=relu, dual_output=dual_output)

@@ -1,0 +1,88 @@
+"""3x3 implicit-GEMM conv (csrc/kernels/conv3x3.hip): forward, BN-statistics epilogue, rotated
+weights for the stride-1 input gradient, and the fused conv3x3+BN+ReLU op — against plain
+PyTorch fp32 references of the same ops."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributeddataparallel_amd._native import load
+
+pytestmark = pytest.mark.gpu
+
+C = load() if torch.cuda.is_available() else None
+
+
+def _cl(t):
+    return t.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("b,cin,h,w,cout,s,off", [
+    (2, 64, 14, 14, 64, 1, 0.0),     # N = 64 tile, M = 392: partial last M-tile
+    (3, 128, 9, 7, 128, 1, 30.0),    # odd spatial size, 256x128 tile, |mean| >> std per channel
+    (2, 64, 15, 15, 256, 2, 0.0),    # strided, odd input size
+    (1, 512, 7, 7, 512, 1, 0.0),     # long reduction (72 steps), one M-tile
+    (8, 64, 40, 40, 64, 1, 0.0),     # 100 M-tiles: many stats partials
+])
+def test_conv3x3_forward_matches_conv2d(b, cin, h, w, cout, s, off):
+    torch.manual_seed(0)
+    x = _cl(torch.randn(b, cin, h, w, device="cuda") + off)
+    wt = _cl(torch.randn(cout, cin, 3, 3, device="cuda") / (9 * cin) ** 0.5)
+    y, part = C.conv3x3_forward(x, wt, s, True)
+    ref = F.conv2d(x.float(), wt.float(), stride=s, padding=1)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+    # epilogue statistics of the stored bf16 output
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, cout)
+    rm, rv = torch.zeros(cout, device="cuda"), torch.ones(cout, device="cuda")
+    nbt = torch.zeros((), dtype=torch.long, device="cuda")
+    mean, invstd, _ = C.bn_stats_from_partials(part, yf.shape[0], None, None, rm, rv, nbt, 0.1, False, 1e-5, True)
+    torch.testing.assert_close(mean, yf.mean(0), rtol=1e-5, atol=1e-4 * yf.std(0).max().item())
+    torch.testing.assert_close(1.0 / invstd ** 2 - 1e-5, yf.var(0, unbiased=False), rtol=2e-3, atol=1e-6)
+
+
+def test_conv3x3_rotated_weight_gives_input_gradient():
+    torch.manual_seed(1)
+    x = torch.randn(2, 128, 10, 11, device="cuda")
+    wt = torch.randn(64, 128, 3, 3, device="cuda") / 34
+    dy = torch.randn(2, 64, 10, 11, device="cuda")
+    rot = C.conv3x3_rot_weight(_cl(wt))
+    torch.testing.assert_close(rot.float(), _cl(wt).float().flip(2, 3).transpose(0, 1), rtol=0, atol=0)
+    dx = C.conv3x3_forward(_cl(dy), rot, 1, False)[0]
+    xr = x.to(torch.bfloat16).float().requires_grad_()
+    F.conv2d(xr, _cl(wt).float(), padding=1).backward(_cl(dy).float())
+    torch.testing.assert_close(dx.float(), xr.grad, rtol=1e-2, atol=1e-2 * xr.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv3x3_bn_relu_forward_backward(stride):
+    from distributeddataparallel_amd.ops import FusedBatchNorm2d, conv3x3_bn_relu
+
+    torch.manual_seed(2)
+    conv = torch.nn.Conv2d(64, 128, 3, stride=stride, padding=1, bias=False).cuda().to(torch.bfloat16)
+    conv = conv.to(memory_format=torch.channels_last)
+    bn = FusedBatchNorm2d(128).cuda().to(torch.bfloat16)
+    bn.relu = True
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    x = _cl(torch.randn(4, 64, 13, 13, device="cuda")).requires_grad_()
+    out = conv3x3_bn_relu(x, conv, bn)
+    g = torch.randn_like(out)
+    out.backward(g)
+    xr = x.detach().float().requires_grad_()
+    wr = conv.weight.detach().float().requires_grad_()
+    gr, br = bn.weight.detach().float().requires_grad_(), bn.bias.detach().float().requires_grad_()
+    yr = F.conv2d(xr, wr, stride=stride, padding=1)
+    yr = yr + (yr.to(torch.bfloat16).float() - yr).detach()  # the kernel normalizes the stored bf16 y
+    o = torch.relu(F.batch_norm(yr, None, None, gr, br, True, 0.1, 1e-5))
+    o.backward(g.float())
+    torch.testing.assert_close(out.float(), o.detach(), rtol=3e-2, atol=3e-2 * o.abs().max().item())
+
+    def rel(a, b):
+        return ((a.float() - b).norm() / (b.norm() + 1e-12)).item()
+
+    assert rel(x.grad, xr.grad) < 2e-2
+    assert rel(conv.weight.grad, wr.grad) < 2e-2
+    assert rel(bn.weight.grad, gr.grad) < 2e-2
+    assert rel(bn.bias.grad, br.grad) < 2e-2
+    assert int(bn.num_batches_tracked) == 1
