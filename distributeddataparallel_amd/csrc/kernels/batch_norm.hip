@@ -339,7 +339,8 @@ template <typename W>
 __global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(const float* __restrict__ part, int rblocks, int C,
                                                              int64_t M, const W* __restrict__ weight,
                                                              const float* __restrict__ invstd, W* dweight,
-                                                             W* dbias, float* __restrict__ coef) {
+                                                             W* dbias, float* __restrict__ coef,
+                                                             const float* __restrict__ fold_mean) {
   const int cv = blockIdx.x, lane = threadIdx.x;
   float acc[16];
 #pragma unroll
@@ -365,6 +366,8 @@ __global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(const float* __rest
   coef[c] = g * inv;                                   // k1
   coef[C + c] = -g * inv * inv * inv * sdx * invM;     // k2
   coef[2 * C + c] = -g * inv * sd * invM;              // k3
+  // fold_mean: dx = k1·g + k2·x + (k3 - k2·mean), the form a consumer GEMM prologue applies
+  if (fold_mean) coef[2 * C + c] -= coef[C + c] * fold_mean[c];
 }
 
 template <typename T, int MASK, bool DRES, bool DUAL>
@@ -570,7 +573,7 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
                                     const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
                                     const at::Tensor& invstd, const c10::optional<at::Tensor>& ss, bool relu,
                                     bool need_dres, bool need_dweight, const c10::optional<at::Tensor>& dy2_in,
-                                    const c10::optional<at::Tensor>& mask_bits) {
+                                    const c10::optional<at::Tensor>& mask_bits, bool coef_only) {
   check_nhwc(x);
   auto dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
   const bool dual = dy2_in.has_value() && dy2_in->defined();
@@ -588,7 +591,11 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
                              "mask bits must be uint8[M*C/8]");
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
   auto fopt = x.options().dtype(at::kFloat);
-  auto dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  // coef_only: skip the elementwise pass and return the per-channel (k1, k2, k3 - k2·mean) [3, C]
+  // in dx's slot; the gradient k1·g + k2·x + k3' is formed by the consumer (conv GEMM prologue),
+  // with g = dres (written here) or, without ReLU/second gradient, dy itself
+  if (coef_only) TORCH_CHECK(need_dres || (!relu && !dual), "bn_backward: coef_only needs g materialized");
+  auto dx = coef_only ? at::Tensor() : at::empty_like(x, at::MemoryFormat::ChannelsLast);
   at::Tensor dres = need_dres ? at::empty_like(x, at::MemoryFormat::ChannelsLast) : at::Tensor();
   const bool has_w = weight.has_value() && weight->defined();
   const auto wdt = has_w ? weight->scalar_type() : at::kFloat;
@@ -630,10 +637,13 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
                          part.data_ptr<float>(), g.rblocks, (int)C, M,
                          has_w ? reinterpret_cast<const W*>(weight->data_ptr()) : nullptr, invstd.data_ptr<float>(),
                          dw.defined() ? reinterpret_cast<W*>(dw.data_ptr()) : nullptr,
-                         db.defined() ? reinterpret_cast<W*>(db.data_ptr()) : nullptr, coef.data_ptr<float>());
+                         db.defined() ? reinterpret_cast<W*>(db.data_ptr()) : nullptr, coef.data_ptr<float>(),
+                         coef_only ? mean.data_ptr<float>() : nullptr);
       XDDP_HIP_CHECK(hipGetLastError());
       const int64_t nvec = M * C / 8;
-      if (wg) {
+      if (coef_only) {
+        // nothing more: the consumer applies the coefficients
+      } else if (wg) {
         hipLaunchKernelGGL((bn_bwd_elem_kernel<T, 0, false, false>), dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
                            reinterpret_cast<const T*>(dres.data_ptr()), nullptr,
                            reinterpret_cast<const T*>(x.data_ptr()), nullptr, nullptr,
@@ -657,7 +667,7 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
       XDDP_HIP_CHECK(hipGetLastError());
     });
   });
-  return {dx, dw, db, dres};
+  return {coef_only ? coef : dx, dw, db, dres};
 }
 
 }  // namespace kernels

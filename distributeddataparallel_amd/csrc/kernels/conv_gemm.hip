@@ -62,11 +62,14 @@ struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every st
   }
 };
 
-template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, bool STRIDED>
+// PRO: 0 = plain A; 1 = relu(A·s_k + b_k) (the previous BN's apply); 2 = a_k·A + b_k·X2 + c_k, the
+// BatchNorm-backward elementwise pass (A = masked upstream gradient, X2 = the BN input) folded
+// into the input-gradient GEMM so that gradient is never written to HBM.
+template <int BM, int BN, int WM, int WN, int PRO, bool STATS, bool STRIDED>
 __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, int64_t M, int N,
     int K, RowMap rm, const float* __restrict__ pro_ss, float* __restrict__ part, int mtiles, int ntiles,
-    int groups) {
+    int groups, const uint16_t* __restrict__ X2) {
   constexpr int NT = 64 * WM * WN, RSTEP = NT / 8;  // threads; rows staged per pass (8 chunks per row)
   constexpr int AR = BM / RSTEP, BR = BN / RSTEP;    // 16-B loads per thread per operand tile
   constexpr int WTM = BM / WM, WTN = BN / WN;        // wave tile
@@ -98,15 +101,16 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
 #pragma unroll
   for (int i = 0; i < BR; ++i) wrow[i] = Wt + (int64_t)(n0 + lr + RSTEP * i) * K + lc * 8;
 
-  u32x4 sa[AR], sb[BR];
-  // PRO: the previous BN's (scale, shift) for all K input channels, staged once into LDS after
-  // the two operand buffers (kept out of the VGPRs that the MFMA phase needs)
+  u32x4 sa[AR], sb[BR], sa2[PRO == 2 ? AR : 1];
+  // PRO: the per-input-channel coefficients for all K channels, staged once into LDS after the
+  // two operand buffers (kept out of the VGPRs that the MFMA phase needs)
   float* pro_lds = reinterpret_cast<float*>(smem + 2 * BUF);
   if (PRO) {
-    for (int i = tid; i < 2 * K; i += NT) pro_lds[i] = pro_ss[i];
+    for (int i = tid; i < (PRO == 2 ? 3 : 2) * K; i += NT) pro_lds[i] = pro_ss[i];
     lds_barrier();
   }
   const uint16_t* arow[AR];
+  int64_t aoff2[PRO == 2 ? AR : 1];
   // Rows past M load row M-1 (clamped, branch-free: a per-row "load or zero" select makes hipcc
   // branch around every load); their outputs are neither stored nor counted in the statistics.
   auto set_rows = [&](int mt) {
@@ -114,18 +118,41 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
     for (int i = 0; i < AR; ++i) {
       const int m = (int)min<int64_t>((int64_t)mt * BM + lr + RSTEP * i, M - 1);
       arow[i] = X + rm.in_row<STRIDED>(m) * K + lc * 8;
+      if (PRO == 2) aoff2[i] = arow[i] - X;
     }
   };
   auto load = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < AR; ++i) sa[i] = *reinterpret_cast<const u32x4*>(arow[i] + kt * kBK);
+    if (PRO == 2) {
+#pragma unroll
+      for (int i = 0; i < AR; ++i) sa2[i] = *reinterpret_cast<const u32x4*>(X2 + aoff2[i] + kt * kBK);
+    }
 #pragma unroll
     for (int i = 0; i < BR; ++i) sb[i] = *reinterpret_cast<const u32x4*>(wrow[i] + kt * kBK);
   };
   auto store = [&](int buf, int kt) {
     uint8_t* A = smem + buf * BUF;
     uint8_t* B = A + ABYTES;
-    if (PRO) {  // previous BN's apply + ReLU on this thread's 8 input channels
+    if (PRO == 2) {  // BN backward on this thread's 8 channels: a·g + b·x + c
+      const int k0 = kt * kBK + lc * 8;
+      float ca[8], cb[8], cc[8];
+      dev::Vec8<float>::ld(pro_lds + k0, ca);
+      dev::Vec8<float>::ld(pro_lds + K + k0, cb);
+      dev::Vec8<float>::ld(pro_lds + 2 * K + k0, cc);
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float lo = fmaf(ca[2 * q], __uint_as_float(sa[i][q] << 16),
+                                fmaf(cb[2 * q], __uint_as_float(sa2[i][q] << 16), cc[2 * q]));
+          const float hi = fmaf(ca[2 * q + 1], __uint_as_float(sa[i][q] & 0xffff0000u),
+                                fmaf(cb[2 * q + 1], __uint_as_float(sa2[i][q] & 0xffff0000u), cc[2 * q + 1]));
+          sa[i][q] = dev::pack_bf16x2(lo, hi);
+        }
+      }
+    }
+    if (PRO == 1) {  // previous BN's apply + ReLU on this thread's 8 input channels
       const int k0 = kt * kBK + lc * 8;
       float sc[8], sh[8];
       dev::Vec8<float>::ld(pro_lds + k0, sc);
@@ -379,11 +406,15 @@ __device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
 }
 
-template <int TN, int TK, bool STRIDED>
+// PRO: dY = a_n·G + b_n·Y2 + c_n is formed while staging (the BatchNorm-backward elementwise
+// pass folded in; G is the masked upstream gradient, Y2 the BN input).
+template <int TN, int TK, bool STRIDED, bool PRO>
 __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* __restrict__ dY,
                                                                 const uint16_t* __restrict__ X,
                                                                 float* __restrict__ ws, int M, int N, int K,
-                                                                RowMap rm, int ntiles, int ktiles, int mchunk) {
+                                                                RowMap rm, int ntiles, int ktiles, int mchunk,
+                                                                const uint16_t* __restrict__ Y2,
+                                                                const float* __restrict__ coef) {
   constexpr int BM = 64;                       // pixel rows per step (two 32-deep MFMA k-steps)
   constexpr int SA = TN * 2 + 32, SB = TK * 2 + 32;
   constexpr int ABYTES = BM * SA, BUF = ABYTES + BM * SB;
@@ -399,14 +430,27 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
   const int n0 = (tile % ntiles) * TN, k0 = (tile / ntiles) * TK;
   const int m_begin = sidx * mchunk, m_end = min(M, m_begin + mchunk);
 
-  u32x4 sa[LA], sb[LB];
+  u32x4 sa[LA], sb[LB], sa2[PRO ? LA : 1];
+  float pa[8], pb[8], pc[8];  // this thread's 8 dY channels (fixed: 256 % CA == 0)
+  if (PRO) {
+    const int c = tid % CA;
+    dev::Vec8<float>::ld(coef + n0 + c * 8, pa);
+    dev::Vec8<float>::ld(coef + N + n0 + c * 8, pb);
+    dev::Vec8<float>::ld(coef + 2 * N + n0 + c * 8, pc);
+  }
   auto load = [&](int m) {
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int q = tid + 256 * i, row = q / CA, c = q - (q / CA) * CA;
       const int mm = m + row;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(dY + (int64_t)min(mm, M - 1) * N + n0 + c * 8);
-      sa[i] = mm < m_end ? v : u32x4{0, 0, 0, 0};  // rows past the range contribute zero
+      const int64_t off = (int64_t)min(mm, M - 1) * N + n0 + c * 8;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(dY + off);
+      if (PRO) {
+        sa[i] = v;  // the row-range select happens after the transform (store)
+        sa2[i] = *reinterpret_cast<const u32x4*>(Y2 + off);
+      } else {
+        sa[i] = mm < m_end ? v : u32x4{0, 0, 0, 0};  // rows past the range contribute zero
+      }
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
@@ -416,12 +460,24 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
       sb[i] = mm < m_end ? v : u32x4{0, 0, 0, 0};
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, int m) {
     uint8_t* A = smem + buf * BUF;
     uint8_t* B = A + ABYTES;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int q = tid + 256 * i, row = q / CA, c = q - (q / CA) * CA;
+      if (PRO) {
+        u32x4 t;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const float lo = fmaf(pa[2 * h], __uint_as_float(sa[i][h] << 16),
+                                fmaf(pb[2 * h], __uint_as_float(sa2[i][h] << 16), pc[2 * h]));
+          const float hi = fmaf(pa[2 * h + 1], __uint_as_float(sa[i][h] & 0xffff0000u),
+                                fmaf(pb[2 * h + 1], __uint_as_float(sa2[i][h] & 0xffff0000u), pc[2 * h + 1]));
+          t[h] = dev::pack_bf16x2(lo, hi);
+        }
+        sa[i] = m + row < m_end ? t : u32x4{0, 0, 0, 0};
+      }
       *reinterpret_cast<u32x4*>(A + row * SA + c * 16) = sa[i];
     }
 #pragma unroll
@@ -441,7 +497,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
   const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
   if (m_begin < m_end) {
     load(m_begin);
-    store(0);
+    store(0, m_begin);
     lds_barrier();
     int cur = 0;
     for (int m = m_begin; m < m_end; m += BM) {
@@ -472,7 +528,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
 #pragma unroll
           for (int j = 0; j < FK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
       }
-      if (more) store(cur ^ 1);
+      if (more) store(cur ^ 1, m + BM);
       lds_barrier();
       cur ^= 1;
     }
@@ -536,22 +592,23 @@ int num_cus() {
 }
 
 template <int BM, int BN, int WM, int WN>
-void launch_gemm(bool pro, bool stats, dim3 grid, size_t lds, hipStream_t s, const uint16_t* x, const uint16_t* w,
+void launch_gemm(int pro, bool stats, dim3 grid, size_t lds, hipStream_t s, const uint16_t* x, const uint16_t* w,
                  uint16_t* y, int64_t M, int N, int K, RowMap rm, const float* pss, float* part, int mt, int nt,
-                 int groups) {
+                 int groups, const uint16_t* x2) {
   auto go = [&](auto kern) {
     static size_t lds_set = 0;  // per kernel instantiation: opt in to > 64 KB of dynamic LDS once
     if (lds > 65536 && lds > lds_set) {
       XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       lds_set = lds;
     }
-    hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, s, x, w, y, M, N, K, rm, pss, part, mt, nt, groups);
+    hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, s, x, w, y, M, N, K, rm, pss, part, mt, nt, groups, x2);
   };
 #define XDDP_G(P, S)                                                                                       \
   if (rm.stride > 1) go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, true>);                                   \
   else go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, false>)
-  if (pro) { if (stats) XDDP_G(true, true); else XDDP_G(true, false); }
-  else { if (stats) XDDP_G(false, true); else XDDP_G(false, false); }
+  if (pro == 2) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 2, false, false>);  // stride-1 input gradient only
+  else if (pro == 1) { if (stats) XDDP_G(1, true); else XDDP_G(1, false); }
+  else { if (stats) XDDP_G(0, true); else XDDP_G(0, false); }
 #undef XDDP_G
   XDDP_HIP_CHECK(hipGetLastError());
 }
@@ -562,7 +619,8 @@ void launch_gemm(bool pro, bool stats, dim3 grid, size_t lds, hipStream_t s, con
 // prologue_ss: optional float [2, K] (scale, shift) -> op(x) = relu(x*scale + shift).
 // Returns (y [B, N, OH, OW] channels_last, partials [groups, 3, N] or undefined).
 std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride,
-                                     const c10::optional<at::Tensor>& prologue_ss, bool stats) {
+                                     const c10::optional<at::Tensor>& prologue_ss, bool stats,
+                                     const c10::optional<at::Tensor>& prologue_y) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16, "conv1x1_gemm: x must be 4-D bf16 on GPU");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv1x1_gemm: x must be channels_last");
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 1 && w.size(3) == 1 && w.scalar_type() == at::kBFloat16,
@@ -575,9 +633,15 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   const int64_t OH = (IH - 1) / stride + 1, OW = (IW - 1) / stride + 1;
   const int64_t M = B * OH * OW;
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 31), "conv1x1_gemm: bad M");
-  const bool pro = prologue_ss.has_value() && prologue_ss->defined();
-  if (pro) TORCH_CHECK(prologue_ss->scalar_type() == at::kFloat && prologue_ss->numel() == 2 * K &&
-                           prologue_ss->is_contiguous(), "conv1x1_gemm: prologue scale/shift must be float [2, K]");
+  const bool has_y2 = prologue_y.has_value() && prologue_y->defined();
+  const int pro = has_y2 ? 2 : ((prologue_ss.has_value() && prologue_ss->defined()) ? 1 : 0);
+  if (pro) TORCH_CHECK(prologue_ss.has_value() && prologue_ss->defined() && prologue_ss->scalar_type() == at::kFloat &&
+                           prologue_ss->numel() == (pro == 2 ? 3 : 2) * K && prologue_ss->is_contiguous(),
+                       "conv1x1_gemm: prologue coefficients must be float [2, K] (or [3, K] with prologue_y)");
+  if (pro == 2)
+    TORCH_CHECK(prologue_y->sizes() == x.sizes() && prologue_y->scalar_type() == at::kBFloat16 &&
+                    prologue_y->is_contiguous(at::MemoryFormat::ChannelsLast) && stride == 1 && !stats,
+                "conv1x1_gemm: prologue_y must match x (bf16 channels_last), stride 1, no stats");
   auto y = at::empty({B, N, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
   const int BM = 128, BN = (N % 128 == 0) ? 128 : 64;
@@ -592,7 +656,8 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   at::Tensor part = stats ? at::empty({groups, 3, N}, x.options().dtype(at::kFloat)) : at::Tensor();
   RowMap rm{(int)OH, (int)OW, (int)IH, (int)IW, (int)stride};
   const dim3 grid(groups * ntiles);
-  const size_t lds = 2 * (size_t)(BM + BN) * 128 + (pro ? 2 * K * sizeof(float) : 0);
+  const size_t lds = 2 * (size_t)(BM + BN) * 128 + (pro ? (pro == 2 ? 3 : 2) * K * sizeof(float) : 0);
+  const auto* x2p = pro == 2 ? reinterpret_cast<const uint16_t*>(prologue_y->data_ptr()) : nullptr;
   const auto* xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
   const auto* wp = reinterpret_cast<const uint16_t*>(wc.data_ptr());
   auto* yp = reinterpret_cast<uint16_t*>(y.data_ptr());
@@ -600,18 +665,21 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   float* pp = stats ? part.data_ptr<float>() : nullptr;
   if (BN == 128)
     launch_gemm<128, 128, 4, 2>(pro, stats, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,
-                          groups);
+                          groups, x2p);
   else
     launch_gemm<128, 64, 8, 1>(pro, stats, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,
-                         groups);
+                         groups, x2p);
   return {y, part};
 }
 
 
 // dY: [B, N, OH, OW] channels_last bf16; x: [B, K, IH, IW] channels_last bf16 (the conv input);
 // returns dW [N, K, 1, 1] in w_like's dtype (fp32 accumulation, split over pixel rows).
-at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like) {
+// With prologue_y/coef: dY = coef[0]·dy + coef[1]·prologue_y + coef[2] per dY channel (stride 1).
+at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,
+                         const c10::optional<at::Tensor>& prologue_y, const c10::optional<at::Tensor>& coef) {
   const auto wdtype = w_like.scalar_type();
+  const bool pro = prologue_y.has_value() && prologue_y->defined();
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16,
               "conv1x1_wgrad: bf16 GPU tensors expected");
   TORCH_CHECK(dy.dim() == 4 && x.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
@@ -622,6 +690,14 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stri
   TORCH_CHECK(N % 64 == 0 && K % 64 == 0, "conv1x1_wgrad: channel counts must be multiples of 64");
   const int64_t M = B * OH * OW;
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 31), "conv1x1_wgrad: bad M");
+  if (pro)
+    TORCH_CHECK(prologue_y->sizes() == dy.sizes() && prologue_y->scalar_type() == at::kBFloat16 &&
+                    prologue_y->is_contiguous(at::MemoryFormat::ChannelsLast) && stride == 1 && coef.has_value() &&
+                    coef->defined() && coef->scalar_type() == at::kFloat && coef->numel() == 3 * N &&
+                    coef->is_contiguous(),
+                "conv1x1_wgrad: prologue_y must match dy (bf16 channels_last, stride 1) with float coef [3, N]");
+  const auto* y2p = pro ? reinterpret_cast<const uint16_t*>(prologue_y->data_ptr()) : nullptr;
+  const float* cfp = pro ? coef->data_ptr<float>() : nullptr;
   const int TN = N % 128 == 0 ? 128 : 64, TK = K % 128 == 0 ? 128 : 64;
   const int ntiles = (int)(N / TN), ktiles = (int)(K / TK), tiles = ntiles * ktiles;
   const int64_t steps = (M + 63) / 64;
@@ -641,12 +717,13 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stri
     }
     hipLaunchKernelGGL(kern, dim3(S * tiles), dim3(256), lds, stream,
                        reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                       ws.data_ptr<float>(), (int)M, (int)N, (int)K, rm, ntiles, ktiles, (int)mchunk);
+                       ws.data_ptr<float>(), (int)M, (int)N, (int)K, rm, ntiles, ktiles, (int)mchunk, y2p, cfp);
     XDDP_HIP_CHECK(hipGetLastError());
   };
   const bool strided = stride > 1;
 #define XDDP_W(A, Bk) \
-  if (strided) go(conv1x1_wgrad_kernel<A, Bk, true>); else go(conv1x1_wgrad_kernel<A, Bk, false>)
+  if (pro) go(conv1x1_wgrad_kernel<A, Bk, false, true>);                                           \
+  else if (strided) go(conv1x1_wgrad_kernel<A, Bk, true, false>); else go(conv1x1_wgrad_kernel<A, Bk, false, false>)
   if (TN == 128 && TK == 128) { XDDP_W(128, 128); }
   else if (TN == 128) { XDDP_W(128, 64); }
   else if (TK == 128) { XDDP_W(64, 128); }

@@ -19,16 +19,18 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy, const at::Tensor& x, c
                                     const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
                                     const at::Tensor& invstd, const c10::optional<at::Tensor>& ss, bool relu,
                                     bool need_dres, bool need_dweight, const c10::optional<at::Tensor>& dy2,
-                                    const c10::optional<at::Tensor>& mask_bits);
+                                    const c10::optional<at::Tensor>& mask_bits, bool coef_only);
 std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, const c10::optional<at::Tensor>& residual,
                                  bool relu, bool save_mask, const c10::optional<at::Tensor>& num_batches_tracked);
 // 1x1 conv as an MFMA GEMM with BN prologue (previous BN's apply+ReLU) / epilogue (stats partials)
 std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride,
-                                     const c10::optional<at::Tensor>& prologue_ss, bool stats);
+                                     const c10::optional<at::Tensor>& prologue_ss, bool stats,
+                                     const c10::optional<at::Tensor>& prologue_y);
 // 3x3 pad-1 conv (stride 1/2) as an implicit MFMA GEMM (csrc/kernels/conv3x3.hip)
 std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats);
 at::Tensor conv3x3_rot_weight(const at::Tensor& w);
-at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like);
+at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,
+                         const c10::optional<at::Tensor>& prologue_y, const c10::optional<at::Tensor>& coef);
 std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M,
                                                const c10::optional<at::Tensor>& weight,
                                                const c10::optional<at::Tensor>& bias,

@@ -13,14 +13,15 @@ void bind_norm_kernels(py::module_& m) {
         py::arg("cumulative"), py::arg("eps"), py::arg("residual"), py::arg("relu"), py::arg("save_mask") = false);
   m.def("bn_backward", &bn_backward, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("weight"), py::arg("mean"),
         py::arg("invstd"), py::arg("scale_shift"), py::arg("relu"), py::arg("need_dres"), py::arg("need_dweight"),
-        py::arg("dy2") = py::none(), py::arg("mask_bits") = py::none());
+        py::arg("dy2") = py::none(), py::arg("mask_bits") = py::none(), py::arg("coef_only") = false);
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("scale_shift"), py::arg("residual"), py::arg("relu"),
         py::arg("save_mask"), py::arg("num_batches_tracked"));
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("prologue_ss"),
-        py::arg("stats"));
+        py::arg("stats"), py::arg("prologue_y") = py::none());
   m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"));
   m.def("conv3x3_rot_weight", &conv3x3_rot_weight, py::arg("w"));
-  m.def("conv1x1_wgrad", &conv1x1_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"));
+  m.def("conv1x1_wgrad", &conv1x1_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"),
+        py::arg("prologue_y") = py::none(), py::arg("coef") = py::none());
   m.def("bn_stats_from_partials", &bn_stats_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"),
         py::arg("momentum"), py::arg("cumulative"), py::arg("eps"), py::arg("group_minor") = false);

@@ -58,10 +58,25 @@ class _Conv1x1BN(torch.autograd.Function):
         if dout is None:
             return (None,) * 14
         need_bn_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
-        dy, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu,
-                                               ctx.has_res and ctx.needs_input_grad[10], need_bn_w, dout2, bits)
         s = ctx.stride
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        need_dres = ctx.has_res and ctx.needs_input_grad[10]
+        if (s == 1 and need_x and need_w and _bwd_prologue() and _dgrad_gemm() and _wgrad_gemm()
+                and (need_dres or (not ctx.relu and dout2 is None))):
+            # BN-backward elementwise pass folded into both GEMMs: dY = k1·g + k2·y + k3' is formed
+            # while staging (g = the masked gradient the reduce pass writes as d(residual), or the
+            # incoming gradient itself), so dY is never written to and re-read from HBM
+            coef, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu, need_dres,
+                                                     need_bn_w, dout2, bits, True)
+            g = dres if need_dres else dout.contiguous(memory_format=torch.channels_last)
+            n_out, k_in = w.shape[0], w.shape[1]
+            wt = w.reshape(n_out, k_in).t().contiguous().view(k_in, n_out, 1, 1)
+            dx = C.conv1x1_gemm(g, wt, 1, coef, False, y)[0]
+            dw = C.conv1x1_wgrad(g, x, 1, w, y, coef)
+            return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
+                    None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None)
+        dy, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu, need_dres,
+                                               need_bn_w, dout2, bits)
         dx = dw = None
         if need_x and s == 1 and _dgrad_gemm():
             # dX[M, K] = dY[M, N] · W[N, K] is the same NT GEMM on (dY, Wᵀ): 35 % less time than
@@ -131,6 +146,12 @@ def _conv3x3() -> bool:
 def _dgrad_gemm() -> bool:
     """XDDP_CONV_DGRAD_GEMM=0 sends the stride-1 input gradient back to MIOpen (A/B switch)."""
     return os.environ.get("XDDP_CONV_DGRAD_GEMM", "1") != "0"
+
+
+def _bwd_prologue() -> bool:
+    """XDDP_CONV_BWD_PROLOGUE=0 materializes the BN-backward gradient instead of folding it into
+    the stride-1 input/weight-gradient GEMMs (A/B switch)."""
+    return os.environ.get("XDDP_CONV_BWD_PROLOGUE", "1") != "0"
 
 
 def _wgrad_gemm() -> bool:

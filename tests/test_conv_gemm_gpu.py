@@ -78,7 +78,27 @@ def test_epilogue_stats_match_torch(offset):
     torch.testing.assert_close(rv, 0.9 + 0.1 * yf.var(0, unbiased=True), rtol=1e-3, atol=1e-4)
 
 
-@pytest.mark.parametrize("residual,relu,stride", [(False, True, 1), (True, True, 1), (False, False, 2)])
+@pytest.mark.parametrize("b,cin,h,w,cout", [(2, 64, 14, 14, 256), (3, 128, 9, 7, 64)])
+def test_bn_backward_prologue_in_gemms(b, cin, h, w, cout):
+    """Input- and weight-gradient GEMMs forming dY = a·G + b·Y + c while staging equal the plain
+    GEMMs on the materialized dY."""
+    torch.manual_seed(4)
+    g, yb, x = _x(b, cout, h, w), _x(b, cout, h, w), _x(b, cin, h, w)
+    coef = torch.randn(3, cout, device="cuda")
+    dy = (coef[0].view(1, -1, 1, 1) * g.float() + coef[1].view(1, -1, 1, 1) * yb.float()
+          + coef[2].view(1, -1, 1, 1)).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(cin, cout, 1, 1, device="cuda") / cout ** 0.5).to(torch.bfloat16)  # [K_in, N_out] = W^T
+    dx = C.conv1x1_gemm(g, wt, 1, coef, False, yb)[0]
+    ref = C.conv1x1_gemm(dy, wt, 1, None, False)[0]
+    torch.testing.assert_close(dx.float(), ref.float(), rtol=2e-2, atol=2e-2 * ref.float().abs().max().item())
+    like = torch.empty(cout, cin, 1, 1, device="cuda", dtype=torch.float32)
+    dw = C.conv1x1_wgrad(g, x, 1, like, yb, coef)
+    refw = C.conv1x1_wgrad(dy, x, 1, like)
+    torch.testing.assert_close(dw, refw, rtol=2e-2, atol=2e-2 * refw.abs().max().item())
+
+
+@pytest.mark.parametrize("residual,relu,stride", [(False, True, 1), (True, True, 1), (False, False, 2),
+                                                  (False, False, 1)])
 def test_conv1x1_bn_act_forward_backward(residual, relu, stride):
     from distributeddataparallel_amd.ops import FusedBatchNorm2d, conv1x1_bn_act
 
