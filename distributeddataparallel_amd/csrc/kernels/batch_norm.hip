@@ -594,14 +594,17 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
   // coef_only: skip the elementwise pass and return the per-channel (k1, k2, k3 - k2·mean) [3, C]
   // in dx's slot; the gradient k1·g + k2·x + k3' is formed by the consumer (conv GEMM prologue),
   // with g = dres (written here) or, without ReLU/second gradient, dy itself
-  if (coef_only) TORCH_CHECK(need_dres || (!relu && !dual), "bn_backward: coef_only needs g materialized");
+  // with a ReLU whose mask is recomputed (scale/shift given, no residual gradient) the consumer
+  // also needs (scale, shift): coef is then [5, C] = (k1, k2, k3', scale, shift)
+  const bool coef_mask = coef_only && !need_dres && relu && !dual && !have_bits && !have_y && have_ss;
+  if (coef_only) TORCH_CHECK(need_dres || (!relu && !dual) || coef_mask, "bn_backward: coef_only needs g materialized");
   auto dx = coef_only ? at::Tensor() : at::empty_like(x, at::MemoryFormat::ChannelsLast);
   at::Tensor dres = need_dres ? at::empty_like(x, at::MemoryFormat::ChannelsLast) : at::Tensor();
   const bool has_w = weight.has_value() && weight->defined();
   const auto wdt = has_w ? weight->scalar_type() : at::kFloat;
   at::Tensor dw = (has_w && need_dweight) ? at::empty({C}, weight->options()) : at::Tensor();
   at::Tensor db = (has_w && need_dweight) ? at::empty({C}, weight->options()) : at::Tensor();
-  auto coef = at::empty({3, C}, fopt);
+  auto coef = at::empty({coef_mask ? 5 : 3, C}, fopt);
   Geo g = make_geo(M, (int)C);
   auto part = at::empty({(int64_t)g.rblocks, C, 2}, fopt);
   // need_dres: the reduce pass writes g = mask*(dy+dy2) into dres; the elementwise pass then
@@ -641,8 +644,10 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
                          coef_only ? mean.data_ptr<float>() : nullptr);
       XDDP_HIP_CHECK(hipGetLastError());
       const int64_t nvec = M * C / 8;
-      if (coef_only) {
-        // nothing more: the consumer applies the coefficients
+      if (coef_only) {  // nothing more: the consumer applies the coefficients
+        if (coef_mask)
+          XDDP_HIP_CHECK(hipMemcpyAsync(coef.data_ptr<float>() + 3 * C, ss->data_ptr<float>(), 2 * C * sizeof(float),
+                                        hipMemcpyDeviceToDevice, stream));
       } else if (wg) {
         hipLaunchKernelGGL((bn_bwd_elem_kernel<T, 0, false, false>), dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
                            reinterpret_cast<const T*>(dres.data_ptr()), nullptr,

@@ -64,7 +64,8 @@ struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every st
 
 // PRO: 0 = plain A; 1 = relu(A·s_k + b_k) (the previous BN's apply); 2 = a_k·A + b_k·X2 + c_k, the
 // BatchNorm-backward elementwise pass (A = masked upstream gradient, X2 = the BN input) folded
-// into the input-gradient GEMM so that gradient is never written to HBM.
+// into the input-gradient GEMM so that gradient is never written to HBM; 3 = as 2 with the BN's
+// ReLU mask recomputed in registers: A -> (X2·s_k + t_k > 0) ? A : 0.
 template <int BM, int BN, int WM, int WN, int PRO, bool STATS, bool STRIDED>
 __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, int64_t M, int N,
@@ -101,16 +102,16 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
 #pragma unroll
   for (int i = 0; i < BR; ++i) wrow[i] = Wt + (int64_t)(n0 + lr + RSTEP * i) * K + lc * 8;
 
-  u32x4 sa[AR], sb[BR], sa2[PRO == 2 ? AR : 1];
+  u32x4 sa[AR], sb[BR], sa2[PRO >= 2 ? AR : 1];
   // PRO: the per-input-channel coefficients for all K channels, staged once into LDS after the
   // two operand buffers (kept out of the VGPRs that the MFMA phase needs)
   float* pro_lds = reinterpret_cast<float*>(smem + 2 * BUF);
   if (PRO) {
-    for (int i = tid; i < (PRO == 2 ? 3 : 2) * K; i += NT) pro_lds[i] = pro_ss[i];
+    for (int i = tid; i < (PRO == 3 ? 5 : PRO == 2 ? 3 : 2) * K; i += NT) pro_lds[i] = pro_ss[i];
     lds_barrier();
   }
   const uint16_t* arow[AR];
-  int64_t aoff2[PRO == 2 ? AR : 1];
+  const int64_t dx2 = PRO >= 2 ? X2 - X : 0;  // the second A source at the same element offsets
   // Rows past M load row M-1 (clamped, branch-free: a per-row "load or zero" select makes hipcc
   // branch around every load); their outputs are neither stored nor counted in the statistics.
   auto set_rows = [&](int mt) {
@@ -118,15 +119,14 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
     for (int i = 0; i < AR; ++i) {
       const int m = (int)min<int64_t>((int64_t)mt * BM + lr + RSTEP * i, M - 1);
       arow[i] = X + rm.in_row<STRIDED>(m) * K + lc * 8;
-      if (PRO == 2) aoff2[i] = arow[i] - X;
     }
   };
   auto load = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < AR; ++i) sa[i] = *reinterpret_cast<const u32x4*>(arow[i] + kt * kBK);
-    if (PRO == 2) {
+    if (PRO >= 2) {
 #pragma unroll
-      for (int i = 0; i < AR; ++i) sa2[i] = *reinterpret_cast<const u32x4*>(X2 + aoff2[i] + kt * kBK);
+      for (int i = 0; i < AR; ++i) sa2[i] = *reinterpret_cast<const u32x4*>(arow[i] + dx2 + kt * kBK);
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) sb[i] = *reinterpret_cast<const u32x4*>(wrow[i] + kt * kBK);
@@ -134,21 +134,28 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
   auto store = [&](int buf, int kt) {
     uint8_t* A = smem + buf * BUF;
     uint8_t* B = A + ABYTES;
-    if (PRO == 2) {  // BN backward on this thread's 8 channels: a·g + b·x + c
+    if (PRO >= 2) {  // BN backward on this thread's 8 channels: a·g + b·x + c (g masked by ReLU for 3)
+      // coefficients two channels at a time (float2 LDS reads): few live VGPRs in this phase
       const int k0 = kt * kBK + lc * 8;
-      float ca[8], cb[8], cc[8];
-      dev::Vec8<float>::ld(pro_lds + k0, ca);
-      dev::Vec8<float>::ld(pro_lds + K + k0, cb);
-      dev::Vec8<float>::ld(pro_lds + 2 * K + k0, cc);
 #pragma unroll
-      for (int i = 0; i < AR; ++i) {
+      for (int q = 0; q < 4; ++q) {
+        const float2 ca = *reinterpret_cast<const float2*>(pro_lds + k0 + 2 * q);
+        const float2 cb = *reinterpret_cast<const float2*>(pro_lds + K + k0 + 2 * q);
+        const float2 cc = *reinterpret_cast<const float2*>(pro_lds + 2 * K + k0 + 2 * q);
+        float2 ms = {0.f, 0.f}, mt = {0.f, 0.f};
+        if (PRO == 3) {
+          ms = *reinterpret_cast<const float2*>(pro_lds + 3 * K + k0 + 2 * q);
+          mt = *reinterpret_cast<const float2*>(pro_lds + 4 * K + k0 + 2 * q);
+        }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float lo = fmaf(ca[2 * q], __uint_as_float(sa[i][q] << 16),
-                                fmaf(cb[2 * q], __uint_as_float(sa2[i][q] << 16), cc[2 * q]));
-          const float hi = fmaf(ca[2 * q + 1], __uint_as_float(sa[i][q] & 0xffff0000u),
-                                fmaf(cb[2 * q + 1], __uint_as_float(sa2[i][q] & 0xffff0000u), cc[2 * q + 1]));
-          sa[i][q] = dev::pack_bf16x2(lo, hi);
+        for (int i = 0; i < AR; ++i) {
+          float g0 = __uint_as_float(sa[i][q] << 16), g1 = __uint_as_float(sa[i][q] & 0xffff0000u);
+          const float x0 = __uint_as_float(sa2[i][q] << 16), x1 = __uint_as_float(sa2[i][q] & 0xffff0000u);
+          if (PRO == 3) {
+            g0 = fmaf(x0, ms.x, mt.x) > 0.f ? g0 : 0.f;
+            g1 = fmaf(x1, ms.y, mt.y) > 0.f ? g1 : 0.f;
+          }
+          sa[i][q] = dev::pack_bf16x2(fmaf(ca.x, g0, fmaf(cb.x, x0, cc.x)), fmaf(ca.y, g1, fmaf(cb.y, x1, cc.y)));
         }
       }
     }
@@ -406,9 +413,10 @@ __device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
 }
 
-// PRO: dY = a_n·G + b_n·Y2 + c_n is formed while staging (the BatchNorm-backward elementwise
-// pass folded in; G is the masked upstream gradient, Y2 the BN input).
-template <int TN, int TK, bool STRIDED, bool PRO>
+// PRO (2, 3): dY = a_n·G + b_n·Y2 + c_n is formed while staging (the BatchNorm-backward
+// elementwise pass folded in; G is the masked upstream gradient, Y2 the BN input; with 3 the ReLU
+// mask (Y2·s_n + t_n > 0) is applied to G here).
+template <int TN, int TK, bool STRIDED, int PRO>
 __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* __restrict__ dY,
                                                                 const uint16_t* __restrict__ X,
                                                                 float* __restrict__ ws, int M, int N, int K,
@@ -431,12 +439,16 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
   const int m_begin = sidx * mchunk, m_end = min(M, m_begin + mchunk);
 
   u32x4 sa[LA], sb[LB], sa2[PRO ? LA : 1];
-  float pa[8], pb[8], pc[8];  // this thread's 8 dY channels (fixed: 256 % CA == 0)
+  float pa[8], pb[8], pc[8], pms[8], pmt[8];  // this thread's 8 dY channels (fixed: 256 % CA == 0)
   if (PRO) {
     const int c = tid % CA;
     dev::Vec8<float>::ld(coef + n0 + c * 8, pa);
     dev::Vec8<float>::ld(coef + N + n0 + c * 8, pb);
     dev::Vec8<float>::ld(coef + 2 * N + n0 + c * 8, pc);
+    if (PRO == 3) {
+      dev::Vec8<float>::ld(coef + 3 * N + n0 + c * 8, pms);
+      dev::Vec8<float>::ld(coef + 4 * N + n0 + c * 8, pmt);
+    }
   }
   auto load = [&](int m) {
 #pragma unroll
@@ -470,11 +482,14 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
         u32x4 t;
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
-          const float lo = fmaf(pa[2 * h], __uint_as_float(sa[i][h] << 16),
-                                fmaf(pb[2 * h], __uint_as_float(sa2[i][h] << 16), pc[2 * h]));
-          const float hi = fmaf(pa[2 * h + 1], __uint_as_float(sa[i][h] & 0xffff0000u),
-                                fmaf(pb[2 * h + 1], __uint_as_float(sa2[i][h] & 0xffff0000u), pc[2 * h + 1]));
-          t[h] = dev::pack_bf16x2(lo, hi);
+          float g0 = __uint_as_float(sa[i][h] << 16), g1 = __uint_as_float(sa[i][h] & 0xffff0000u);
+          const float x0 = __uint_as_float(sa2[i][h] << 16), x1 = __uint_as_float(sa2[i][h] & 0xffff0000u);
+          if (PRO == 3) {
+            g0 = fmaf(x0, pms[2 * h], pmt[2 * h]) > 0.f ? g0 : 0.f;
+            g1 = fmaf(x1, pms[2 * h + 1], pmt[2 * h + 1]) > 0.f ? g1 : 0.f;
+          }
+          t[h] = dev::pack_bf16x2(fmaf(pa[2 * h], g0, fmaf(pb[2 * h], x0, pc[2 * h])),
+                                  fmaf(pa[2 * h + 1], g1, fmaf(pb[2 * h + 1], x1, pc[2 * h + 1])));
         }
         sa[i] = m + row < m_end ? t : u32x4{0, 0, 0, 0};
       }
@@ -606,7 +621,8 @@ void launch_gemm(int pro, bool stats, dim3 grid, size_t lds, hipStream_t s, cons
 #define XDDP_G(P, S)                                                                                       \
   if (rm.stride > 1) go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, true>);                                   \
   else go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, false>)
-  if (pro == 2) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 2, false, false>);  // stride-1 input gradient only
+  if (pro == 3) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 3, false, false>);  // stride-1 input gradient only
+  else if (pro == 2) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 2, false, false>);
   else if (pro == 1) { if (stats) XDDP_G(1, true); else XDDP_G(1, false); }
   else { if (stats) XDDP_G(0, true); else XDDP_G(0, false); }
 #undef XDDP_G
@@ -634,11 +650,13 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   const int64_t M = B * OH * OW;
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 31), "conv1x1_gemm: bad M");
   const bool has_y2 = prologue_y.has_value() && prologue_y->defined();
-  const int pro = has_y2 ? 2 : ((prologue_ss.has_value() && prologue_ss->defined()) ? 1 : 0);
-  if (pro) TORCH_CHECK(prologue_ss.has_value() && prologue_ss->defined() && prologue_ss->scalar_type() == at::kFloat &&
-                           prologue_ss->numel() == (pro == 2 ? 3 : 2) * K && prologue_ss->is_contiguous(),
-                       "conv1x1_gemm: prologue coefficients must be float [2, K] (or [3, K] with prologue_y)");
-  if (pro == 2)
+  const bool has_ss = prologue_ss.has_value() && prologue_ss->defined();
+  const int pro = has_y2 ? (has_ss && prologue_ss->numel() == 5 * K ? 3 : 2) : (has_ss ? 1 : 0);
+  const int ncoef = pro == 3 ? 5 : pro == 2 ? 3 : 2;
+  if (pro) TORCH_CHECK(has_ss && prologue_ss->scalar_type() == at::kFloat && prologue_ss->numel() == ncoef * K &&
+                           prologue_ss->is_contiguous(),
+                       "conv1x1_gemm: prologue coefficients must be float [2, K] (or [3|5, K] with prologue_y)");
+  if (pro >= 2)
     TORCH_CHECK(prologue_y->sizes() == x.sizes() && prologue_y->scalar_type() == at::kBFloat16 &&
                     prologue_y->is_contiguous(at::MemoryFormat::ChannelsLast) && stride == 1 && !stats,
                 "conv1x1_gemm: prologue_y must match x (bf16 channels_last), stride 1, no stats");
@@ -656,8 +674,8 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   at::Tensor part = stats ? at::empty({groups, 3, N}, x.options().dtype(at::kFloat)) : at::Tensor();
   RowMap rm{(int)OH, (int)OW, (int)IH, (int)IW, (int)stride};
   const dim3 grid(groups * ntiles);
-  const size_t lds = 2 * (size_t)(BM + BN) * 128 + (pro ? (pro == 2 ? 3 : 2) * K * sizeof(float) : 0);
-  const auto* x2p = pro == 2 ? reinterpret_cast<const uint16_t*>(prologue_y->data_ptr()) : nullptr;
+  const size_t lds = 2 * (size_t)(BM + BN) * 128 + (pro ? ncoef * K * sizeof(float) : 0);
+  const auto* x2p = pro >= 2 ? reinterpret_cast<const uint16_t*>(prologue_y->data_ptr()) : nullptr;
   const auto* xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
   const auto* wp = reinterpret_cast<const uint16_t*>(wc.data_ptr());
   auto* yp = reinterpret_cast<uint16_t*>(y.data_ptr());
@@ -679,7 +697,8 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
 at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,
                          const c10::optional<at::Tensor>& prologue_y, const c10::optional<at::Tensor>& coef) {
   const auto wdtype = w_like.scalar_type();
-  const bool pro = prologue_y.has_value() && prologue_y->defined();
+  const bool has_y2 = prologue_y.has_value() && prologue_y->defined();
+  const int pro = has_y2 ? (coef.has_value() && coef->defined() && coef->numel() == 5 * dy.size(1) ? 3 : 2) : 0;
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16,
               "conv1x1_wgrad: bf16 GPU tensors expected");
   TORCH_CHECK(dy.dim() == 4 && x.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
@@ -693,9 +712,9 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stri
   if (pro)
     TORCH_CHECK(prologue_y->sizes() == dy.sizes() && prologue_y->scalar_type() == at::kBFloat16 &&
                     prologue_y->is_contiguous(at::MemoryFormat::ChannelsLast) && stride == 1 && coef.has_value() &&
-                    coef->defined() && coef->scalar_type() == at::kFloat && coef->numel() == 3 * N &&
+                    coef->defined() && coef->scalar_type() == at::kFloat && coef->numel() == (pro == 3 ? 5 : 3) * N &&
                     coef->is_contiguous(),
-                "conv1x1_wgrad: prologue_y must match dy (bf16 channels_last, stride 1) with float coef [3, N]");
+                "conv1x1_wgrad: prologue_y must match dy (bf16 channels_last, stride 1) with float coef [3|5, N]");
   const auto* y2p = pro ? reinterpret_cast<const uint16_t*>(prologue_y->data_ptr()) : nullptr;
   const float* cfp = pro ? coef->data_ptr<float>() : nullptr;
   const int TN = N % 128 == 0 ? 128 : 64, TK = K % 128 == 0 ? 128 : 64;
@@ -722,8 +741,9 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stri
   };
   const bool strided = stride > 1;
 #define XDDP_W(A, Bk) \
-  if (pro) go(conv1x1_wgrad_kernel<A, Bk, false, true>);                                           \
-  else if (strided) go(conv1x1_wgrad_kernel<A, Bk, true, false>); else go(conv1x1_wgrad_kernel<A, Bk, false, false>)
+  if (pro == 3) go(conv1x1_wgrad_kernel<A, Bk, false, 3>);                                         \
+  else if (pro == 2) go(conv1x1_wgrad_kernel<A, Bk, false, 2>);                                    \
+  else if (strided) go(conv1x1_wgrad_kernel<A, Bk, true, 0>); else go(conv1x1_wgrad_kernel<A, Bk, false, 0>)
   if (TN == 128 && TK == 128) { XDDP_W(128, 128); }
   else if (TN == 128) { XDDP_W(128, 64); }
   else if (TK == 128) { XDDP_W(64, 128); }

@@ -62,10 +62,11 @@ class _Conv1x1BN(torch.autograd.Function):
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         need_dres = ctx.has_res and ctx.needs_input_grad[10]
         if (s == 1 and need_x and need_w and _bwd_prologue() and _dgrad_gemm() and _wgrad_gemm()
-                and (need_dres or (not ctx.relu and dout2 is None))):
+                and (need_dres or (dout2 is None and bits is None and (not ctx.relu or _bwd_prologue_masked())))):
             # BN-backward elementwise pass folded into both GEMMs: dY = k1·g + k2·y + k3' is formed
             # while staging (g = the masked gradient the reduce pass writes as d(residual), or the
-            # incoming gradient itself), so dY is never written to and re-read from HBM
+            # incoming gradient itself, masked in the prologue by relu(y·scale + shift) > 0 when
+            # the BN has a ReLU), so dY is never written to and re-read from HBM
             coef, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu, need_dres,
                                                      need_bn_w, dout2, bits, True)
             g = dres if need_dres else dout.contiguous(memory_format=torch.channels_last)
@@ -152,6 +153,14 @@ def _bwd_prologue() -> bool:
     """XDDP_CONV_BWD_PROLOGUE=0 materializes the BN-backward gradient instead of folding it into
     the stride-1 input/weight-gradient GEMMs (A/B switch)."""
     return os.environ.get("XDDP_CONV_BWD_PROLOGUE", "1") != "0"
+
+
+def _bwd_prologue_masked() -> bool:
+    """XDDP_CONV_BWD_PROLOGUE_MASK=1 also folds the BN+ReLU (recomputed-mask) backward of the
+    bottleneck's conv1 into its gradient GEMMs. Off by default: that input-gradient GEMM re-reads
+    its A operand once per output-channel tile (C_in / 128 of them), so reading two sources there
+    costs more than the skipped pass saves (10,378 vs 10,436 img/s, ResNet-50 bs256)."""
+    return os.environ.get("XDDP_CONV_BWD_PROLOGUE_MASK", "0") == "1"
 
 
 def _wgrad_gemm() -> bool:

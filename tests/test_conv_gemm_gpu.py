@@ -78,15 +78,17 @@ def test_epilogue_stats_match_torch(offset):
     torch.testing.assert_close(rv, 0.9 + 0.1 * yf.var(0, unbiased=True), rtol=1e-3, atol=1e-4)
 
 
-@pytest.mark.parametrize("b,cin,h,w,cout", [(2, 64, 14, 14, 256), (3, 128, 9, 7, 64)])
-def test_bn_backward_prologue_in_gemms(b, cin, h, w, cout):
-    """Input- and weight-gradient GEMMs forming dY = a·G + b·Y + c while staging equal the plain
-    GEMMs on the materialized dY."""
+@pytest.mark.parametrize("b,cin,h,w,cout,masked", [(2, 64, 14, 14, 256, False), (3, 128, 9, 7, 64, False),
+                                                   (2, 128, 10, 10, 128, True)])
+def test_bn_backward_prologue_in_gemms(b, cin, h, w, cout, masked):
+    """Input- and weight-gradient GEMMs forming dY = a·G + b·Y + c (G masked by Y·s + t > 0 when
+    masked) while staging equal the plain GEMMs on the materialized dY."""
     torch.manual_seed(4)
     g, yb, x = _x(b, cout, h, w), _x(b, cout, h, w), _x(b, cin, h, w)
-    coef = torch.randn(3, cout, device="cuda")
-    dy = (coef[0].view(1, -1, 1, 1) * g.float() + coef[1].view(1, -1, 1, 1) * yb.float()
-          + coef[2].view(1, -1, 1, 1)).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    coef = torch.randn(5 if masked else 3, cout, device="cuda")
+    v = lambda i: coef[i].view(1, -1, 1, 1)  # noqa: E731
+    gm = torch.where(yb.float() * v(3) + v(4) > 0, g.float(), 0.0) if masked else g.float()
+    dy = (v(0) * gm + v(1) * yb.float() + v(2)).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     wt = (torch.randn(cin, cout, 1, 1, device="cuda") / cout ** 0.5).to(torch.bfloat16)  # [K_in, N_out] = W^T
     dx = C.conv1x1_gemm(g, wt, 1, coef, False, yb)[0]
     ref = C.conv1x1_gemm(dy, wt, 1, None, False)[0]
