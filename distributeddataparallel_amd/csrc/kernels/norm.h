@@ -29,6 +29,7 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
 // 3x3 pad-1 conv (stride 1/2) as an implicit MFMA GEMM (csrc/kernels/conv3x3.hip)
 std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats);
 at::Tensor conv3x3_rot_weight(const at::Tensor& w);
+at::Tensor conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like);
 at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,
                          const c10::optional<at::Tensor>& prologue_y, const c10::optional<at::Tensor>& coef);
 std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M,

@@ -20,6 +20,7 @@ void bind_norm_kernels(py::module_& m) {
         py::arg("stats"), py::arg("prologue_y") = py::none());
   m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"));
   m.def("conv3x3_rot_weight", &conv3x3_rot_weight, py::arg("w"));
+  m.def("conv3x3_wgrad", &conv3x3_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"));
   m.def("conv1x1_wgrad", &conv1x1_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"),
         py::arg("prologue_y") = py::none(), py::arg("coef") = py::none());
   m.def("bn_stats_from_partials", &bn_stats_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),

@@ -29,7 +29,7 @@ def timeit(fn, iters=20):
     return (time.perf_counter() - t) / iters * 1e6
 
 
-tot = [0.0] * 5
+tot = [0.0] * 6
 for cin, hw, cout, s, cnt in SHAPES:
     B = 256
     x = torch.randn(B, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -54,11 +54,17 @@ for cin, hw, cout, s, cnt in SHAPES:
         derr = (dgot.float() - dref.float()).abs().max().item() / dref.float().abs().max().item()
         td = timeit(lambda: C.conv3x3_forward(dy, wt, 1, False))
     t.append(td)
+    wref = cb(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
+    wgot = C.conv3x3_wgrad(dy, x, s, w)
+    werr = (wgot.float() - wref.float()).norm().item() / wref.float().norm().item()
+    t.append(timeit(lambda: C.conv3x3_wgrad(dy, x, s, w)))
     for i in range(5):
         tot[i] += (t[i] if t[i] == t[i] else t[1]) * cnt
+    tot[5] += t[5] * cnt
     print(f"C{cin}->{cout} {hw}x{hw} s{s} x{cnt}: GFLOP {fl/1e9:6.1f} | fwd {t[0]:6.1f} us {fl/t[0]/1e6:5.0f} TF/s | "
           f"dgrad {t[1]:6.1f} us {fl/t[1]/1e6:5.0f} TF/s | wgrad {t[2]:6.1f} us {fl/t[2]/1e6:5.0f} TF/s || "
-          f"ours fwd {t[3]:6.1f} us {fl/t[3]/1e6:5.0f} TF/s (err {err:.1e}) dgrad {t[4]:6.1f} us (err {derr:.1e})",
+          f"ours fwd {t[3]:6.1f} us {fl/t[3]/1e6:5.0f} TF/s (err {err:.1e}) dgrad {t[4]:6.1f} us (err {derr:.1e}) "
+          f"wgrad {t[5]:6.1f} us {fl/t[5]/1e6:5.0f} TF/s (rel {werr:.1e})",
           flush=True)
 print(f"TOTAL (x count) ms: fwd {tot[0]/1e3:.3f} dgrad {tot[1]/1e3:.3f} wgrad {tot[2]/1e3:.3f} | "
-      f"ours fwd {tot[3]/1e3:.3f} dgrad (s2 on MIOpen) {tot[4]/1e3:.3f}")
+      f"ours fwd {tot[3]/1e3:.3f} dgrad (s2 on MIOpen) {tot[4]/1e3:.3f} wgrad {tot[5]/1e3:.3f}")

@@ -190,12 +190,14 @@ def _graphed_train_step_check():
         loss2 = step(x, y)
         torch.cuda.synchronize()
         torch.testing.assert_close(loss2, loss3, rtol=1e-3, atol=1e-4)
-        # compare the step's updates (MIOpen may pick different conv algorithms for the two
-        # models; fp32 reduction-order noise is a relative error of the update, not of the weight)
+        # compare the step's updates (capture runs MIOpen in immediate mode, the eager model in
+        # find mode, so the two use different conv algorithms; their fp32 reduction-order noise is
+        # a relative error of the update — up to ~1 % on the small layer4 gradients — not of the
+        # weight)
         for (n, a), b, q in zip(m2.named_parameters(), m3.parameters(), p0):
             u2, u3 = (a - q).flatten(), (b - q).flatten()
             err = float((u2 - u3).norm() / (u3.norm() + 1e-12))
-            assert err < 1e-2, (n, err)
+            assert err < 3e-2, (n, err)
         for (n, a), b in zip(m2.named_buffers(), m3.buffers()):
             if a.is_floating_point():
                 torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-5, msg=lambda m, n=n: f"{n}: {m}")
