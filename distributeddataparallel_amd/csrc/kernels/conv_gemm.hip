@@ -50,6 +50,12 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 __device__ __forceinline__ float bf16_round(float v) { return __uint_as_float(dev::pack_bf16x2(v, 0.f) << 16); }
 
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
 struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every stride-th pixel)
   int OH, OW, IH, IW, stride;
   template <bool STRIDED>
@@ -66,7 +72,10 @@ struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every st
 // BatchNorm-backward elementwise pass (A = masked upstream gradient, X2 = the BN input) folded
 // into the input-gradient GEMM so that gradient is never written to HBM; 3 = as 2 with the BN's
 // ReLU mask recomputed in registers: A -> (X2·s_k + t_k > 0) ? A : 0.
-template <int BM, int BN, int WM, int WN, int PRO, bool STATS, bool STRIDED>
+// BT: the B operand is given K-major (Wt[k][n], e.g. the forward weight W[n_out][k_in] used as Wᵀ by
+// the input-gradient GEMM): staged as [64 k][BN n] rows (padded 32 B) and read into fragments with
+// the transposing ds_read_b64_tr_b16, so no transposed weight copy is made.
+template <int BM, int BN, int WM, int WN, int PRO, bool STATS, bool STRIDED, bool BT = false>
 __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, int64_t M, int N,
     int K, RowMap rm, const float* __restrict__ pro_ss, float* __restrict__ part, int mtiles, int ntiles,
@@ -75,7 +84,8 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
   constexpr int AR = BM / RSTEP, BR = BN / RSTEP;    // 16-B loads per thread per operand tile
   constexpr int WTM = BM / WM, WTN = BN / WN;        // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;        // 16x16 MFMA tiles per wave
-  constexpr int ABYTES = BM * 128, BBYTES = BN * 128, BUF = ABYTES + BBYTES;
+  constexpr int SBT = BN * 2 + 32;                   // BT: LDS row stride of the [64 k][BN n] B tile
+  constexpr int ABYTES = BM * 128, BBYTES = BT ? 64 * SBT : BN * 128, BUF = ABYTES + BBYTES;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
@@ -99,8 +109,17 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
   for (int e = 0; e < 8; ++e) st_s[e] = st_ss[e] = 0.f;
 
   const uint16_t* wrow[BR];
+  constexpr int BCH = BN / 8;  // BT: 16-B chunks per staged k row (64 * BCH == NT * BR)
+  static_assert(!BT || 64 * BCH == NT * BR, "BT staging must cover the B tile exactly");
 #pragma unroll
-  for (int i = 0; i < BR; ++i) wrow[i] = Wt + (int64_t)(n0 + lr + RSTEP * i) * K + lc * 8;
+  for (int i = 0; i < BR; ++i) {
+    if (BT) {
+      const int q = tid + NT * i, row = q / BCH, c = q % BCH;
+      wrow[i] = Wt + (int64_t)row * N + n0 + c * 8;  // + kt * 64 * N per K-tile
+    } else {
+      wrow[i] = Wt + (int64_t)(n0 + lr + RSTEP * i) * K + lc * 8;
+    }
+  }
 
   u32x4 sa[AR], sb[BR], sa2[PRO >= 2 ? AR : 1];
   // PRO: the per-input-channel coefficients for all K channels, staged once into LDS after the
@@ -129,7 +148,8 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
       for (int i = 0; i < AR; ++i) sa2[i] = *reinterpret_cast<const u32x4*>(arow[i] + dx2 + kt * kBK);
     }
 #pragma unroll
-    for (int i = 0; i < BR; ++i) sb[i] = *reinterpret_cast<const u32x4*>(wrow[i] + kt * kBK);
+    for (int i = 0; i < BR; ++i)
+      sb[i] = *reinterpret_cast<const u32x4*>(wrow[i] + (BT ? (int64_t)kt * kBK * N : (int64_t)kt * kBK));
   };
   auto store = [&](int buf, int kt) {
     uint8_t* A = smem + buf * BUF;
@@ -177,7 +197,14 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
 #pragma unroll
     for (int i = 0; i < AR; ++i) *reinterpret_cast<u32x4*>(A + swz(lr + RSTEP * i, lc)) = sa[i];
 #pragma unroll
-    for (int i = 0; i < BR; ++i) *reinterpret_cast<u32x4*>(B + swz(lr + RSTEP * i, lc)) = sb[i];
+    for (int i = 0; i < BR; ++i) {
+      if (BT) {
+        const int q = tid + NT * i, row = q / BCH, c = q % BCH;
+        *reinterpret_cast<u32x4*>(B + row * SBT + c * 16) = sb[i];
+      } else {
+        *reinterpret_cast<u32x4*>(B + swz(lr + RSTEP * i, lc)) = sb[i];
+      }
+    }
   };
 
   set_rows(g);
@@ -214,8 +241,16 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
         for (int i = 0; i < TM; ++i)
           a[i] = *reinterpret_cast<const bf16x8*>(A + swz(wm * WTM + i * 16 + (lane & 15), ch));
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          b[j] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WTN + j * 16 + (lane & 15), ch));
+        for (int j = 0; j < TN; ++j) {
+          if (BT) {  // k rows s*32 + 8*(lane>>4) + 0..3 and + 4..7 of column n, via transposed reads
+            const int r0 = s * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2);
+            const int col = wn * WTN + j * 16 + 4 * (lane & 3);
+            const v4s v8[2] = {lds_tr16(B + r0 * SBT + col * 2), lds_tr16(B + (r0 + 4) * SBT + col * 2)};
+            b[j] = __builtin_bit_cast(bf16x8, v8);
+          } else {
+            b[j] = *reinterpret_cast<const bf16x8*>(B + swz(wn * WTN + j * 16 + (lane & 15), ch));
+          }
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -407,11 +442,6 @@ __global__ __launch_bounds__(256) void bn_partial_finalize_kernel(
 // receiving one column), so no register or LDS transposition pass is needed. The reduction is
 // split over M across blocks (fp32 slabs), then one small kernel sums the slabs into dW.
 // LDS rows are padded by 32 B so the 4 rows of a transposed read fall on distinct banks.
-typedef short v4s __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
-}
 
 // PRO (2, 3): dY = a_n·G + b_n·Y2 + c_n is formed while staging (the BatchNorm-backward
 // elementwise pass folded in; G is the masked upstream gradient, Y2 the BN input; with 3 the ReLU
@@ -623,9 +653,9 @@ int num_cus() {
 }
 
 template <int BM, int BN, int WM, int WN>
-void launch_gemm(int pro, bool stats, dim3 grid, size_t lds, hipStream_t s, const uint16_t* x, const uint16_t* w,
-                 uint16_t* y, int64_t M, int N, int K, RowMap rm, const float* pss, float* part, int mt, int nt,
-                 int groups, const uint16_t* x2) {
+void launch_gemm(int pro, bool stats, bool bt, dim3 grid, size_t lds, hipStream_t s, const uint16_t* x,
+                 const uint16_t* w, uint16_t* y, int64_t M, int N, int K, RowMap rm, const float* pss, float* part,
+                 int mt, int nt, int groups, const uint16_t* x2) {
   auto go = [&](auto kern) {
     static size_t lds_set = 0;  // per kernel instantiation: opt in to > 64 KB of dynamic LDS once
     if (lds > 65536 && lds > lds_set) {
@@ -637,7 +667,11 @@ void launch_gemm(int pro, bool stats, dim3 grid, size_t lds, hipStream_t s, cons
 #define XDDP_G(P, S)                                                                                       \
   if (rm.stride > 1) go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, true>);                                   \
   else go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, false>)
-  if (pro == 3) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 3, false, false>);  // stride-1 input gradient only
+  if (bt) {  // input gradient on the untransposed weight: stride 1, no statistics
+    if (pro == 3) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 3, false, false, true>);
+    else if (pro == 2) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 2, false, false, true>);
+    else go(conv1x1_gemm_kernel<BM, BN, WM, WN, 0, false, false, true>);
+  } else if (pro == 3) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 3, false, false>);  // stride-1 input gradient only
   else if (pro == 2) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 2, false, false>);
   else if (pro == 1) { if (stats) XDDP_G(1, true); else XDDP_G(1, false); }
   else { if (stats) XDDP_G(0, true); else XDDP_G(0, false); }
@@ -652,14 +686,16 @@ void launch_gemm(int pro, bool stats, dim3 grid, size_t lds, hipStream_t s, cons
 // Returns (y [B, N, OH, OW] channels_last, partials [groups, 3, N] or undefined).
 std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride,
                                      const c10::optional<at::Tensor>& prologue_ss, bool stats,
-                                     const c10::optional<at::Tensor>& prologue_y) {
+                                     const c10::optional<at::Tensor>& prologue_y, bool w_t) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16, "conv1x1_gemm: x must be 4-D bf16 on GPU");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv1x1_gemm: x must be channels_last");
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 1 && w.size(3) == 1 && w.scalar_type() == at::kBFloat16,
               "conv1x1_gemm: w must be [N, K, 1, 1] bf16");
   TORCH_CHECK(stride >= 1, "conv1x1_gemm: bad stride");
-  const int64_t B = x.size(0), K = x.size(1), IH = x.size(2), IW = x.size(3), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K, "conv1x1_gemm: channel mismatch");
+  // w_t: w is [K, N, 1, 1] (the forward weight of the conv whose input gradient this is), used as Wᵀ
+  const int64_t B = x.size(0), K = x.size(1), IH = x.size(2), IW = x.size(3), N = w.size(w_t ? 1 : 0);
+  TORCH_CHECK(w.size(w_t ? 0 : 1) == K, "conv1x1_gemm: channel mismatch");
+  TORCH_CHECK(!w_t || (stride == 1 && !stats), "conv1x1_gemm: w_t is for stride-1 input gradients without stats");
   TORCH_CHECK(K % kBK == 0 && N % 64 == 0, "conv1x1_gemm: needs Cin % 64 == 0 and Cout % 64 == 0");
   auto wc = w.contiguous();  // [N][K] row-major for either weight memory format (1x1: same bytes)
   const int64_t OH = (IH - 1) / stride + 1, OW = (IW - 1) / stride + 1;
@@ -690,7 +726,8 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   at::Tensor part = stats ? at::empty({groups, 3, N}, x.options().dtype(at::kFloat)) : at::Tensor();
   RowMap rm{(int)OH, (int)OW, (int)IH, (int)IW, (int)stride};
   const dim3 grid(groups * ntiles);
-  const size_t lds = 2 * (size_t)(BM + BN) * 128 + (pro ? ncoef * K * sizeof(float) : 0);
+  const size_t bbytes = w_t ? (size_t)64 * (BN * 2 + 32) : (size_t)BN * 128;
+  const size_t lds = 2 * ((size_t)BM * 128 + bbytes) + (pro ? ncoef * K * sizeof(float) : 0);
   const auto* x2p = pro >= 2 ? reinterpret_cast<const uint16_t*>(prologue_y->data_ptr()) : nullptr;
   const auto* xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
   const auto* wp = reinterpret_cast<const uint16_t*>(wc.data_ptr());
@@ -698,11 +735,11 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   const float* pss = pro ? prologue_ss->data_ptr<float>() : nullptr;
   float* pp = stats ? part.data_ptr<float>() : nullptr;
   if (BN == 128)
-    launch_gemm<128, 128, 4, 2>(pro, stats, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,
-                          groups, x2p);
+    launch_gemm<128, 128, 4, 2>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles,
+                                ntiles, groups, x2p);
   else
-    launch_gemm<128, 64, 8, 1>(pro, stats, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,
-                         groups, x2p);
+    launch_gemm<128, 64, 8, 1>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles,
+                               ntiles, groups, x2p);
   return {y, part};
 }
 

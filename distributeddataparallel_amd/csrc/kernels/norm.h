@@ -25,7 +25,7 @@ std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, cons
 // 1x1 conv as an MFMA GEMM with BN prologue (previous BN's apply+ReLU) / epilogue (stats partials)
 std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride,
                                      const c10::optional<at::Tensor>& prologue_ss, bool stats,
-                                     const c10::optional<at::Tensor>& prologue_y);
+                                     const c10::optional<at::Tensor>& prologue_y, bool w_t);
 // 3x3 pad-1 conv (stride 1/2) as an implicit MFMA GEMM (csrc/kernels/conv3x3.hip)
 std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats);
 at::Tensor conv3x3_rot_weight(const at::Tensor& w);

@@ -70,9 +70,7 @@ class _Conv1x1BN(torch.autograd.Function):
             coef, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu, need_dres,
                                                      need_bn_w, dout2, bits, True)
             g = dres if need_dres else dout.contiguous(memory_format=torch.channels_last)
-            n_out, k_in = w.shape[0], w.shape[1]
-            wt = w.reshape(n_out, k_in).t().contiguous().view(k_in, n_out, 1, 1)
-            dx = C.conv1x1_gemm(g, wt, 1, coef, False, y)[0]
+            dx = _dgrad(C, g, w, coef, y)
             dw = C.conv1x1_wgrad(g, x, 1, w, y, coef)
             return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
                     None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None)
@@ -82,9 +80,7 @@ class _Conv1x1BN(torch.autograd.Function):
         if need_x and s == 1 and _dgrad_gemm():
             # dX[M, K] = dY[M, N] · W[N, K] is the same NT GEMM on (dY, Wᵀ): 35 % less time than
             # MIOpen's 1x1 dgrad over the ResNet-50 shapes (scripts/dgrad_bench.py)
-            n_out, k_in = w.shape[0], w.shape[1]
-            wt = w.reshape(n_out, k_in).t().contiguous().view(k_in, n_out, 1, 1)
-            dx = C.conv1x1_gemm(dy, wt, 1, None, False)[0]
+            dx = _dgrad(C, dy, w, None, None)
             need_x = False
         if need_w and _wgrad_gemm():
             # dW[N, K] = dYᵀ[N, M] · X[M, K] (strided pixel rows for the downsample): 14 % less
@@ -137,6 +133,16 @@ class _Conv3x3BNReLU(torch.autograd.Function):
             dw = gw if need_w else None
         return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
                 None, None, None, None, None, None, None)
+
+
+def _dgrad(C, g, w, coef, y):
+    """dX = dY · W on the MFMA GEMM, W read K-major through transposed LDS reads (no transposed
+    weight copy; XDDP_GEMM_WT=0 makes the copy instead, A/B switch)."""
+    if os.environ.get("XDDP_GEMM_WT", "1") != "0":
+        return C.conv1x1_gemm(g, w, 1, coef, False, y, True)[0]
+    n_out, k_in = w.shape[0], w.shape[1]
+    wt = w.reshape(n_out, k_in).t().contiguous().view(k_in, n_out, 1, 1)
+    return C.conv1x1_gemm(g, wt, 1, coef, False, y)[0]
 
 
 def _conv3x3() -> bool:

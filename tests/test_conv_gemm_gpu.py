@@ -93,6 +93,13 @@ def test_bn_backward_prologue_in_gemms(b, cin, h, w, cout, masked):
     dx = C.conv1x1_gemm(g, wt, 1, coef, False, yb)[0]
     ref = C.conv1x1_gemm(dy, wt, 1, None, False)[0]
     torch.testing.assert_close(dx.float(), ref.float(), rtol=2e-2, atol=2e-2 * ref.float().abs().max().item())
+    # the same GEMMs reading the forward weight W = [N_out, K_in] K-major (w_t): no transposed copy
+    wf = wt.view(cin, cout).t().contiguous().view(cout, cin, 1, 1)
+    dxt = C.conv1x1_gemm(g, wf, 1, coef, False, yb, True)[0]
+    torch.testing.assert_close(dxt, dx, rtol=0, atol=0)
+    reft = C.conv1x1_gemm(dy, wf, 1, None, False, None, True)[0]
+    dref = F.conv_transpose2d(dy.float(), wf.float())  # dX = dY · W in fp32
+    torch.testing.assert_close(reft.float(), dref, rtol=2e-2, atol=2e-2 * dref.abs().max().item())
     like = torch.empty(cout, cin, 1, 1, device="cuda", dtype=torch.float32)
     dw = C.conv1x1_wgrad(g, x, 1, like, yb, coef)
     refw = C.conv1x1_wgrad(dy, x, 1, like)
