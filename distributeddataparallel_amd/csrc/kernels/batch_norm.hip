@@ -675,5 +675,33 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
   return {coef_only ? coef : dx, dw, db, dres};
 }
 
+// BN backward coefficients from partials produced elsewhere (the EPI epilogue of conv_gemm.hip):
+// part [groups, C, 2] = (sum g, sum g·(x - mean)) -> (coef [3, C] = (k1, k2, k3 - k2·mean), dw, db).
+std::vector<at::Tensor> bn_backward_from_partials(const at::Tensor& part, int64_t M,
+                                                  const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
+                                                  const at::Tensor& invstd, bool need_dweight) {
+  TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.size(2) == 2 && part.scalar_type() == at::kFloat &&
+                  part.is_contiguous(),
+              "bn_backward_from_partials: partials must be float [groups, C, 2]");
+  const int64_t C = part.size(1);
+  TORCH_CHECK(C % 8 == 0 && mean.numel() == C && invstd.numel() == C, "bn_backward_from_partials: bad channel count");
+  auto stream = c10::hip::getCurrentHIPStream(part.device().index()).stream();
+  auto coef = at::empty({3, C}, part.options());
+  const bool has_w = weight.has_value() && weight->defined();
+  const auto wdt = has_w ? weight->scalar_type() : at::kFloat;
+  at::Tensor dw = (has_w && need_dweight) ? at::empty({C}, weight->options()) : at::Tensor();
+  at::Tensor db = (has_w && need_dweight) ? at::empty({C}, weight->options()) : at::Tensor();
+  dispatch_w(wdt, [&](auto tag_w) {
+    using W = decltype(tag_w);
+    hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(64), 0, stream, part.data_ptr<float>(),
+                       (int)part.size(0), (int)C, M, has_w ? reinterpret_cast<const W*>(weight->data_ptr()) : nullptr,
+                       invstd.data_ptr<float>(), dw.defined() ? reinterpret_cast<W*>(dw.data_ptr()) : nullptr,
+                       db.defined() ? reinterpret_cast<W*>(db.data_ptr()) : nullptr, coef.data_ptr<float>(),
+                       mean.data_ptr<float>());
+    XDDP_HIP_CHECK(hipGetLastError());
+  });
+  return {coef, dw, db};
+}
+
 }  // namespace kernels
 }  // namespace xddp

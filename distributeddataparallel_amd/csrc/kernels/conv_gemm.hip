@@ -56,6 +56,20 @@ __device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
 }
 
+// EPI (input-gradient GEMM of a bottleneck's conv1 whose input is the previous block's output):
+// the C tile dX (gradient through conv1) is combined with the gradient the same tensor gets
+// through the identity path (add), masked by the previous block's final ReLU (bits), stored as
+// g — that block's d(residual) / BN-backward input — and reduced per channel into the previous
+// BN's backward partials (sum g, sum g·(y - mean)) in bn_bwd_finalize's [groups][C][2] layout.
+// The previous block's separate BN-backward reduce pass (which re-read both gradients) is gone.
+struct EpiBN {
+  const uint16_t* add;
+  const uint16_t* y;
+  const uint8_t* bits;
+  const float* mean;
+  float* part;
+};
+
 struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every stride-th pixel)
   int OH, OW, IH, IW, stride;
   template <bool STRIDED>
@@ -75,11 +89,11 @@ struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every st
 // BT: the B operand is given K-major (Wt[k][n], e.g. the forward weight W[n_out][k_in] used as Wᵀ by
 // the input-gradient GEMM): staged as [64 k][BN n] rows (padded 32 B) and read into fragments with
 // the transposing ds_read_b64_tr_b16, so no transposed weight copy is made.
-template <int BM, int BN, int WM, int WN, int PRO, bool STATS, bool STRIDED, bool BT = false>
+template <int BM, int BN, int WM, int WN, int PRO, bool STATS, bool STRIDED, bool BT = false, bool EPI = false>
 __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, int64_t M, int N,
     int K, RowMap rm, const float* __restrict__ pro_ss, float* __restrict__ part, int mtiles, int ntiles,
-    int groups, const uint16_t* __restrict__ X2) {
+    int groups, const uint16_t* __restrict__ X2, EpiBN epi) {
   constexpr int NT = 64 * WM * WN, RSTEP = NT / 8;  // threads; rows staged per pass (8 chunks per row)
   constexpr int AR = BM / RSTEP, BR = BN / RSTEP;    // 16-B loads per thread per operand tile
   constexpr int WTM = BM / WM, WTN = BN / WN;        // wave tile
@@ -107,6 +121,8 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
   u32x4 st_k = {0, 0, 0, 0};  // the shift, kept as the 8 packed bf16 values it came from
 #pragma unroll
   for (int e = 0; e < 8; ++e) st_s[e] = st_ss[e] = 0.f;
+  float ep_mu[8];  // EPI: the previous BN's mean of this thread's 8 channels (st_s / st_ss hold its sums)
+  if (EPI) dev::Vec8<float>::ld(epi.mean + n0 + cc * 8, ep_mu);
 
   const uint16_t* wrow[BR];
   constexpr int BCH = BN / 8;  // BT: 16-B chunks per staged k row (64 * BCH == NT * BR)
@@ -289,7 +305,27 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
     for (int q = tid; q < BM * CPR; q += NT) {
       const int row = q / CPR;
       if (row < rows_valid) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
+        u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
+        if (EPI) {
+          const int64_t e0 = (m0 + row) * N + n0 + cc * 8;
+          const u32x4 ad = *reinterpret_cast<const u32x4*>(epi.add + e0);
+          const u32x4 yv = *reinterpret_cast<const u32x4*>(epi.y + e0);
+          const uint32_t mb = epi.bits[e0 >> 3];
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            float g0 = __uint_as_float(v[h] << 16) + __uint_as_float(ad[h] << 16);
+            float g1 = __uint_as_float(v[h] & 0xffff0000u) + __uint_as_float(ad[h] & 0xffff0000u);
+            g0 = ((mb >> (2 * h)) & 1u) ? g0 : 0.f;
+            g1 = ((mb >> (2 * h + 1)) & 1u) ? g1 : 0.f;
+            v[h] = dev::pack_bf16x2(g0, g1);
+            g0 = __uint_as_float(v[h] << 16);  // the sums see g at storage precision
+            g1 = __uint_as_float(v[h] & 0xffff0000u);
+            st_s[2 * h] += g0;
+            st_s[2 * h + 1] += g1;
+            st_ss[2 * h] = fmaf(g0, __uint_as_float(yv[h] << 16) - ep_mu[2 * h], st_ss[2 * h]);
+            st_ss[2 * h + 1] = fmaf(g1, __uint_as_float(yv[h] & 0xffff0000u) - ep_mu[2 * h + 1], st_ss[2 * h + 1]);
+          }
+        }
         if (NTSTORE) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + (m0 + row) * N + n0 + cc * 8));
         else *reinterpret_cast<u32x4*>(Y + (m0 + row) * N + n0 + cc * 8) = v;
         if (STATS) {
@@ -307,6 +343,38 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
       }
     }
     lds_barrier();  // Cs aliases the operand buffers the next tile stores into
+  }
+
+  if (EPI) {
+    // plain sums: add over the lanes sharing cc, then over the waves through LDS
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        st_s[e] += __shfl_xor(st_s[e], o, 64);
+        st_ss[e] += __shfl_xor(st_ss[e], o, 64);
+      }
+    }
+    constexpr int NW = NT / 64;
+    float* red = reinterpret_cast<float*>(smem);  // [NW][BN][2]
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wid * BN + cc * 8 + e) * 2 + 0] = st_s[e];
+        red[(wid * BN + cc * 8 + e) * 2 + 1] = st_ss[e];
+      }
+    }
+    lds_barrier();
+    for (int c = tid; c < BN; c += NT) {
+      float sd = 0.f, sdx = 0.f;
+      for (int w = 0; w < NW; ++w) {
+        sd += red[(w * BN + c) * 2 + 0];
+        sdx += red[(w * BN + c) * 2 + 1];
+      }
+      epi.part[((int64_t)g * N + n0 + c) * 2 + 0] = sd;
+      epi.part[((int64_t)g * N + n0 + c) * 2 + 1] = sdx;
+    }
+    return;
   }
 
   if (STATS) {
@@ -655,20 +723,22 @@ int num_cus() {
 template <int BM, int BN, int WM, int WN>
 void launch_gemm(int pro, bool stats, bool bt, dim3 grid, size_t lds, hipStream_t s, const uint16_t* x,
                  const uint16_t* w, uint16_t* y, int64_t M, int N, int K, RowMap rm, const float* pss, float* part,
-                 int mt, int nt, int groups, const uint16_t* x2) {
+                 int mt, int nt, int groups, const uint16_t* x2, const EpiBN& epi) {
   auto go = [&](auto kern) {
     static size_t lds_set = 0;  // per kernel instantiation: opt in to > 64 KB of dynamic LDS once
     if (lds > 65536 && lds > lds_set) {
       XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       lds_set = lds;
     }
-    hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, s, x, w, y, M, N, K, rm, pss, part, mt, nt, groups, x2);
+    hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, s, x, w, y, M, N, K, rm, pss, part, mt, nt, groups, x2,
+                       epi);
   };
 #define XDDP_G(P, S)                                                                                       \
   if (rm.stride > 1) go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, true>);                                   \
   else go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, false>)
   if (bt) {  // input gradient on the untransposed weight: stride 1, no statistics
-    if (pro == 3) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 3, false, false, true>);
+    if (epi.part) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 0, false, false, true, true>);
+    else if (pro == 3) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 3, false, false, true>);
     else if (pro == 2) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 2, false, false, true>);
     else go(conv1x1_gemm_kernel<BM, BN, WM, WN, 0, false, false, true>);
   } else if (pro == 3) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 3, false, false>);  // stride-1 input gradient only
@@ -686,7 +756,9 @@ void launch_gemm(int pro, bool stats, bool bt, dim3 grid, size_t lds, hipStream_
 // Returns (y [B, N, OH, OW] channels_last, partials [groups, 3, N] or undefined).
 std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride,
                                      const c10::optional<at::Tensor>& prologue_ss, bool stats,
-                                     const c10::optional<at::Tensor>& prologue_y, bool w_t) {
+                                     const c10::optional<at::Tensor>& prologue_y, bool w_t,
+                                     const c10::optional<at::Tensor>& epi_add, const c10::optional<at::Tensor>& epi_y,
+                                     const c10::optional<at::Tensor>& epi_bits, const c10::optional<at::Tensor>& epi_mean) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16, "conv1x1_gemm: x must be 4-D bf16 on GPU");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv1x1_gemm: x must be channels_last");
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 1 && w.size(3) == 1 && w.scalar_type() == at::kBFloat16,
@@ -714,6 +786,17 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
                 "conv1x1_gemm: prologue_y must match x (bf16 channels_last), stride 1, no stats");
   auto y = at::empty({B, N, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  const bool epi_on = epi_add.has_value() && epi_add->defined();
+  if (epi_on) {
+    TORCH_CHECK(w_t && pro == 0, "conv1x1_gemm: the BN-reduce epilogue needs w_t and no prologue");
+    TORCH_CHECK(epi_add->sizes() == y.sizes() && epi_add->scalar_type() == at::kBFloat16 &&
+                    epi_add->is_contiguous(at::MemoryFormat::ChannelsLast) && epi_y.has_value() &&
+                    epi_y->sizes() == y.sizes() && epi_y->scalar_type() == at::kBFloat16 &&
+                    epi_y->is_contiguous(at::MemoryFormat::ChannelsLast) && epi_bits.has_value() &&
+                    epi_bits->scalar_type() == at::kByte && epi_bits->numel() * 8 == y.numel() &&
+                    epi_mean.has_value() && epi_mean->scalar_type() == at::kFloat && epi_mean->numel() == N,
+                "conv1x1_gemm: epilogue tensors must match the output (bf16 channels_last, uint8 bits, float mean)");
+  }
   const int BM = 128, BN = (N % 128 == 0) ? 128 : 64;
   const int mtiles = (int)((M + BM - 1) / BM), ntiles = (int)(N / BN);
   // 2-3 blocks per CU resident (LDS 48-64 KB, <= 128 VGPRs): size the grid to a few rounds
@@ -723,7 +806,12 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   }();
   const int target = num_cus() * blocks_per_cu;
   int groups = std::max(1, std::min(mtiles, (target + ntiles - 1) / ntiles));
-  at::Tensor part = stats ? at::empty({groups, 3, N}, x.options().dtype(at::kFloat)) : at::Tensor();
+  at::Tensor part = stats ? at::empty({groups, 3, N}, x.options().dtype(at::kFloat))
+                          : (epi_on ? at::empty({groups, N, 2}, x.options().dtype(at::kFloat)) : at::Tensor());
+  EpiBN epi{nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (epi_on)
+    epi = EpiBN{reinterpret_cast<const uint16_t*>(epi_add->data_ptr()), reinterpret_cast<const uint16_t*>(epi_y->data_ptr()),
+                epi_bits->data_ptr<uint8_t>(), epi_mean->data_ptr<float>(), part.data_ptr<float>()};
   RowMap rm{(int)OH, (int)OW, (int)IH, (int)IW, (int)stride};
   const dim3 grid(groups * ntiles);
   const size_t bbytes = w_t ? (size_t)64 * (BN * 2 + 32) : (size_t)BN * 128;
@@ -733,13 +821,13 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   const auto* wp = reinterpret_cast<const uint16_t*>(wc.data_ptr());
   auto* yp = reinterpret_cast<uint16_t*>(y.data_ptr());
   const float* pss = pro ? prologue_ss->data_ptr<float>() : nullptr;
-  float* pp = stats ? part.data_ptr<float>() : nullptr;
+  float* pp = stats ? part.data_ptr<float>() : nullptr;  // (EPI partials travel in epi)
   if (BN == 128)
     launch_gemm<128, 128, 4, 2>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles,
-                                ntiles, groups, x2p);
+                                ntiles, groups, x2p, epi);
   else
     launch_gemm<128, 64, 8, 1>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles,
-                               ntiles, groups, x2p);
+                               ntiles, groups, x2p, epi);
   return {y, part};
 }
 

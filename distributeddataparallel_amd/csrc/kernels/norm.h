@@ -25,7 +25,14 @@ std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, cons
 // 1x1 conv as an MFMA GEMM with BN prologue (previous BN's apply+ReLU) / epilogue (stats partials)
 std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride,
                                      const c10::optional<at::Tensor>& prologue_ss, bool stats,
-                                     const c10::optional<at::Tensor>& prologue_y, bool w_t);
+                                     const c10::optional<at::Tensor>& prologue_y, bool w_t,
+                                     const c10::optional<at::Tensor>& epi_add, const c10::optional<at::Tensor>& epi_y,
+                                     const c10::optional<at::Tensor>& epi_bits, const c10::optional<at::Tensor>& epi_mean);
+// BN backward from external (sum g, sum g·(x - mean)) partials [groups, C, 2]: (coef [3, C] with the
+// mean folded in, dweight, dbias)
+std::vector<at::Tensor> bn_backward_from_partials(const at::Tensor& part, int64_t M,
+                                                  const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
+                                                  const at::Tensor& invstd, bool need_dweight);
 // 3x3 pad-1 conv (stride 1/2) as an implicit MFMA GEMM (csrc/kernels/conv3x3.hip)
 std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats);
 at::Tensor conv3x3_rot_weight(const at::Tensor& w);

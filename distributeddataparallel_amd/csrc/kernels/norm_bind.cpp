@@ -17,7 +17,10 @@ void bind_norm_kernels(py::module_& m) {
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("scale_shift"), py::arg("residual"), py::arg("relu"),
         py::arg("save_mask"), py::arg("num_batches_tracked"));
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("prologue_ss"),
-        py::arg("stats"), py::arg("prologue_y") = py::none(), py::arg("w_t") = false);
+        py::arg("stats"), py::arg("prologue_y") = py::none(), py::arg("w_t") = false, py::arg("epi_add") = py::none(),
+        py::arg("epi_y") = py::none(), py::arg("epi_bits") = py::none(), py::arg("epi_mean") = py::none());
+  m.def("bn_backward_from_partials", &bn_backward_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),
+        py::arg("mean"), py::arg("invstd"), py::arg("need_dweight"));
   m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"));
   m.def("conv3x3_rot_weight", &conv3x3_rot_weight, py::arg("w"));
   m.def("conv3x3_wgrad", &conv3x3_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"));

@@ -96,9 +96,13 @@ class Bottleneck(nn.Module):
             from ..ops.conv_bn import conv1x1_bn_act, conv3x3_bn_relu
 
             identity = xr if self.downsample is None else conv1x1_bn_act(xr, self.downsample[0], self.downsample[1])
-            out = conv1x1_bn_act(x, self.conv1, self.bn1, relu=True)
+            # previous block's output consumed by conv1 and the identity: their backward hands the
+            # identity gradient to conv1's input-gradient GEMM epilogue (ops/conv_bn.py:EpiLink)
+            link = getattr(x, "_xddp_epi", None) if self.downsample is None else None
+            out = conv1x1_bn_act(x, self.conv1, self.bn1, relu=True, link_x=link)
             out = self.act2(conv3x3_bn_relu(out, self.conv2, self.bn2))
-            return conv1x1_bn_act(out, self.conv3, self.bn3, residual=identity, relu=True, dual_output=True)
+            return conv1x1_bn_act(out, self.conv3, self.bn3, residual=identity, relu=True, dual_output=True,
+                                  link_res=link)
         identity = xr if self.downsample is None else self.downsample(xr)
         out = self.act1(self.bn1(self.conv1(x)))
         out = self.act2(self.bn2(self.conv2(out)))

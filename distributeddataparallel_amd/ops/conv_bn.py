@@ -31,10 +31,25 @@ from .._native import load
 __all__ = ["conv1x1_bn_act", "conv3x3_bn_relu", "conv_bn_supported"]
 
 
+class EpiLink:
+    """Backward hand-off between a bottleneck's last conv+BN+add+ReLU (the producer of a dual
+    output) and the next block's two consumers of that output: its conv3 BN backward leaves the
+    identity-path gradient here (``add``) instead of returning it, and its conv1 input-gradient
+    GEMM folds ``add``, the producer's ReLU mask and the producer's BN-backward reduction into its
+    epilogue (``conv1x1_gemm(..., epi_*)``), leaving the BN partials here (``part``). The producer's
+    backward then starts from the finished gradient g and the partials: its separate reduce pass
+    over (dout, dout2, y, mask) is gone (csrc/kernels/conv_gemm.hip, EpiBN)."""
+
+    __slots__ = ("y", "bits", "mean", "add", "part")
+
+    def __init__(self):
+        self.y = self.bits = self.mean = self.add = self.part = None
+
+
 class _Conv1x1BN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, residual, relu, dual,
-                stride):
+                stride, link_out, link_x, link_res):
         C = load()
         ctx.set_materialize_grads(False)
         y, part = C.conv1x1_gemm(x, w, stride, None, True)
@@ -45,6 +60,12 @@ class _Conv1x1BN(torch.autograd.Function):
         out, bits = C.bn_apply(y, ss, residual, relu, keep_mask, nbt)
         ctx.relu, ctx.has_res, ctx.stride = relu, residual is not None, stride
         ctx.save_for_backward(x, w, y, bits if keep_mask else None, weight, mean, invstd, ss)
+        ctx.link_out, ctx.link_x, ctx.link_res = link_out, link_x, link_res
+        if link_out is not None:
+            if keep_mask and dual:
+                link_out.y, link_out.bits, link_out.mean = y, bits, mean
+            else:
+                ctx.link_out = None
         if dual:  # two consumers: gradients arrive separately and are summed in the BN backward kernel
             return out, out.view_as(out)
         return out
@@ -53,14 +74,44 @@ class _Conv1x1BN(torch.autograd.Function):
     def backward(ctx, dout, dout2=None):
         C = load()
         x, w, y, bits, weight, mean, invstd, ss = ctx.saved_tensors
+        lo = ctx.link_out
+        epi_part = None
+        if lo is not None:  # the next block's conv1 took (or left) the identity-path gradient
+            if lo.part is not None:
+                epi_part, dout2 = lo.part, None
+            elif lo.add is not None:
+                dout2 = lo.add if dout2 is None else dout2 + lo.add
+            lo.y = lo.bits = lo.mean = lo.add = lo.part = None
         if dout is None:
             dout, dout2 = dout2, None
         if dout is None:
-            return (None,) * 14
+            return (None,) * 17
         need_bn_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         s = ctx.stride
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         need_dres = ctx.has_res and ctx.needs_input_grad[10]
+        if epi_part is not None:
+            # dout is g = mask·(d conv1 + d identity) from the next block's conv1 GEMM epilogue,
+            # which also reduced this BN's backward partials
+            M = y.numel() // y.size(1)
+            coef, dw_bn, db_bn = C.bn_backward_from_partials(epi_part, M, weight, mean, invstd, need_bn_w)
+            g = dout
+            dres = g if need_dres else None
+            dx = dw = None
+            if s == 1 and need_x and _dgrad_gemm():
+                dx = _dgrad(C, g, w, coef, y)
+            if need_w and s == 1 and _wgrad_gemm():
+                dw = C.conv1x1_wgrad(g, x, 1, w, y, coef)
+            if (need_x and dx is None) or (need_w and dw is None):
+                v = lambda i: coef[i].view(1, -1, 1, 1)  # noqa: E731
+                dy = (v(0) * g.float() + v(1) * y.float() + v(2)).to(g.dtype).contiguous(
+                    memory_format=torch.channels_last)
+                gx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0],
+                                                                1, [need_x and dx is None, need_w and dw is None,
+                                                                    False])
+                dx = gx if dx is None else dx
+                dw = gw if dw is None else dw
+            return _grads(ctx, dx, dw, dw_bn, db_bn, dres)
         if (s == 1 and need_x and need_w and _bwd_prologue() and _dgrad_gemm() and _wgrad_gemm()
                 and (need_dres or (dout2 is None and bits is None and (not ctx.relu or _bwd_prologue_masked())))):
             # BN-backward elementwise pass folded into both GEMMs: dY = k1·g + k2·y + k3' is formed
@@ -72,15 +123,21 @@ class _Conv1x1BN(torch.autograd.Function):
             g = dres if need_dres else dout.contiguous(memory_format=torch.channels_last)
             dx = _dgrad(C, g, w, coef, y)
             dw = C.conv1x1_wgrad(g, x, 1, w, y, coef)
-            return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
-                    None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None)
+            return _grads(ctx, dx, dw, dw_bn, db_bn, dres)
         dy, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu, need_dres,
                                                need_bn_w, dout2, bits)
         dx = dw = None
         if need_x and s == 1 and _dgrad_gemm():
             # dX[M, K] = dY[M, N] · W[N, K] is the same NT GEMM on (dY, Wᵀ): 35 % less time than
             # MIOpen's 1x1 dgrad over the ResNet-50 shapes (scripts/dgrad_bench.py)
-            dx = _dgrad(C, dy, w, None, None)
+            lx = ctx.link_x
+            if lx is not None and lx.add is not None and lx.y is not None and _epi():
+                # the previous block's output gradient: dX + identity-path gradient, masked by its
+                # ReLU and reduced into its BN-backward partials in this GEMM's epilogue
+                dx, lx.part = C.conv1x1_gemm(dy, w, 1, None, False, None, True, lx.add, lx.y, lx.bits, lx.mean)
+                lx.add = None
+            else:
+                dx = _dgrad(C, dy, w, None, None)
             need_x = False
         if need_w and _wgrad_gemm():
             # dW[N, K] = dYᵀ[N, M] · X[M, K] (strided pixel rows for the downsample): 14 % less
@@ -92,8 +149,15 @@ class _Conv1x1BN(torch.autograd.Function):
                                                             [need_x, need_w, False])
             dx = gx if need_x else dx
             dw = gw if need_w else dw
-        return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
-                None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None)
+        return _grads(ctx, dx, dw, dw_bn, db_bn, dres)
+
+
+def _grads(ctx, dx, dw, dw_bn, db_bn, dres):
+    """The 17 input gradients of _Conv1x1BN; a linked residual gradient goes to the consumer link."""
+    if dres is not None and ctx.link_res is not None:
+        ctx.link_res.add, dres = dres, None
+    return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
+            None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None, None, None, None)
 
 
 class _Conv3x3BNReLU(torch.autograd.Function):
@@ -150,6 +214,12 @@ def _conv3x3() -> bool:
     return os.environ.get("XDDP_CONV3X3", "1") != "0"
 
 
+def _epi() -> bool:
+    """XDDP_CONV_EPI=0 keeps the previous block's BN-backward reduce pass separate instead of
+    folding it into the next block's conv1 input-gradient GEMM epilogue (A/B switch)."""
+    return os.environ.get("XDDP_CONV_EPI", "1") != "0"
+
+
 def _dgrad_gemm() -> bool:
     """XDDP_CONV_DGRAD_GEMM=0 sends the stride-1 input gradient back to MIOpen (A/B switch)."""
     return os.environ.get("XDDP_CONV_DGRAD_GEMM", "1") != "0"
@@ -198,12 +268,21 @@ def conv3x3_bn_relu(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module):
 
 
 def conv1x1_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, residual: Optional[torch.Tensor] = None,
-                   relu: bool = False, dual_output: bool = False):
-    """``relu(bn(conv(x)) [+ residual])`` with BN statistics from the conv epilogue when supported."""
+                   relu: bool = False, dual_output: bool = False, link_x: Optional[EpiLink] = None,
+                   link_res: Optional[EpiLink] = None):
+    """``relu(bn(conv(x)) [+ residual])`` with BN statistics from the conv epilogue when supported.
+
+    link_x / link_res: the :class:`EpiLink` of the block output that is this conv's input /
+    this op's residual (``x._xddp_epi`` of a dual output); with dual_output and residual + ReLU
+    the returned output carries a fresh link for the next block."""
     if conv.kernel_size != (1, 1) or not conv_bn_supported(x, conv, bn) or (residual is not None and not (
             residual.shape[0] == x.shape[0] and residual.dtype == x.dtype
             and residual.is_contiguous(memory_format=torch.channels_last))):
         return bn(conv(x), residual=residual, relu=relu, dual_output=dual_output)
-    return _Conv1x1BN.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                            bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), residual, relu,
-                            dual_output, int(conv.stride[0]))
+    link_out = EpiLink() if (dual_output and residual is not None and relu and _epi()) else None
+    out = _Conv1x1BN.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                           bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), residual, relu,
+                           dual_output, int(conv.stride[0]), link_out, link_x, link_res)
+    if link_out is not None:
+        out[0]._xddp_epi = link_out
+    return out

@@ -187,3 +187,65 @@ def test_bottleneck_resnet_conv_bn_fusion_matches_unfused(monkeypatch):
     assert err(gf) < 1.5 * err(gu) + 0.02, (err(gf), err(gu))
     cos = lambda g: F.cosine_similarity(g, g32, dim=0).item()  # noqa: E731
     assert cos(gf) > cos(gu) - 0.02, (cos(gf), cos(gu))
+
+
+@pytest.mark.parametrize("b,cin,h,w,cout", [(2, 64, 14, 14, 256), (3, 64, 9, 7, 128), (2, 128, 7, 7, 64)])
+def test_dgrad_bn_reduce_epilogue(b, cin, h, w, cout):
+    """Input-gradient GEMM with the EPI epilogue: g = mask·(dY·W + add) stored, and per-channel
+    (sum g, sum g·(y - mean)) partials, against fp32 PyTorch of the same math."""
+    torch.manual_seed(5)
+    dy = _x(b, cin, h, w)  # gradient at the conv1 output: [M, N_out = cin]
+    wf = (torch.randn(cin, cout, 1, 1, device="cuda") / cin ** 0.5).to(torch.bfloat16)  # W[N_out, K_in = cout]
+    add, yb = _x(b, cout, h, w), _x(b, cout, h, w, offset=0.3)
+    keep = torch.rand(b, cout, h, w, device="cuda") > 0.4
+    flat = keep.permute(0, 2, 3, 1).reshape(-1, 8).to(torch.int32)
+    bits = (flat << torch.arange(8, device="cuda", dtype=torch.int32)).sum(1).to(torch.uint8)
+    mean = yb.float().mean((0, 2, 3))
+    g, part = C.conv1x1_gemm(dy, wf, 1, None, False, None, True, add, yb, bits, mean)
+    ref = torch.where(keep, F.conv_transpose2d(dy.float(), wf.float()) + add.float(), 0.0)
+    torch.testing.assert_close(g.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+    assert part.dim() == 3 and part.size(1) == cout and part.size(2) == 2
+    sd, sdx = part.sum(0).unbind(1)
+    gq = g.float()
+    torch.testing.assert_close(sd, gq.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(sdx, (gq * (yb.float() - mean.view(1, -1, 1, 1))).sum((0, 2, 3)), rtol=1e-3,
+                               atol=1e-2)
+    # finalize: (k1, k2, k3 - k2·mean) and (dweight, dbias) of the previous BN
+    weight = torch.rand(cout, device="cuda") + 0.5
+    invstd = torch.rand(cout, device="cuda") + 0.5
+    M = b * h * w
+    coef, dwt, dbs = C.bn_backward_from_partials(part, M, weight, mean, invstd, True)
+    torch.testing.assert_close(dbs, sd, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dwt, sdx * invstd, rtol=1e-4, atol=1e-4)
+    k1, k2 = weight * invstd, -weight * invstd ** 3 * sdx / M
+    k3 = -weight * invstd * sd / M - k2 * mean
+    torch.testing.assert_close(coef, torch.stack([k1, k2, k3]), rtol=1e-4, atol=1e-5)
+
+
+def test_bottleneck_epilogue_handoff_matches_separate_pass(monkeypatch):
+    """ResNet with two bottlenecks in a stage (so one block output feeds a non-downsample block):
+    the conv1-epilogue hand-off of the previous block's BN backward (XDDP_CONV_EPI=1) gives the
+    same gradients as the separate reduce pass (=0)."""
+    from distributeddataparallel_amd.models.resnet import Bottleneck, ResNet
+    from distributeddataparallel_amd.ops import FusedBatchNorm2d
+
+    torch.manual_seed(6)
+    m = ResNet(Bottleneck, [2, 2, 1, 1], norm_layer=FusedBatchNorm2d).cuda().to(torch.bfloat16)
+    m = m.to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 64, 64, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (4,), device="cuda")
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+
+    def run(flag):
+        monkeypatch.setenv("XDDP_CONV_EPI", flag)
+        m.load_state_dict(sd)
+        m.zero_grad()
+        loss = F.cross_entropy(m(x).float(), y)
+        loss.backward()
+        return loss.item(), torch.cat([p.grad.float().flatten() for p in m.parameters()])
+
+    l1, g1 = run("1")
+    l0, g0 = run("0")
+    assert abs(l1 - l0) < 1e-6 * max(1.0, abs(l0))
+    assert ((g1 - g0).norm() / g0.norm()).item() < 2e-2
+    assert F.cosine_similarity(g1, g0, dim=0).item() > 0.999
