@@ -4,33 +4,164 @@
 BASELINE.json metric: "images/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X; scaling
 efficiency", config "ResNet-50 bf16 DDP on 8×MI355X, synthetic ImageNet-shaped input".
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched
-by ``torch.distributed.run`` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in the env), one rank per
-GPU over RCCL. W untimed steps, then exactly K timed steps bracketed by barrier +
-synchronize on both sides; the MAX elapsed over ranks is reported; rank 0 prints ONE JSON
-line. Weak scaling: the per-GPU batch is fixed as N grows.
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``. W untimed steps, then
+exactly K timed steps bracketed by barrier + synchronize on both sides; the MAX elapsed over
+ranks is reported; rank 0 prints ONE JSON line. Weak scaling: the per-GPU batch is fixed as N
+grows. Launch modes for N>1 (one rank per GPU over RCCL):
 
-Each step is a full training step: H2D-free synthetic batch (already on device), forward,
-cross-entropy, backward with bucketed RCCL all-reduce overlapped with backward (xddp
-Reducer), fused SGD (momentum 0.9, wd 1e-4, fp32 master weights) — nothing skipped.
+* under ``torch.distributed.run`` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in the env);
+* directly (``python bench.py --gpus N``): the parent starts N fresh child processes with
+  RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT set — before touching the GPU — forwards
+  rank 0's JSON line and exits non-zero if any child fails (the reference's own launch model:
+  ``world_size = device_count()`` + ``mp.spawn``, ``ref:dpp.py:60-62``).
+
+Each step is a full training step: synthetic batch already on the device, forward,
+cross-entropy, backward with bucketed RCCL all-reduce overlapped with backward (xddp Reducer),
+fused SGD (momentum 0.9, wd 1e-4, fp32 master weights) — nothing skipped. Besides the headline
+number the JSON reports what the communicator saw (``nranks``), the rebuilt bucket layout, the
+Reducer's sampled backward comm / overlap times (measured AFTER the timed region, in extra
+diagnostic steps, so the timed loop is untouched), the achieved all-reduce bus bandwidth per
+bucket size (N>1), model-FLOPs utilisation, and, given ``--baseline-json`` of the N=1 run, the
+scaling efficiency.
+
+CPU rehearsal of the same paths: ``python bench.py --gpus 2 --device cpu --backend cpu --model mlp``.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
+import threading
 import time
 
-# MIOpen conv tuning (MI355X-specific): an exhaustive search picks conv solutions ~11% faster
-# than MIOpen's default heuristic for this config but costs ~200 s. The repo ships the resulting
-# find-db + perf-db + compiled-kernel cache (tuning/miopen, generated on MI355X by
-# scripts/gpu_tune.sh); each process copies it to a private temp dir (MIOpen writes to it) and
-# MIOpen's default DYNAMIC_HYBRID find mode resolves every conv from the db (first step <1 s).
+REPO = os.path.dirname(os.path.abspath(__file__))
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
 
 
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU)")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch-size", type=int, default=None, help="per-rank (micro-)batch")
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
+    ap.add_argument("--backend", default=None, help="xddp backend: rccl (GPU default) or cpu")
+    ap.add_argument("--impl", choices=["xddp", "torch"], default="xddp",
+                    help="xddp = this framework; torch = torch.nn.parallel.DDP reference stack (comparison only)")
+    ap.add_argument("--norm", choices=["xddp", "torch"], default="xddp", help="BatchNorm implementation")
+    ap.add_argument("--bucket-cap-mb", type=float, default=None,
+                    help="explicit cap = reference bucketing; default = xGMI bucket policy")
+    ap.add_argument("--bucket-policy", default=None, help="xgmi | reference")
+    ap.add_argument("--comm-dtype", default="none", help="gradient comm dtype (none = param dtype)")
+    ap.add_argument("--grad-as-bucket-view", type=int, default=1)
+    ap.add_argument("--channels-last", type=int, default=1)
+    ap.add_argument("--no-sync-accum", type=int, default=1,
+                    help="micro-batches per optimizer step: k-1 under no_sync(), the last one syncs "
+                         "(each micro-batch has --batch-size samples)")
+    ap.add_argument("--seq-len", type=int, default=4096, help="LM configs: tokens per sequence")
+    ap.add_argument("--checkpoint", type=int, default=0, help="activation checkpointing (transformers)")
+    ap.add_argument("--graphs", type=int, default=0, help="replay the whole DDP step as one captured HIP graph")
+    ap.add_argument("--diag-steps", type=int, default=3,
+                    help="untimed steps after the timed region with comm timers on every step")
+    ap.add_argument("--busbw-iters", type=int, default=5, help="all-reduce bandwidth probe iterations (N>1)")
+    ap.add_argument("--baseline-json", default=None, help="N=1 result line -> scaling_efficiency")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0, help="self-launch: kill children after this")
+    ap.add_argument("--json-out", default=None)
+    a = ap.parse_args(argv)
+    if a.batch_size is None:
+        a.batch_size = {"mlp": 64, "simplecnn": 32}.get(a.model, 256)
+    if a.backend is None:
+        a.backend = "rccl" if a.device == "cuda" else "cpu"
+    return a
+
+
+# ------------------------------------------------------------------------------ self-launch
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _child_preexec():
+    try:  # children die with the parent (PR_SET_PDEATHSIG = SIGTERM)
+        import ctypes
+
+        ctypes.CDLL("libc.so.6").prctl(1, signal.SIGTERM)
+    except OSError:
+        pass
+
+
+def self_launch(args, argv) -> int:
+    """Start one fresh child per rank; never touches the GPU in this (parent) process."""
+    n = args.gpus
+    port = _free_port()
+    procs = []
+    json_lines = []
+
+    def pump(stream):
+        for raw in iter(stream.readline, b""):
+            line = raw.decode(errors="replace")
+            if line.startswith('{"metric"'):
+                json_lines.append(line.strip())
+            else:
+                sys.stderr.write(line)
+                sys.stderr.flush()
+
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), XDDP_BENCH_CHILD="1")
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                             stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                             preexec_fn=_child_preexec)
+        procs.append(p)
+    t = threading.Thread(target=pump, args=(procs[0].stdout,), daemon=True)
+    t.start()
+    deadline = time.time() + args.launch_timeout
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(i, c) for i, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = bad[0]
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.time() > deadline:
+            failed = (-1, "timeout")
+            break
+        time.sleep(0.2)
+    if failed is not None:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        end = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(max(0.1, end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        print(f"[bench] rank {failed[0]} failed ({failed[1]}); all ranks stopped", file=sys.stderr, flush=True)
+    t.join(timeout=10)
+    if failed is None and json_lines:
+        print(json_lines[-1], flush=True)
+    if failed is not None:
+        return 1 if failed[1] == "timeout" else (failed[1] if isinstance(failed[1], int) and failed[1] > 0 else 1)
+    return 0 if json_lines else 1
+
+
+# ------------------------------------------------------------------------------ MIOpen tuning db
 def _install_miopen_tuning():
-    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "miopen")
+    """MIOpen conv tuning (MI355X-specific): the repo ships a find-db + perf-db + kernel cache
+    made by an exhaustive search on MI355X (tuning/miopen); each process copies it to a private
+    temp dir (MIOpen writes to it) so first steps do not pay the search."""
+    src = os.path.join(REPO, "tuning", "miopen")
     if os.environ.get("XDDP_MIOPEN_DB", "") == "none" or not os.path.isdir(src):
         return
     import shutil
@@ -43,45 +174,23 @@ def _install_miopen_tuning():
             os.environ[var] = os.path.join(dst, sub)
 
 
-_install_miopen_tuning()
-
-import torch  # noqa: E402
-import torch.nn as nn  # noqa: E402
-import torch.nn.functional as F  # noqa: E402
-
-REPO = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, REPO)
+# ------------------------------------------------------------------------------ model / data
+def is_lm(args):
+    return args.model.startswith("llama")
 
 
-def parse():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--model", default="resnet50")
-    ap.add_argument("--batch-size", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--image-size", type=int, default=224)
-    ap.add_argument("--impl", choices=["xddp", "torch"], default="xddp",
-                    help="xddp = this framework; torch = torch.nn.parallel.DDP reference stack (comparison only)")
-    ap.add_argument("--norm", choices=["xddp", "torch"], default="xddp", help="BatchNorm implementation")
-    ap.add_argument("--bucket-cap-mb", type=float, default=None)
-    ap.add_argument("--comm-dtype", default="none", help="gradient comm dtype (none = param dtype)")
-    ap.add_argument("--grad-as-bucket-view", type=int, default=1)
-    ap.add_argument("--channels-last", type=int, default=1)
-    ap.add_argument("--no-sync-accum", type=int, default=1, help="micro-batches per step (no_sync accumulation)")
-    ap.add_argument("--seq-len", type=int, default=4096, help="LM configs: tokens per sequence")
-    ap.add_argument("--checkpoint", type=int, default=0, help="activation checkpointing (transformers)")
-    ap.add_argument("--graphs", type=int, default=0, help="replay the whole DDP step as one captured HIP graph")
-    ap.add_argument("--json-out", default=None)
-    return ap.parse_args()
+def is_conv(args):
+    return args.model.startswith("resnet") or args.model == "simplecnn"
 
 
-def build_model(args, device):
+def build_model(args, device, dtype):
+    import torch
+
     from distributeddataparallel_amd import models
 
-    if args.model.startswith("resnet") or args.model == "simplecnn":
+    if is_conv(args):
         norm_layer = None
-        if args.norm == "xddp":
+        if args.norm == "xddp" and device.type == "cuda":
             from distributeddataparallel_amd.ops.batch_norm import FusedBatchNorm2d
 
             norm_layer = FusedBatchNorm2d
@@ -96,87 +205,149 @@ def build_model(args, device):
             m = models.llama3_8b(max_seq_len=args.seq_len, checkpoint_activations=bool(args.checkpoint))
     elif args.model == "llama_tiny":
         m = models.llama_tiny(max_seq_len=args.seq_len)
+    elif args.model == "mlp":  # BASELINE.json config 1 (MNIST-shaped)
+        m = models.MLP()
     else:
         raise SystemExit(f"unknown model {args.model}")
-    m = m.to(device=device, dtype=torch.bfloat16)
-    if args.channels_last and (args.model.startswith("resnet") or args.model == "simplecnn"):
+    m = m.to(device=device, dtype=dtype)
+    if args.channels_last and is_conv(args) and device.type == "cuda":
         m = m.to(memory_format=torch.channels_last)
     return m
 
 
-def is_lm(args):
-    return args.model.startswith("llama")
+def sample_shape(args):
+    if is_lm(args):
+        return (args.seq_len,)
+    if args.model == "mlp":
+        return (1, 28, 28)
+    return (3, args.image_size, args.image_size)
 
 
-def main():
-    args = parse()
+def num_classes(args, model):
+    if is_lm(args):
+        return model.cfg.vocab_size
+    return 10 if args.model in ("simplecnn", "mlp") else 1000
+
+
+def train_flops_per_sample(args):
+    """Model FLOPs of one forward+backward per sample (torch FlopCounterMode on the meta device;
+    plain torch ops, so the count is independent of which kernels run)."""
+    import torch
+    from torch.utils.flop_counter import FlopCounterMode
+
+    from distributeddataparallel_amd import models
+
+    try:
+        with torch.device("meta"):
+            if is_conv(args):
+                m = models.SimpleCNN() if args.model == "simplecnn" else getattr(models, args.model)()
+                x = torch.empty(1, *sample_shape(args))
+            elif args.model.startswith("vit"):
+                m = getattr(models, args.model)()
+                x = torch.empty(1, *sample_shape(args))
+            elif args.model == "llama3_8b":
+                m = models.llama3_8b(max_seq_len=args.seq_len)
+                x = torch.zeros(1, args.seq_len, dtype=torch.long)
+            elif args.model == "llama_tiny":
+                m = models.llama_tiny(max_seq_len=args.seq_len)
+                x = torch.zeros(1, args.seq_len, dtype=torch.long)
+            else:
+                m = models.MLP()
+                x = torch.empty(1, *sample_shape(args))
+        with FlopCounterMode(display=False) as fc:
+            m(x).float().sum().backward()
+        return float(fc.get_total_flops())
+    except Exception as e:  # noqa: BLE001 — MFU is a diagnostic, never fail the bench over it
+        print(f"[bench] flop count failed: {e}", file=sys.stderr)
+        return None
+
+
+# ------------------------------------------------------------------------------ main
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched via torch.distributed.run (one rank per GPU)")
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("RANK", str(rank))
     os.environ.setdefault("WORLD_SIZE", str(world))
     os.environ.setdefault("LOCAL_RANK", str(local_rank))
     if "MASTER_PORT" not in os.environ:
-        from distributeddataparallel_amd.utils.spawn import free_port
+        os.environ["MASTER_PORT"] = str(_free_port())
+    if args.device == "cuda":
+        _install_miopen_tuning()
+    sys.path.insert(0, REPO)
 
-        os.environ["MASTER_PORT"] = str(free_port())
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
-    torch.backends.cudnn.benchmark = bool(int(os.environ.get("XDDP_CUDNN_BENCHMARK", "0")))
+    import torch
+    import torch.nn.functional as F
 
+    gpu = args.device == "cuda"
+    if gpu:
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+        torch.backends.cudnn.benchmark = bool(int(os.environ.get("XDDP_CUDNN_BENCHMARK", "0")))
+    else:
+        device = torch.device("cpu")
+    dtype = torch.bfloat16 if gpu else torch.float32
+
+    def sync():
+        if gpu:
+            torch.cuda.synchronize()
+
+    rccl_env = {}
     if args.impl == "xddp":
         import distributeddataparallel_amd as xddp
         from distributeddataparallel_amd import distributed as dist
-        from distributeddataparallel_amd.optim import FusedSGD
+        from distributeddataparallel_amd.optim import FusedAdamW, FusedSGD
+        from distributeddataparallel_amd.parallel.bucket_policy import rccl_env_defaults
 
-        dist.init_process_group("rccl", device_id=local_rank)
+        rccl_env = rccl_env_defaults(world, args.backend)
+        dist.init_process_group(args.backend, device_id=local_rank if gpu else None)
     else:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=device)
+        dist.init_process_group("nccl" if gpu else "gloo", device_id=device if gpu else None)
 
     torch.manual_seed(0)
-    model = build_model(args, device)
+    model = build_model(args, device, dtype)
+    conv = is_conv(args)
     if args.impl == "xddp":
         comm_dtype = None if args.comm_dtype == "none" else getattr(torch, args.comm_dtype)
-        ddp = xddp.DDP(model, device_ids=[local_rank], bucket_cap_mb=args.bucket_cap_mb,
-                       gradient_as_bucket_view=bool(args.grad_as_bucket_view), comm_dtype=comm_dtype)
-        if args.model.startswith("resnet") or args.model == "simplecnn":
-            opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, master_weights=True)
+        ddp = xddp.DDP(model, device_ids=[local_rank] if gpu else None, bucket_cap_mb=args.bucket_cap_mb,
+                       bucket_policy=args.bucket_policy, gradient_as_bucket_view=bool(args.grad_as_bucket_view),
+                       comm_dtype=comm_dtype)
+        if conv or args.model == "mlp":
+            opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, master_weights=gpu)
         else:
-            from distributeddataparallel_amd.optim import FusedAdamW
-
             opt = FusedAdamW(ddp.parameters(), lr=1e-4, weight_decay=0.1, master_weights=True)
-        zero_kw = dict(set_to_none=True)
     else:
         ddp = torch.nn.parallel.DistributedDataParallel(
-            model, device_ids=[local_rank], bucket_cap_mb=args.bucket_cap_mb or 25,
+            model, device_ids=[local_rank] if gpu else None, bucket_cap_mb=args.bucket_cap_mb or 25,
             gradient_as_bucket_view=bool(args.grad_as_bucket_view))
         opt = torch.optim.SGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
-        zero_kw = dict(set_to_none=True)
 
-    B, S = args.batch_size, args.image_size
+    B = args.batch_size
+    micro = max(1, args.no_sync_accum)
     g = torch.Generator(device=device).manual_seed(1234 + rank)
+    ncls = num_classes(args, model)
     if is_lm(args):
-        vocab = model.cfg.vocab_size
-        x = torch.randint(0, vocab, (B, args.seq_len), device=device, generator=g)
-        y = torch.randint(0, vocab, (B, args.seq_len), device=device, generator=g)
+        xs = [torch.randint(0, ncls, (B, args.seq_len), device=device, generator=g) for _ in range(micro)]
+        ys = [torch.randint(0, ncls, (B, args.seq_len), device=device, generator=g) for _ in range(micro)]
     else:
-        conv = args.model.startswith("resnet") or args.model == "simplecnn"
-        mf = torch.channels_last if (args.channels_last and conv) else torch.contiguous_format
-        x = torch.randn(B, 3, S, S, device=device, generator=g).to(torch.bfloat16).contiguous(memory_format=mf)
-        y = torch.randint(0, 10 if args.model == "simplecnn" else 1000, (B,), device=device, generator=g)
+        mf = torch.channels_last if (args.channels_last and conv and gpu) else torch.contiguous_format
+        xs = [torch.randn(B, *sample_shape(args), device=device, generator=g).to(dtype).contiguous(memory_format=mf)
+              for _ in range(micro)]
+        ys = [torch.randint(0, ncls, (B,), device=device, generator=g) for _ in range(micro)]
 
     def loss_fn(out, tgt):
         if is_lm(args):
             return F.cross_entropy(out.float().view(-1, out.shape[-1]), tgt.view(-1))
         return F.cross_entropy(out.float(), tgt)
-    micro = max(1, args.no_sync_accum)
-    xs, ys = x.chunk(micro), y.chunk(micro)
 
     graphed = None
     if args.graphs:
@@ -184,19 +355,17 @@ def main():
             raise SystemExit("--graphs does not combine with --no-sync-accum")
         from distributeddataparallel_amd.utils.graphs import GraphedTrainStep
 
-        graphed = GraphedTrainStep(ddp, opt, loss_fn, x, y, warmup_steps=3)
+        graphed = GraphedTrainStep(ddp, opt, loss_fn, xs[0], ys[0], warmup_steps=3)
 
     def step():
         if graphed is not None:
-            return graphed(x, y)
-        opt.zero_grad(**zero_kw)
-        for i in range(micro):
-            if i < micro - 1:
-                with ddp.no_sync():
-                    loss_fn(ddp(xs[i]), ys[i]).backward()
-            else:
-                loss = loss_fn(ddp(xs[i]), ys[i])
-                loss.backward()
+            return graphed(xs[0], ys[0])
+        opt.zero_grad(set_to_none=True)
+        for i in range(micro - 1):
+            with ddp.no_sync():
+                loss_fn(ddp(xs[i]), ys[i]).backward()
+        loss = loss_fn(ddp(xs[-1]), ys[-1])
+        loss.backward()
         opt.step()
         return loss
 
@@ -204,36 +373,49 @@ def main():
         tw = time.perf_counter()
         loss = step()
         if rank == 0:
-            torch.cuda.synchronize()
+            sync()
             print(f"[bench] warmup step {i + 1}/{args.warmup}: {time.perf_counter() - tw:.2f}s", file=sys.stderr,
                   flush=True)
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     et = torch.tensor([elapsed], device=device, dtype=torch.float64)
-    if args.impl == "xddp":
-        dist.all_reduce(et, op=dist.ReduceOp.MAX)
-    else:
-        dist.all_reduce(et, op=dist.ReduceOp.MAX)
+    dist.all_reduce(et, op=dist.ReduceOp.MAX)
     elapsed = float(et.item())
     final_loss = float(loss.float().item())
+
+    # ---------------- diagnostics (outside the timed region)
+    diag = {}
+    if args.impl == "xddp":
+        diag = diagnostics(args, ddp, step, sync, dist, device, world)
+
     ms = elapsed / args.steps * 1e3
-    units = B * world * args.steps * (args.seq_len if is_lm(args) else 1)
+    per_step_samples = B * micro * world
+    units = per_step_samples * args.steps * (args.seq_len if is_lm(args) else 1)
     value = units / elapsed
     if rank == 0:
+        flops = train_flops_per_sample(args)
         if args.model == "resnet50":
             metric = "images/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X; scaling efficiency"
         elif is_lm(args):
             metric = f"tokens/sec (whole node) {args.model} pure DDP"
         else:
             metric = f"images/sec (whole node) {args.model} DDP"
+        eff = None
+        if args.baseline_json:
+            try:
+                with open(args.baseline_json) as f:
+                    base = json.loads(f.read().strip().splitlines()[-1])
+                eff = round(value / (world * float(base["value"])), 4)
+            except (OSError, ValueError, KeyError) as e:
+                print(f"[bench] cannot read baseline {args.baseline_json}: {e}", file=sys.stderr)
         out = {
             "metric": metric,
             "value": round(value, 2),
@@ -245,36 +427,104 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
             "data": ("synthetic (random token ids; random-init weights)" if is_lm(args) else
-                     f"synthetic (random 3x{S}x{S} bf16 inputs, random labels; random-init weights)"),
+                     f"synthetic (random {'x'.join(map(str, sample_shape(args)))} inputs, random labels; "
+                     "random-init weights)"),
             "config": {
                 "model": args.model,
-                "global_batch": B * world,
-                "per_gpu_batch": B,
+                "global_batch": per_step_samples,
+                "per_gpu_batch": B * micro,
+                "micro_batch": B,
                 "seq_len": args.seq_len if is_lm(args) else None,
-                "image_size": S,
+                "image_size": args.image_size if (conv or args.model.startswith("vit")) else None,
                 "parallelism": f"dp{world}",
                 "impl": args.impl,
+                "backend": args.backend if args.impl == "xddp" else ("nccl" if gpu else "gloo"),
                 "norm": args.norm,
-                "optimizer": ("SGD(momentum=0.9, wd=1e-4) fp32 master weights"
-                              if args.model.startswith("resnet") or args.model == "simplecnn"
-                              else "AdamW(wd=0.1) fp32 master weights"),
+                "optimizer": ("SGD(momentum=0.9, wd=1e-4)" + (" fp32 master weights" if gpu else "")
+                              if (conv or args.model == "mlp") else "AdamW(wd=0.1) fp32 master weights"),
                 "channels_last": bool(args.channels_last),
                 "comm_dtype": args.comm_dtype,
                 "gradient_as_bucket_view": bool(args.grad_as_bucket_view),
                 "micro_batches": micro,
                 "hip_graphs": bool(args.graphs),
+                "rccl_env_defaults": rccl_env,
             },
             "final_loss": round(final_loss, 4),
+            "scaling_efficiency": eff,
         }
+        if flops:
+            tf = flops * per_step_samples / (ms * 1e-3) / 1e12
+            out["model_tflops_per_gpu"] = round(tf / world, 1)
+            out["mfu"] = round(tf / world / BF16_DENSE_PEAK_TFLOPS, 4) if gpu else None
+        out.update(diag)
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     dist.destroy_process_group()
+    return 0
+
+
+def diagnostics(args, ddp, step, sync, dist, device, world):
+    """Comm observability: communicator rank count, rebuilt buckets, sampled
+    backward comm / overlap (Reducer hipEvent timers on every diagnostic step), and the
+    achieved all-reduce bus bandwidth of each bucket size when N>1."""
+    import torch
+
+    red = ddp.reducer
+    pg = ddp.process_group
+    out = {"nranks": int(pg.comm.size()), "comm_backend": pg.backend}
+    sizes = list(red.bucket_sizes_bytes())
+    out["buckets"] = {"count": len(sizes), "bytes": sizes, **ddp.bucket_plan.as_dict()}
+    if args.graphs:
+        return out
+    red.reset_runtime_stats()
+    ddp._set_ddp_runtime_logging_sample_rate(1)
+    for _ in range(max(2, args.diag_steps) + 1):  # the last step harvests the previous one's timers
+        step()
+        sync()  # timers are harvested at the next forward only once their events completed
+    d = ddp._get_ddp_logging_data()
+    comm = d.get("avg_backward_comm_time", 0) / 1e6
+    ov = d.get("avg_backward_compute_comm_overlap_time", 0) / 1e6
+    out["comm"] = {
+        "avg_backward_compute_ms": round(d.get("avg_backward_compute_time", 0) / 1e6, 3),
+        "avg_backward_comm_ms": round(comm, 3),
+        "avg_overlap_ms": round(ov, 3),
+        "exposed_comm_ms": round(max(0.0, comm - ov), 3),
+        "overlap_pct": round(100.0 * ov / comm, 1) if comm > 0 else None,
+        "timed_iterations": int(d.get("num_timed_iterations", 0)),
+        "grouped_launches": int(d.get("num_grouped_launches", 0)),
+    }
+    ddp._set_ddp_runtime_logging_sample_rate(100)
+    if world > 1 and args.busbw_iters > 0:
+        probes = []
+        dt = next(p for p in ddp.module.parameters()).dtype
+        if ddp._comm_dtype is not None:
+            dt = ddp._comm_dtype
+        esz = torch.empty(0, dtype=dt).element_size()
+        for nbytes in sorted(set(sizes)):
+            buf = torch.ones(max(1, nbytes // esz), dtype=dt, device=device)
+            for _ in range(2):
+                pg.allreduce(buf, dist.ReduceOp.AVG).wait()
+            sync()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.busbw_iters):
+                pg.allreduce(buf, dist.ReduceOp.AVG).wait()
+            sync()
+            t = (time.perf_counter() - t0) / args.busbw_iters
+            tt = torch.tensor([t], dtype=torch.float64, device=device)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t = float(tt.item())
+            probes.append({"bytes": nbytes, "ms": round(t * 1e3, 4),
+                           "busbw_GBps": round(2.0 * (world - 1) / world * nbytes / t / 1e9, 1)})
+            del buf
+        out["allreduce_busbw"] = probes
+    return out
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -57,6 +57,17 @@ struct PyHookResult : HookResult {
   std::shared_ptr<py::object> fut;
 };
 
+// A future whose value is not a bucket (buffer comm hooks): only waited on.
+struct PyFutureWait : HookResult {
+  explicit PyFutureWait(py::object f) : fut(hold(std::move(f))) {}
+  at::Tensor wait() override {
+    py::gil_scoped_acquire g;
+    fut->attr("wait")();
+    return at::Tensor();
+  }
+  std::shared_ptr<py::object> fut;
+};
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -220,8 +231,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(py::init([](std::vector<at::Tensor> params, std::vector<std::vector<int64_t>> bucket_indices,
                        std::vector<int64_t> limits, std::shared_ptr<Comm> comm, bool find_unused,
                        bool grad_as_view, bool static_graph, int64_t bucket_cap, int64_t first_bucket_cap,
-                       const std::string& comm_dtype, std::vector<std::string> names) {
+                       const std::string& comm_dtype, std::vector<std::string> names, bool skip_unused,
+                       int64_t tail_cap, std::vector<bool> expect_sparse) {
              ReducerOptions o;
+             o.skip_all_reduce_unused_params = skip_unused;
+             o.tail_bucket_bytes_cap = tail_cap;
+             o.expect_sparse = std::move(expect_sparse);
              o.find_unused_parameters = find_unused;
              o.gradient_as_bucket_view = grad_as_view;
              o.static_graph = static_graph;
@@ -237,7 +252,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("find_unused_parameters") = false, py::arg("gradient_as_bucket_view") = false,
            py::arg("static_graph") = false, py::arg("bucket_bytes_cap") = 25 * 1024 * 1024,
            py::arg("first_bucket_bytes_cap") = 1024 * 1024, py::arg("comm_dtype") = "",
-           py::arg("param_names") = std::vector<std::string>{})
+           py::arg("param_names") = std::vector<std::string>{}, py::arg("skip_all_reduce_unused_params") = false,
+           py::arg("tail_bucket_bytes_cap") = 0, py::arg("expect_sparse") = std::vector<bool>{})
       .def("prepare_for_forward", &Reducer::prepare_for_forward, py::call_guard<py::gil_scoped_release>())
       .def("prepare_for_backward", &Reducer::prepare_for_backward, py::call_guard<py::gil_scoped_release>())
       .def("rebuild_buckets", &Reducer::rebuild_buckets, py::call_guard<py::gil_scoped_release>())
@@ -258,6 +274,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_comm", &Reducer::set_comm)
       .def("set_runtime_logging_sample_rate", &Reducer::set_runtime_logging_sample_rate)
       .def("zeros_like_buckets", &Reducer::zeros_like_buckets)
+      .def("shadow_allreduce_buckets", &Reducer::shadow_allreduce_buckets, py::arg("premul_sum") = false,
+           py::call_guard<py::gil_scoped_release>())
+      .def("push_all_rebuilt_params", &Reducer::push_all_rebuilt_params)
+      .def("install_post_backward_futures", [](Reducer& r, py::list futs) {
+            std::vector<std::shared_ptr<HookResult>> v;
+            for (auto f : futs) v.push_back(std::make_shared<PyFutureWait>(py::reinterpret_borrow<py::object>(f)));
+            r.install_post_backward_futures(std::move(v));
+          }, "Futures (e.g. from a buffer comm hook) awaited at the end of the next backward")
+      .def("reset_runtime_stats", &Reducer::reset_runtime_stats)
       .def("local_used_map", &Reducer::local_used_map)
       .def("bucket_indices", &Reducer::bucket_indices)
       .def("bucket_sizes_bytes", &Reducer::bucket_sizes_bytes)

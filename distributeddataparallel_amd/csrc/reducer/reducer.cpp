@@ -53,7 +53,12 @@ std::pair<std::vector<std::vector<int64_t>>, std::vector<int64_t>> compute_bucke
     const std::vector<at::Tensor>& tensors, const std::vector<int64_t>& limits,
     const std::vector<bool>& expect_sparse, const std::vector<int64_t>& tensor_indices) {
   TORCH_CHECK(!limits.empty(), "bucket size limits must not be empty");
-  TORCH_CHECK(expect_sparse.empty() || expect_sparse.size() == tensors.size(), "expect_sparse length mismatch");
+  // expect_sparse is indexed by tensor index (tensor_indices[i] when given, else i)
+  TORCH_CHECK(expect_sparse.empty() || !tensor_indices.empty() || expect_sparse.size() == tensors.size(),
+              "expect_sparse length mismatch");
+  for (auto ti : tensor_indices)
+    TORCH_CHECK(expect_sparse.empty() || (ti >= 0 && ti < (int64_t)expect_sparse.size()),
+                "expect_sparse does not cover tensor index ", ti);
   TORCH_CHECK(tensor_indices.empty() || tensor_indices.size() == tensors.size(), "tensor_indices length mismatch");
   struct Acc {
     std::vector<int64_t> idx;
@@ -123,14 +128,17 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t
     TORCH_CHECK(p.requires_grad(), "xddp Reducer: every parameter must require grad");
     TORCH_CHECK(p.device() == device_, "xddp Reducer: all parameters must live on one device (got ", p.device(),
                 " and ", device_, ")");
-    TORCH_CHECK(!p.is_sparse(), "xddp Reducer: sparse parameters are not supported");
+    TORCH_CHECK(!p.is_sparse(), "xddp Reducer: sparse parameters are not supported (sparse GRADIENTS are: "
+                                "pass expect_sparse)");
   }
+  if (opts_.expect_sparse.size() != params_.size()) opts_.expect_sparse.assign(params_.size(), false);
   if (names_.size() != params_.size()) {
     names_.clear();
     for (size_t i = 0; i < params_.size(); ++i) names_.push_back("param_" + std::to_string(i));
   }
   const size_t n = params_.size();
   ready_.assign(n, 0);
+  unused_mask_.assign(n, 0);
   local_used_ = at::zeros({static_cast<int64_t>(n)}, at::kInt);
   hook_count_.assign(n, 0);
   if (per_bucket_size_limits.size() != bucket_indices.size())
@@ -162,7 +170,6 @@ void Reducer::install_hooks() {
           if (auto r = weak.lock()) r->autograd_hook(idx);
           return outputs;
         }));
-    acc_to_index_[acc.get()] = idx;
     grad_accs_.push_back(std::move(acc));
     hook_keys_.push_back(key);
   }
@@ -174,7 +181,6 @@ void Reducer::remove_autograd_hooks() {
   for (size_t i = 0; i < grad_accs_.size(); ++i) grad_accs_[i]->del_post_hook(hook_keys_[i]);
   grad_accs_.clear();
   hook_keys_.clear();
-  acc_to_index_.clear();
   hooks_installed_ = false;
 }
 
@@ -189,6 +195,22 @@ void Reducer::initialize_buckets(const std::vector<std::vector<int64_t>>& indice
     Bucket bk;
     bk.vars = indices[b];
     TORCH_CHECK(!bk.vars.empty(), "xddp Reducer: empty bucket");
+    bool any_sparse = false;
+    for (auto v : bk.vars) any_sparse = any_sparse || (v >= 0 && v < (int64_t)n && opts_.expect_sparse[v]);
+    if (any_sparse) {
+      TORCH_CHECK(bk.vars.size() == 1, "xddp Reducer: a sparse-gradient parameter needs a bucket of its own");
+      const int64_t v = bk.vars[0];
+      TORCH_CHECK(!seen[v], "xddp Reducer: param ", v, " assigned to two buckets");
+      seen[v] = 1;
+      bk.sparse = true;
+      bk.offsets = {0};
+      bk.lengths = {params_[v].numel()};
+      bk.pending = 1;
+      bk.size_limit = b < limits.size() ? limits[b] : opts_.bucket_bytes_cap;
+      var_loc_[v] = {static_cast<int64_t>(b), 0};
+      buckets_.push_back(std::move(bk));
+      continue;
+    }
     const auto dt = params_[bk.vars[0]].scalar_type();
     int64_t off = 0;
     for (size_t s = 0; s < bk.vars.size(); ++s) {
@@ -221,6 +243,7 @@ void Reducer::initialize_buckets(const std::vector<std::vector<int64_t>>& indice
   if (opts_.gradient_as_bucket_view) {
     // existing grads move into the bucket so accumulation happens in place from now on
     for (size_t i = 0; i < n; ++i) {
+      if (buckets_[var_loc_[i].first].sparse) continue;
       auto& g = params_[i].mutable_grad();
       const auto& view = buckets_[var_loc_[i].first].views[var_loc_[i].second];
       if (g.defined() && !g.is_alias_of(view)) {
@@ -336,7 +359,6 @@ void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs) {
       if (!ready_[i]) { os << " " << names_[i]; shown++; }
     TORCH_CHECK(false, os.str());
   }
-  num_backward_calls_++;
   timer_record(1);
   expect_hooks_ = true;
   require_finalize_ = true;
@@ -351,9 +373,11 @@ void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs) {
     bk.hook_result.reset();
     bk.grad_bucket.reset();
     bk.launched = false;
+    bk.skipped = false;
   }
   if (!has_rebuilt_) ready_order_.clear();
   local_used_.zero_();
+  for (auto u : unused_) unused_mask_[u] = 0;
   unused_.clear();
   const bool static_first = opts_.static_graph && !static_first_iter_done_;
   if (opts_.find_unused_parameters && !static_first && !opts_.static_graph) search_unused_parameters(outputs);
@@ -361,6 +385,7 @@ void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs) {
     for (size_t i = 0; i < params_.size(); ++i)
       if (hook_count_expected_[i] == 0) unused_.push_back(static_cast<int64_t>(i));
   }
+  for (auto u : unused_) unused_mask_[u] = 1;
 }
 
 void Reducer::search_unused_parameters(const std::vector<at::Tensor>& outputs) {
@@ -436,8 +461,25 @@ void Reducer::mark_variable_ready(int64_t index) {
 
 void Reducer::mark_bucket_ready(int64_t b) {
   if (b != next_bucket_) return;  // launch strictly in bucket order (cross-rank determinism)
-  while (next_bucket_ < static_cast<int64_t>(buckets_.size()) && buckets_[next_bucket_].pending == 0)
-    launch_bucket(next_bucket_++);
+  const int64_t nb = static_cast<int64_t>(buckets_.size());
+  int64_t burst = 0;
+  while (next_bucket_ + burst < nb && buckets_[next_bucket_ + burst].pending == 0) burst++;
+  // Several buckets ready at once (the tail of backward, iteration 0, static-graph first
+  // iteration): one RCCL group, so RCCL schedules the burst as one launch over the links.
+  // Not with a Python comm hook (it may block or run non-RCCL work) or a PREMUL_SUM op (its
+  // custom reduction op is created and destroyed per call).
+  const bool group = burst > 1 && !hook_ && divide_factor_ <= 0.0;
+  if (group) comm_->group_start();
+  try {
+    for (int64_t k = 0; k < burst; ++k) launch_bucket(next_bucket_++);
+  } catch (...) {
+    if (group) comm_->group_end();
+    throw;
+  }
+  if (group) {
+    comm_->group_end();
+    grouped_launches_++;
+  }
   if (next_bucket_ == static_cast<int64_t>(buckets_.size()) && !finalize_queued_) {
     timer_record(2);
     finalize_queued_ = true;
@@ -452,6 +494,20 @@ void Reducer::launch_bucket(int64_t b) {
   RECORD_FUNCTION("xddp::reducer::launch_bucket", std::vector<c10::IValue>());
   Range range("xddp::reducer::launch_bucket");
   auto& bk = buckets_[b];
+  if (b == 0) timer_record(3);
+  if (bk.sparse) {  // reduced at finalize (needs the peers' nnz first)
+    bk.launched = true;
+    return;
+  }
+  if (opts_.skip_all_reduce_unused_params && opts_.find_unused_parameters) {
+    bool all_unused = true;
+    for (auto v : bk.vars) all_unused = all_unused && unused_mask_[v];
+    if (all_unused) {
+      bk.skipped = true;
+      bk.launched = true;
+      return;
+    }
+  }
   const bool cast = !bk.comm.is_same(bk.flat);
   // In view mode grads live in `flat`; otherwise (cast) we pack straight into the comm buffer.
   const bool pack_to_comm = cast && !opts_.gradient_as_bucket_view;
@@ -464,7 +520,8 @@ void Reducer::launch_bucket(int64_t b) {
       zero.push_back(view);
       continue;
     }
-    TORCH_CHECK(!g.is_sparse(), "xddp Reducer: sparse gradients are not supported");
+    TORCH_CHECK(!g.is_sparse(), "xddp Reducer: parameter ", names_[bk.vars[s]],
+                " produced a sparse gradient but was not declared sparse (expect_sparse)");
     if (!pack_to_comm && g.is_alias_of(bk.views[s])) continue;  // already accumulated in place
     if (same_layout(g, view) && g.scalar_type() == p.scalar_type()) {
       src.push_back(g);
@@ -498,7 +555,6 @@ void Reducer::launch_bucket(int64_t b) {
       bk.comm.copy_(bk.flat);
     }
   }
-  if (b == 0) timer_record(3);
   if (hook_) {
     auto gb = std::make_shared<GradBucket>();
     gb->index = b;
@@ -549,6 +605,7 @@ void Reducer::finalize_backward() {
   const bool use_map = opts_.find_unused_parameters || static_first;
   if (use_map) all_reduce_local_used_map();
   for (auto& bk : buckets_) {
+    if (bk.sparse || bk.skipped) continue;
     at::Tensor result;
     if (bk.hook_result) {
       result = bk.hook_result->wait();
@@ -561,8 +618,17 @@ void Reducer::finalize_backward() {
     }
     if (result.defined() && !result.is_same(bk.comm)) bk.comm.view(-1).copy_(result.reshape(-1));
   }
+  // sparse gradients: all-gather (indices, values), sum, scale (same divide rule as dense)
+  for (auto& bk : buckets_) {
+    if (!bk.sparse) continue;
+    const int64_t v = bk.vars[0];
+    if (use_map && local_used_.data_ptr<int>()[v] == 0) continue;
+    auto& gr = params_[v].mutable_grad();
+    gr = sparse_allreduce(gr.defined() ? gr : at::zeros_like(params_[v]).to_sparse());
+  }
   // copy-out
   for (auto& bk : buckets_) {
+    if (bk.sparse || bk.skipped) continue;
     const bool cast = !bk.comm.is_same(bk.flat);
     if (cast && opts_.gradient_as_bucket_view) {
       if (on_gpu()) {
@@ -603,6 +669,8 @@ void Reducer::finalize_backward() {
       }
     }
   }
+  for (auto& f : post_bwd_futs_) f->wait();
+  post_bwd_futs_.clear();
   timer_record(4);
   if (timing_this_iter_) timing_pending_ = true;
   timing_this_iter_ = false;
@@ -610,13 +678,118 @@ void Reducer::finalize_backward() {
   expect_hooks_ = false;
   require_finalize_ = false;
   finalize_queued_ = false;
+  divide_factor_ = 0.0;  // a join-time divide factor applies to one backward only
+}
+
+at::Tensor Reducer::sparse_allreduce(const at::Tensor& grad) {
+  RECORD_FUNCTION("xddp::reducer::sparse_allreduce", std::vector<c10::IValue>());
+  const int W = comm_->size();
+  const double scale = 1.0 / (divide_factor_ > 0.0 ? divide_factor_ : static_cast<double>(W));
+  auto g = grad.coalesce();
+  if (W == 1) return g.mul(scale);
+  auto idx = g._indices().contiguous();
+  auto val = g._values().contiguous();
+  const auto dev = val.device();
+  auto lopt = at::TensorOptions().dtype(at::kLong).device(dev);
+  auto nnz_all = at::zeros({W}, lopt);
+  comm_->allgather(nnz_all, at::full({1}, g._nnz(), lopt))->wait();
+  auto nnz_host = nnz_all.cpu();
+  const int64_t* nn = nnz_host.data_ptr<int64_t>();
+  int64_t maxn = 0;
+  for (int r = 0; r < W; ++r) maxn = std::max(maxn, nn[r]);
+  if (maxn == 0) return g.mul(scale);
+  const int64_t sd = idx.size(0);
+  auto dense_shape = val.sizes().vec();
+  dense_shape[0] = maxn;
+  auto idx_pad = at::zeros({sd, maxn}, idx.options());
+  auto val_pad = at::zeros(dense_shape, val.options());
+  idx_pad.narrow(1, 0, idx.size(1)).copy_(idx);
+  val_pad.narrow(0, 0, val.size(0)).copy_(val);
+  auto idx_all = at::empty({W * sd * maxn}, idx.options());
+  auto val_all = at::empty({W * val_pad.numel()}, val.options());
+  comm_->allgather(idx_all, idx_pad.reshape(-1))->wait();
+  comm_->allgather(val_all, val_pad.reshape(-1))->wait();
+  std::vector<at::Tensor> is, vs;
+  auto idx3 = idx_all.view({W, sd, maxn});
+  auto vshape = dense_shape;
+  vshape.insert(vshape.begin(), W);
+  auto val3 = val_all.view(vshape);
+  for (int r = 0; r < W; ++r) {
+    if (nn[r] == 0) continue;
+    is.push_back(idx3[r].narrow(1, 0, nn[r]));
+    vs.push_back(val3[r].narrow(0, 0, nn[r]));
+  }
+  auto out = at::sparse_coo_tensor(at::cat(is, 1), at::cat(vs, 0), g.sizes(), g.options()).coalesce();
+  return out.mul(scale);
 }
 
 // =======================================================================================
 // rebuild
 // =======================================================================================
 bool Reducer::should_rebuild_buckets() const {
-  return !has_rebuilt_ && (opts_.static_graph || !opts_.find_unused_parameters) && num_iterations_ > 0;
+  // iteration 0 never has a grad-ready order yet; rebuild_buckets() also requires one
+  return !has_rebuilt_ && (opts_.static_graph || !opts_.find_unused_parameters);
+}
+
+void Reducer::push_all_rebuilt_params() {
+  std::lock_guard<std::mutex> g(mu_);
+  if (has_rebuilt_ || !prev_ready_order_.empty()) return;
+  // no observed order: the reference's heuristic (reverse registration order ~ grad-ready order)
+  for (int64_t i = static_cast<int64_t>(params_.size()) - 1; i >= 0; --i) prev_ready_order_.push_back(i);
+}
+
+std::pair<std::vector<std::vector<int64_t>>, std::vector<int64_t>> Reducer::assign_rebuilt(
+    const std::vector<int64_t>& order) const {
+  std::vector<at::Tensor> ordered;
+  bool one_dtype = true, any_sparse = false;
+  for (auto v : order) {
+    ordered.push_back(params_[v]);
+    one_dtype = one_dtype && params_[v].scalar_type() == params_[order[0]].scalar_type();
+    any_sparse = any_sparse || opts_.expect_sparse[v];
+  }
+  const std::vector<int64_t> limits = {opts_.first_bucket_bytes_cap, opts_.bucket_bytes_cap};
+  if (opts_.tail_bucket_bytes_cap <= 0 || !one_dtype || any_sparse || order.size() < 2)
+    return compute_bucket_assignment_by_size(ordered, limits, opts_.expect_sparse, order);
+  // tail: the trailing gradients (produced last in backward) up to tail cap form the final bucket
+  size_t k = order.size();
+  int64_t tail_bytes = 0;
+  while (k > 1 && tail_bytes < opts_.tail_bucket_bytes_cap) {
+    --k;
+    tail_bytes += params_[order[k]].numel() * params_[order[k]].element_size();
+  }
+  std::vector<at::Tensor> head(ordered.begin(), ordered.begin() + k);
+  std::vector<int64_t> head_idx(order.begin(), order.begin() + k);
+  auto res = compute_bucket_assignment_by_size(head, limits, opts_.expect_sparse, head_idx);
+  res.first.emplace_back(order.begin() + k, order.end());
+  res.second.push_back(opts_.tail_bucket_bytes_cap);
+  return res;
+}
+
+void Reducer::shadow_allreduce_buckets(bool premul_sum) {
+  std::vector<at::Tensor> zs;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& bk : buckets_) {
+      TORCH_CHECK(!bk.sparse, "xddp Reducer: join() with sparse-gradient parameters is not supported");
+      zs.push_back(at::zeros_like(bk.comm));
+    }
+  }
+  std::vector<std::shared_ptr<Work>> ws;
+  if (!premul_sum && zs.size() > 1) comm_->group_start();
+  for (auto& z : zs) ws.push_back(comm_->allreduce(z, premul_sum ? RedOp::PREMUL_SUM : RedOp::AVG, 1.0));
+  if (!premul_sum && zs.size() > 1) comm_->group_end();
+  for (auto& w : ws) w->synchronize();
+}
+
+void Reducer::install_post_backward_futures(std::vector<std::shared_ptr<HookResult>> futs) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& f : futs) post_bwd_futs_.push_back(std::move(f));
+}
+
+void Reducer::reset_runtime_stats() {
+  std::lock_guard<std::mutex> g(mu_);
+  sum_fwd_ = sum_bwd_ = sum_comm_ = sum_overlap_ = 0;
+  n_timed_ = 0;
 }
 
 std::vector<std::vector<int64_t>> Reducer::sync_bucket_indices(std::vector<std::vector<int64_t>> indices,
@@ -660,10 +833,7 @@ bool Reducer::rebuild_buckets() {
     for (size_t i = 0; i < params_.size(); ++i)
       if (!in[i]) prev_ready_order_.push_back(static_cast<int64_t>(i));
   }
-  std::vector<at::Tensor> ordered;
-  for (auto v : prev_ready_order_) ordered.push_back(params_[v]);
-  auto res = compute_bucket_assignment_by_size(ordered, {opts_.first_bucket_bytes_cap, opts_.bucket_bytes_cap}, {},
-                                               prev_ready_order_);
+  auto res = assign_rebuilt(prev_ready_order_);
   auto limits = res.second;
   auto idx = sync_bucket_indices(res.first, limits);
   initialize_buckets(idx, limits);
@@ -675,7 +845,8 @@ bool Reducer::rebuild_buckets() {
 // =======================================================================================
 std::vector<at::Tensor> Reducer::zeros_like_buckets() const {
   std::vector<at::Tensor> out;
-  for (auto& bk : buckets_) out.push_back(at::zeros_like(bk.comm));
+  for (auto& bk : buckets_)
+    if (!bk.sparse) out.push_back(at::zeros_like(bk.comm));
   return out;
 }
 
@@ -705,6 +876,7 @@ std::map<std::string, double> Reducer::runtime_stats() const {
   m["num_timed_iterations"] = static_cast<double>(n_timed_);
   m["iteration"] = static_cast<double>(num_iterations_);
   m["num_native_launches"] = static_cast<double>(native_launches_);
+  m["num_grouped_launches"] = static_cast<double>(grouped_launches_);
   return m;
 }
 
@@ -723,6 +895,9 @@ std::map<std::string, std::string> Reducer::construction_data() const {
   m["gradient_as_bucket_view"] = opts_.gradient_as_bucket_view ? "1" : "0";
   m["static_graph"] = opts_.static_graph ? "1" : "0";
   m["bucket_cap_bytes"] = std::to_string(opts_.bucket_bytes_cap);
+  m["first_bucket_cap_bytes"] = std::to_string(opts_.first_bucket_bytes_cap);
+  m["tail_bucket_cap_bytes"] = std::to_string(opts_.tail_bucket_bytes_cap);
+  m["skip_all_reduce_unused_params"] = opts_.skip_all_reduce_unused_params ? "1" : "0";
   m["comm_dtype"] = opts_.comm_dtype == at::ScalarType::Undefined ? "" : c10::toString(opts_.comm_dtype);
   m["has_rebuilt_buckets"] = has_rebuilt_ ? "1" : "0";
   if (has_rebuilt_) {

@@ -61,7 +61,16 @@ struct ReducerOptions {
   int64_t first_bucket_bytes_cap = 1024 * 1024;
   // Dtype gradients are communicated in (kUndefined = same as the param).
   at::ScalarType comm_dtype = at::ScalarType::Undefined;
+  // With find_unused_parameters: a bucket whose parameters were all unused this iteration is
+  // not all-reduced (caller guarantees the unused set is identical on every rank).
   bool skip_all_reduce_unused_params = false;
+  // xGMI tail policy (0 = off): after the rebuild, the LAST-launched bucket holds only the
+  // trailing gradients up to this many bytes, so the all-reduce left exposed after backward
+  // (the one that cannot overlap anything) is short. See parallel/bucket_policy.py.
+  int64_t tail_bucket_bytes_cap = 0;
+  // Per-parameter: gradient is sparse (nn.Embedding(sparse=True)). Such a parameter gets a
+  // bucket of its own and is reduced by an all-gather of (indices, values) at finalize.
+  std::vector<bool> expect_sparse;
 };
 
 class Reducer : public std::enable_shared_from_this<Reducer> {
@@ -84,12 +93,22 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   bool has_comm_hook() const { return static_cast<bool>(hook_); }
   void set_comm_dtype(at::ScalarType t);
   void set_static_graph();
+  // Join(divide_by_initial_world_size=False): divide by the number of ranks still training,
+  // for the NEXT backward only (reset at every finalize, like the reference's div_factor_).
   void set_gradient_divide_factor(double f) { divide_factor_ = f; }
   void set_comm(std::shared_ptr<Comm> c) { comm_ = std::move(c); }
   void set_runtime_logging_sample_rate(int64_t r) { sample_rate_ = std::max<int64_t>(1, r); }
 
   // Join support: zero buffers shaped like each bucket, used to shadow all-reduces.
   std::vector<at::Tensor> zeros_like_buckets() const;
+  // Join support: all-reduce a zero buffer per bucket with the SAME op the training ranks use
+  // (AVG, or PREMUL_SUM when `premul_sum`), one RCCL group; returns when the device is done.
+  void shadow_allreduce_buckets(bool premul_sum);
+  // Join support (reference `_push_all_rebuilt_params`): a rank that joined before finishing an
+  // iteration has no grad-ready order; seed it so it still takes part in the rebuild broadcast.
+  void push_all_rebuilt_params();
+  void reset_runtime_stats();
+  void install_post_backward_futures(std::vector<std::shared_ptr<HookResult>> futs);
   at::Tensor local_used_map() const { return local_used_.clone(); }
   std::vector<std::vector<int64_t>> bucket_indices() const;
   std::vector<int64_t> bucket_sizes_bytes() const;
@@ -121,6 +140,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     std::shared_ptr<HookResult> hook_result;
     std::shared_ptr<GradBucket> grad_bucket;
     bool launched = false;
+    bool sparse = false;                  // one sparse-gradient parameter, reduced at finalize
+    bool skipped = false;                 // skip_all_reduce_unused_params: not reduced this iter
   };
 
   void initialize_buckets(const std::vector<std::vector<int64_t>>& indices, const std::vector<int64_t>& limits);
@@ -131,6 +152,9 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   void finalize_backward();
   void search_unused_parameters(const std::vector<at::Tensor>& outputs);
   void all_reduce_local_used_map();
+  at::Tensor sparse_allreduce(const at::Tensor& grad);
+  std::pair<std::vector<std::vector<int64_t>>, std::vector<int64_t>> assign_rebuilt(
+      const std::vector<int64_t>& order) const;
   std::vector<std::vector<int64_t>> sync_bucket_indices(std::vector<std::vector<int64_t>> indices,
                                                        std::vector<int64_t>& limits);
   hipStream_t current_stream() const;
@@ -144,7 +168,6 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   at::Device device_;
   std::vector<std::shared_ptr<torch::autograd::Node>> grad_accs_;
   std::vector<uintptr_t> hook_keys_;
-  std::unordered_map<torch::autograd::Node*, int64_t> acc_to_index_;
   bool hooks_installed_ = false;
 
   std::vector<Bucket> buckets_;
@@ -157,9 +180,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   bool has_marked_unused_ = false;
   std::vector<char> ready_;
   std::vector<int64_t> unused_;  // locally unused this iteration
+  std::vector<char> unused_mask_;
   at::Tensor local_used_;        // int32 CPU bitmap
-  at::Tensor local_used_dev_;
   CommHookFn hook_;
+  std::vector<std::shared_ptr<HookResult>> post_bwd_futs_;
   double divide_factor_ = 0.0;   // 0 => world size (AVG)
 
   // rebuild
@@ -174,8 +198,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<int64_t> hook_count_;
 
   int64_t num_iterations_ = 0;
-  int64_t num_backward_calls_ = 0;
   int64_t native_launches_ = 0;
+  int64_t grouped_launches_ = 0;
   mutable std::mutex mu_;
 
   // timers: slots 0 fwd start, 1 bwd compute start, 2 bwd compute end, 3 comm start, 4 comm end

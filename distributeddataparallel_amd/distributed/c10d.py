@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import time
 import sys
 from datetime import timedelta
 from typing import List, Optional, Sequence
@@ -94,6 +95,18 @@ class Work:
         self._done_post = False
 
     def wait(self, timeout=None):
+        """GPU: order the caller's stream after the collective (no host block). CPU: block.
+        With ``timeout`` (seconds or timedelta) raise RuntimeError if the collective has not
+        completed by then; the collective itself keeps running (it can be waited on again)."""
+        if self._w is not None and timeout is not None:
+            secs = timeout.total_seconds() if hasattr(timeout, "total_seconds") else float(timeout)
+            deadline = time.monotonic() + secs
+            delay = 1e-5
+            while not self._w.is_completed():
+                if time.monotonic() > deadline:
+                    raise RuntimeError(f"xddp: Work.wait timed out after {secs:.3f} s (collective seq {self._w.seq})")
+                time.sleep(delay)
+                delay = min(delay * 2, 5e-3)
         if self._w is not None:
             self._w.wait()
         if self._post is not None and not self._done_post:
@@ -118,18 +131,61 @@ class Work:
         return self._outputs if self._outputs is not None else (self._w.result() if self._w is not None else [])
 
     def get_future(self) -> torch.futures.Future:
-        """A future completed once the collective is ordered before the caller's stream.
+        """A future for the collective's result; never blocks the caller.
 
-        GPU: the caller's current stream waits on the collective's event, so consumers that
-        run on that stream (e.g. a ``.then`` callback launching kernels) are correctly
-        ordered, exactly like the reference stack's NCCL futures.
+        GPU (RCCL): completed at once after the caller's current stream has been made to wait
+        on the collective's event — consumers that run on that stream (a ``.then`` callback
+        launching kernels) are ordered after it, exactly like the reference stack's NCCL
+        futures. CPU backend: completed by a completion thread when the collective finishes
+        (collectives complete in issue order, so one FIFO thread serves all of them).
         """
         if self._fut is None:
-            self.wait()
             self._fut = torch.futures.Future()
-            res = self.result()
-            self._fut.set_result(res)
+            gpu = self._w is not None and self._outputs_on_gpu()
+            if self._w is None or gpu:
+                self.wait()
+                self._fut.set_result(self.result())
+            else:
+                _completer().submit(self)
         return self._fut
+
+    def _outputs_on_gpu(self) -> bool:
+        outs = self._outputs if self._outputs is not None else self._w.result()
+        return any(isinstance(t, torch.Tensor) and t.is_cuda for t in outs)
+
+
+class _FutureCompleter:
+    """One daemon thread completing CPU-backend futures in issue order."""
+
+    def __init__(self):
+        import queue
+        import threading
+
+        self.q = queue.Queue()
+        self.t = threading.Thread(target=self._run, name="xddp-future-completer", daemon=True)
+        self.t.start()
+
+    def submit(self, work: "Work"):
+        self.q.put(work)
+
+    def _run(self):
+        while True:
+            w = self.q.get()
+            try:
+                w.wait()
+                w._fut.set_result(w.result())
+            except Exception as e:  # noqa: BLE001 — surfaced through the future
+                w._fut.set_exception(e)
+
+
+_COMPLETER = None
+
+
+def _completer() -> _FutureCompleter:
+    global _COMPLETER
+    if _COMPLETER is None:
+        _COMPLETER = _FutureCompleter()
+    return _COMPLETER
 
 
 class _GroupMemberSentinel:
@@ -453,9 +509,38 @@ def reduce_scatter_tensor(output, input, op=ReduceOp.SUM, group=None, async_op=F
 
 
 def all_to_all_single(output, input, output_split_sizes=None, input_split_sizes=None, group=None, async_op=False):
-    if output_split_sizes is not None or input_split_sizes is not None:
-        raise NotImplementedError("uneven all_to_all splits are not supported yet")
-    return _ret(_resolve(group).alltoall_base(output, input), async_op)
+    """All-to-all along dim 0; uneven splits supported.
+
+    Uneven splits ride the equal-split collective (one ``ncclAllToAll`` on RCCL): every chunk
+    is padded to the largest split in the group (agreed with one tiny MAX all-reduce), then the
+    received chunks are compacted with one gather. Padding costs bandwidth only in proportion to
+    the imbalance, and the launch count stays at two collectives whatever W is."""
+    pg = _resolve(group)
+    if output_split_sizes is None and input_split_sizes is None:
+        return _ret(pg.alltoall_base(output, input), async_op)
+    W = pg.size()
+    n_in, n_out = input.shape[0], output.shape[0]
+    ins = list(input_split_sizes) if input_split_sizes is not None else [n_in // W] * W
+    outs = list(output_split_sizes) if output_split_sizes is not None else [n_out // W] * W
+    if len(ins) != W or len(outs) != W or sum(ins) != n_in or sum(outs) != n_out:
+        raise ValueError("split sizes must have one entry per rank and sum to dim 0 of the tensors")
+    m = torch.tensor([max(ins + outs)], dtype=torch.int64, device=input.device if pg.backend == "rccl" else "cpu")
+    pg.allreduce(m, ReduceOp.MAX).wait()
+    M = int(m.item())
+    row = tuple(input.shape[1:])
+    send = torch.zeros((W * M,) + row, dtype=input.dtype, device=input.device)
+    src_idx = torch.cat([torch.arange(M * d, M * d + n, device=input.device) for d, n in enumerate(ins)])
+    send.index_copy_(0, src_idx, input.contiguous())
+    recv = torch.empty_like(send)
+    w = pg.alltoall_base(recv, send)
+    dst_idx = torch.cat([torch.arange(M * s, M * s + n, device=output.device) for s, n in enumerate(outs)])
+
+    def post():
+        output.copy_(recv.index_select(0, dst_idx))
+
+    w._post = post
+    w._outputs = [output]
+    return _ret(w, async_op)
 
 
 def send(tensor, dst, group=None):

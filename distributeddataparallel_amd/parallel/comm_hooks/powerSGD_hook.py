@@ -21,20 +21,28 @@ from .default_hooks import _allreduce_fut
 
 
 def _orthogonalize(matrices: torch.Tensor, epsilon: float = 0.0):
-    """In-place Gram-Schmidt over the columns of each matrix in a [B, n, r] batch."""
-    num_cols = matrices.shape[2]
-    for i in range(num_cols):
-        col = matrices[:, :, i: i + 1]
-        if epsilon == 0:
-            try:
-                col /= torch.norm(col, dim=1, keepdim=True)
-            except ZeroDivisionError:
-                col.fill_(0.0)
-        else:
-            col /= torch.norm(col, dim=1, keepdim=True) + epsilon
-        if i + 1 < num_cols:
-            rest = matrices[:, :, i + 1:]
-            rest -= torch.sum(col * rest, dim=1, keepdim=True) * col
+    """Orthonormalize the columns of each matrix of a ``[B, n, r]`` batch in place.
+
+    Cholesky-QR, applied twice ("CholeskyQR2"): with ``G = PᵀP = L Lᵀ`` the matrix ``P L⁻ᵀ``
+    has orthonormal columns and spans the same space, with the positive-diagonal R of
+    Gram-Schmidt. Each pass is one batched ``r x r`` Gram product, one tiny Cholesky and one
+    triangular solve — a handful of batched launches whatever ``r`` is, instead of a
+    column-by-column loop of 4r small kernels. The second pass removes the loss of
+    orthogonality of a single pass (error ~ cond(P)² eps -> ~eps). ``epsilon`` (or a relative
+    1e-10 floor) regularises the Gram diagonal so rank-deficient P (e.g. all-zero gradients)
+    gives finite output.
+    """
+    work = matrices.float() if matrices.dtype in (torch.float16, torch.bfloat16) else matrices
+    r = work.shape[2]
+    eye = torch.eye(r, dtype=work.dtype, device=work.device)
+    for _ in range(2):
+        gram = work.transpose(1, 2) @ work
+        scale = gram.diagonal(dim1=1, dim2=2).amax(dim=1)
+        gram = gram + (max(epsilon, 0.0) + 1e-10 * scale + 1e-30)[:, None, None] * eye
+        chol, _ = torch.linalg.cholesky_ex(gram)
+        # P <- P L^-T  (solve X Lᵀ = P)
+        work = torch.linalg.solve_triangular(chol.transpose(1, 2), work, upper=True, left=False)
+    matrices.copy_(work)
 
 
 def _should_compress(num_rows, num_cols, rank, min_compression_rate):

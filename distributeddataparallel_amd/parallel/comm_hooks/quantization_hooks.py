@@ -18,6 +18,13 @@ def _qparams(t: torch.Tensor):
     return scale, zp
 
 
+def _gather_then(pg, payloads, finish) -> torch.futures.Future:
+    """All-gather each (out, in) pair without blocking the autograd thread; ``finish`` runs when
+    both payloads have arrived (on GPU: once the caller's stream is ordered after them)."""
+    futs = [pg.allgather_into_tensor(out, inp).get_future() for out, inp in payloads]
+    return torch.futures.collect_all(futs).then(lambda _: finish())
+
+
 def quantization_pertensor_hook(process_group, bucket) -> torch.futures.Future:
     pg = process_group if process_group is not None else xdist.get_default_group()
     w = pg.size()
@@ -28,15 +35,14 @@ def quantization_pertensor_hook(process_group, bucket) -> torch.futures.Future:
     qp = torch.stack([scale, zp]).float()
     all_q = torch.empty(w * q.numel(), dtype=torch.uint8, device=q.device)
     all_p = torch.empty(w * 2, dtype=torch.float32, device=q.device)
-    pg.allgather_into_tensor(all_q, q).wait()
-    pg.allgather_into_tensor(all_p, qp).wait()
-    all_q = all_q.view(w, -1).float()
-    all_p = all_p.view(w, 2)
-    deq = (all_q - all_p[:, 1:2]) * all_p[:, 0:1]
-    buf.copy_(deq.mean(0).to(buf.dtype))
-    fut = torch.futures.Future()
-    fut.set_result(buf)
-    return fut
+
+    def finish():
+        p = all_p.view(w, 2)
+        deq = (all_q.view(w, -1).float() - p[:, 1:2]) * p[:, 0:1]
+        buf.copy_(deq.mean(0).to(buf.dtype))
+        return buf
+
+    return _gather_then(pg, [(all_q, q), (all_p, qp)], finish)
 
 
 def quantization_perchannel_hook(process_group, bucket, bucket_size: int = 512) -> torch.futures.Future:
@@ -55,10 +61,10 @@ def quantization_perchannel_hook(process_group, bucket, bucket_size: int = 512) 
     qp = torch.cat([scale, zp], 1).contiguous()
     all_q = torch.empty((w,) + tuple(q.shape), dtype=torch.uint8, device=buf.device)
     all_p = torch.empty((w,) + tuple(qp.shape), dtype=torch.float32, device=buf.device)
-    pg.allgather_into_tensor(all_q, q).wait()
-    pg.allgather_into_tensor(all_p, qp).wait()
-    deq = (all_q.float() - all_p[..., 1:2]) * all_p[..., 0:1]
-    buf.copy_(deq.mean(0).reshape(-1)[:n].to(buf.dtype))
-    fut = torch.futures.Future()
-    fut.set_result(buf)
-    return fut
+
+    def finish():
+        deq = (all_q.float() - all_p[..., 1:2]) * all_p[..., 0:1]
+        buf.copy_(deq.mean(0).reshape(-1)[:n].to(buf.dtype))
+        return buf
+
+    return _gather_then(pg, [(all_q, q), (all_p, qp)], finish)

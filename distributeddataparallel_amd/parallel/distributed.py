@@ -11,11 +11,14 @@ API and behaviour follow the reference stack's wrapper (SURVEY.md §2.2 T6a–T6
 * per-forward buffer broadcast, ``no_sync()``, ``join()``, comm hooks, static graph,
   ``module.``-prefixed ``state_dict`` (the wrapped net lives in ``self.module``).
 
-MI355X additions (opt-in knobs, defaults keep reference semantics):
+MI355X additions:
 
+* ``bucket_policy`` — with ``bucket_cap_mb=None`` on the RCCL backend the rebuilt buckets follow
+  the xGMI policy of ``parallel/bucket_policy.py`` (small first bucket, large middle buckets for
+  big models, a small LAST bucket so the all-reduce exposed after backward is short). An
+  explicit ``bucket_cap_mb`` (or ``XDDP_BUCKET_CAP_MB``) keeps the reference semantics exactly;
 * ``comm_dtype`` — communicate gradients in bf16/fp16 with a fused cast inside the bucket
-  pack kernel (the builtin ``BF16_COMPRESS`` hook without a Python round trip);
-* ``bucket_cap_mb`` defaults can be overridden per job via ``XDDP_BUCKET_CAP_MB``.
+  pack kernel (the builtin ``BF16_COMPRESS`` hook without a Python round trip).
 """
 from __future__ import annotations
 
@@ -35,6 +38,7 @@ from torch.autograd.profiler import record_function
 from .. import distributed as xdist
 from .._native import load
 from ..utils import fault as _fault
+from . import bucket_policy as _bp
 from .join import Join, Joinable, JoinHook
 
 logger = logging.getLogger(__name__)
@@ -43,13 +47,22 @@ DEFAULT_FIRST_BUCKET_BYTES = 1024 * 1024
 DEFAULT_BUCKET_CAP_MB = 25
 BROADCAST_BUCKET_BYTES = 250 * 1024 * 1024
 
-__all__ = ["DistributedDataParallel", "BuiltinCommHookType"]
+__all__ = ["DistributedDataParallel", "BuiltinCommHookType", "BufferCommHookLocation"]
 
 
 class BuiltinCommHookType(Enum):
     ALLREDUCE = auto()
     FP16_COMPRESS = auto()
     BF16_COMPRESS = auto()
+
+
+class BufferCommHookLocation(Enum):
+    """Where a buffer comm hook runs (reference ``_BufferCommHookLocation``)."""
+    PRE_FORWARD = auto()
+    POST_FORWARD = auto()
+
+
+_BufferCommHookLocation = BufferCommHookLocation
 
 
 def _find_tensors(obj) -> List[torch.Tensor]:
@@ -130,15 +143,25 @@ class _DDPJoinHook(JoinHook):
         self.ddp._divide_by_initial_world_size = divide_by_initial_world_size
 
     def main_hook(self):
+        """Mirror, in order, the collectives one training iteration of a non-joined rank issues
+        (reference ``_DDPJoinHook.main_hook``): rebuild broadcast, buffer broadcast, the
+        "will you sync backward" flag, then one all-reduce per bucket with the same reduction
+        op and the unused-parameter bitmap — or nothing more when that iteration does not sync."""
         ddp = self.ddp
         ddp.reducer.rebuild_buckets()
         ddp._check_and_sync_module_buffers()
-        # zero gradient all-reduce per bucket (same order/sizes as the non-joined ranks)
-        for z in ddp.reducer.zeros_like_buckets():
-            ddp.process_group.allreduce(z, xdist.ReduceOp.SUM).wait()
+        should_sync = ddp._check_global_requires_backward_grad_sync(is_joined_rank=True)
+        # a skipped-sync iteration means the next forward does not broadcast buffers either
+        ddp.require_forward_param_sync = should_sync
+        if not should_sync:
+            return
+        ddp.reducer.shadow_allreduce_buckets(premul_sum=not ddp._divide_by_initial_world_size)
         if ddp.find_unused_parameters:
             m = torch.zeros(len(ddp._module_parameters), dtype=torch.int32, device=ddp._comm_device)
             ddp.process_group.allreduce(m, xdist.ReduceOp.SUM).wait()
+        # a rank that joined before finishing an iteration has no grad-ready order; seed one so
+        # it takes part in the rebuild broadcast the other ranks issue at their next forward
+        ddp.reducer.push_all_rebuilt_params()
 
     def post_hook(self, is_last_joiner: bool):
         self.ddp._sync_final_model(is_last_joiner)
@@ -163,18 +186,23 @@ class DistributedDataParallel(nn.Module, Joinable):
         param_to_hook_all_reduce=None,
         mixed_precision=None,
         device_mesh=None,
+        skip_all_reduce_unused_params: bool = False,
         comm_dtype: Optional[torch.dtype] = None,
         first_bucket_cap_mb: Optional[float] = None,
+        bucket_policy: Optional[str] = None,
     ):
         super().__init__()
         Joinable.__init__(self)
         C = load()
-        if device_mesh is not None:
-            raise NotImplementedError("device_mesh is not supported; pass process_group")
         if (delay_all_reduce_named_params is None) != (param_to_hook_all_reduce is None):
             raise ValueError("delay_all_reduce_named_params and param_to_hook_all_reduce need to be set at the "
                              "same time.")
+        if device_mesh is not None:
+            if process_group is not None:
+                raise RuntimeError("Cannot specify both process_group and device_mesh arguments.")
+            process_group = self._group_from_mesh(device_mesh)
         self.process_group = self._resolve_process_group(process_group)
+        self.skip_all_reduce_unused_params = skip_all_reduce_unused_params
         self.module = module
         self.dim = dim
         self.broadcast_buffers = broadcast_buffers
@@ -228,12 +256,13 @@ class DistributedDataParallel(nn.Module, Joinable):
         # used to run several DDP ranks on one GPU, where RCCL refuses duplicate devices)
         self._comm_device = self._param_device
 
-        env_cap = os.environ.get("XDDP_BUCKET_CAP_MB")
-        if bucket_cap_mb is None:
-            bucket_cap_mb = float(env_cap) if env_cap else DEFAULT_BUCKET_CAP_MB
-        self.bucket_bytes_cap = int(bucket_cap_mb * 1024 * 1024)
-        self.first_bucket_bytes_cap = int(first_bucket_cap_mb * 1024 * 1024) if first_bucket_cap_mb else \
-            DEFAULT_FIRST_BUCKET_BYTES
+        total_bytes = sum(p.numel() * p.element_size() for p in self._module_parameters)
+        if comm_dtype is not None:
+            total_bytes = sum(p.numel() for p in self._module_parameters) * torch.empty(0, dtype=comm_dtype).element_size()
+        self.bucket_plan, _ = _bp.resolve_plan(bucket_policy, bucket_cap_mb, first_bucket_cap_mb, total_bytes,
+                                               self.process_group.size(), self.process_group.backend)
+        self.bucket_bytes_cap = self.bucket_plan.cap_bytes
+        self.first_bucket_bytes_cap = self.bucket_plan.first_bytes
         self.broadcast_bucket_size = BROADCAST_BUCKET_BYTES
         self._comm_dtype = comm_dtype
 
@@ -354,6 +383,19 @@ class DistributedDataParallel(nn.Module, Joinable):
 
     # ----------------------------------------------------------------------------- setup
     @staticmethod
+    def _group_from_mesh(device_mesh):
+        """A 1-D device mesh names the data-parallel group (reference ``:688-717``)."""
+        if getattr(device_mesh, "ndim", 1) != 1:
+            raise RuntimeError("Only 1D device mesh is supported, but got {}.".format(device_mesh))
+        get = getattr(device_mesh, "get_group", None)
+        if get is None:
+            raise TypeError("device_mesh must provide get_group() (a torch DeviceMesh or an xddp mesh)")
+        try:
+            return get(mesh_dim=0)
+        except TypeError:
+            return get()
+
+    @staticmethod
     def _resolve_process_group(process_group):
         """xddp group, or a torch.distributed group (wrapped), or the default of either."""
         if process_group is not None and not isinstance(process_group, xdist.ProcessGroup):
@@ -372,14 +414,27 @@ class DistributedDataParallel(nn.Module, Joinable):
             return from_torch_process_group(None)
         return xdist.get_default_group()  # raises the "not initialized" error
 
+    def _expect_sparse_gradient(self) -> List[bool]:
+        """Parameters of ``nn.Embedding/EmbeddingBag(sparse=True)`` produce sparse gradients
+        (reference ``_build_params_for_reducer``, ``pt:nn/parallel/distributed.py:1337-1346``)."""
+        sparse_ids = set()
+        for m in self.module.modules():
+            if isinstance(m, (nn.Embedding, nn.EmbeddingBag)) and getattr(m, "sparse", False):
+                sparse_ids.add(id(m.weight))
+        return [id(p) in sparse_ids for p in self._module_parameters]
+
     def _build_reducer(self):
         C = load()
         params = self._module_parameters
+        expect_sparse = self._expect_sparse_gradient()
+        if any(expect_sparse) and self.gradient_as_bucket_view:
+            logger.warning("xddp: sparse-gradient parameters do not live in buckets (gradient_as_bucket_view "
+                           "applies to the dense ones)")
         if self.find_unused_parameters:
             limits = [self.first_bucket_bytes_cap, self.bucket_bytes_cap]
         else:
             limits = [sys.maxsize]
-        idx, lims = C.compute_bucket_assignment_by_size(params, limits)
+        idx, lims = C.compute_bucket_assignment_by_size(params, limits, expect_sparse)
         idx, lims = list(reversed(idx)), list(reversed(lims))
         cd = "" if self._comm_dtype is None else str(self._comm_dtype).replace("torch.", "")
         self.reducer = C.Reducer(
@@ -391,6 +446,9 @@ class DistributedDataParallel(nn.Module, Joinable):
             first_bucket_bytes_cap=self.first_bucket_bytes_cap,
             comm_dtype=cd,
             param_names=self._param_names,
+            skip_all_reduce_unused_params=self.skip_all_reduce_unused_params,
+            tail_bucket_bytes_cap=self.bucket_plan.tail_bytes,
+            expect_sparse=expect_sparse,
         )
 
     def _rebind_grad_accumulators(self, stream=None):
@@ -436,15 +494,29 @@ class DistributedDataParallel(nn.Module, Joinable):
             logger.info("xddp: rebuilt buckets: %s", self.reducer.bucket_sizes_bytes())
         if self._check_sync_bufs_pre_fwd():
             self._sync_buffers()
+        if self._join_config.enable:
+            # tell joined ranks whether this iteration's backward syncs (their shadow collectives)
+            self._check_global_requires_backward_grad_sync(is_joined_rank=False)
         if self.device_ids:
             inputs = _to_device(inputs, self.device_ids[0])
             kwargs = _to_device(kwargs, self.device_ids[0])
         return inputs, kwargs
 
+    def _check_global_requires_backward_grad_sync(self, is_joined_rank: bool):
+        flag = not is_joined_rank and torch.is_grad_enabled() and self.require_backward_grad_sync
+        t = torch.full((1,), 1 if flag else 0, dtype=torch.int32, device=self._comm_device)
+        work = self.process_group.allreduce(t, xdist.ReduceOp.SUM)
+        if is_joined_rank:
+            work.wait()
+            return bool(t.item() != 0)
+        return work
+
     def _post_forward(self, output):
         self._clear_grad_buffer()
         if self._delay_all_reduce_all_params:
             return output
+        if self._check_sync_bufs_post_fwd():
+            self._sync_buffers()
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             self.require_forward_param_sync = True
             outs = _find_tensors(output) if (self.find_unused_parameters and not self.static_graph) else []
@@ -467,7 +539,26 @@ class DistributedDataParallel(nn.Module, Joinable):
         return self.require_forward_param_sync and self.broadcast_buffers and len(self._buffers_list) > 0
 
     def _check_sync_bufs_pre_fwd(self) -> bool:
-        return self.will_sync_module_buffers()
+        hook = getattr(self, "buffer_hook", None)
+        return self.will_sync_module_buffers() and (hook is None or hook[2] == BufferCommHookLocation.PRE_FORWARD)
+
+    def _check_sync_bufs_post_fwd(self) -> bool:
+        hook = getattr(self, "buffer_hook", None)
+        return self.will_sync_module_buffers() and hook is not None and hook[2] == BufferCommHookLocation.POST_FORWARD
+
+    def _register_buffer_comm_hook(self, state, hook: Callable,
+                                   comm_hook_location=BufferCommHookLocation.POST_FORWARD):
+        """Replace the per-forward rank-0 buffer broadcast with ``hook(state, {name: buffer})``
+        (reference ``pt:nn/parallel/distributed.py:1909-1951``). The hook may return a list of
+        futures; they are awaited at the end of the next backward (finalize), so e.g. an
+        all-reduce of BN statistics overlaps the whole backward pass."""
+        if not callable(hook):
+            raise TypeError("buffer comm hook must be callable")
+        self.buffer_hook = (hook, state, comm_hook_location)
+
+    @property
+    def named_module_buffers(self):
+        return {n: b for n, b in self.module.named_buffers() if n not in self._params_and_buffers_to_ignore}
 
     def _find_common_rank(self, input_rank: int, rank_cond: bool) -> int:
         t = torch.tensor([input_rank if rank_cond else -1], device=self._comm_device)
@@ -481,6 +572,16 @@ class DistributedDataParallel(nn.Module, Joinable):
         with torch.no_grad():
             if self._join_config.enable:
                 src = self._find_common_rank(self.process_group.rank(), True)
+            hook = getattr(self, "buffer_hook", None)
+            if hook is not None:
+                futs = hook[0](hook[1], self.named_module_buffers)
+                if futs:
+                    if torch.is_grad_enabled() and self.require_backward_grad_sync:
+                        self.reducer.install_post_backward_futures(list(futs))
+                    else:
+                        for f in futs:
+                            f.wait()
+                return
             C = load()
             bufs = [b for b in self._buffers_list if b.numel() > 0]
             if bufs:
@@ -561,6 +662,7 @@ class DistributedDataParallel(nn.Module, Joinable):
 
     def _get_ddp_logging_data(self) -> dict:
         d = dict(self.reducer.construction_data())
+        d["bucket_policy"] = self.bucket_plan.policy
         for k, v in self.reducer.runtime_stats().items():
             d[k] = int(v) if float(v).is_integer() else v
         d["module_name"] = type(self.module).__name__

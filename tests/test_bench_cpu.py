@@ -1,0 +1,44 @@
+"""bench.py self-launch + self-reporting on the CPU backend (the same code path as the
+GPU N>1 run: the parent spawns one fresh child per rank, forwards rank 0's JSON line, and
+fails loudly if any rank fails)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(extra_env=None, args=()):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(extra_env or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--device", "cpu",
+                           "--model", "mlp", "--steps", "3", "--warmup", "2", *args],
+                          capture_output=True, text=True, timeout=240, env=env, cwd="/tmp")
+
+
+def test_self_launch_reports_one_json_line(tmp_path):
+    base = tmp_path / "n1.json"
+    base.write_text(json.dumps({"value": 1000.0}) + "\n")
+    r = _run(args=("--baseline-json", str(base)))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["nranks"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["steps"] == 3 and d["warmup"] == 2 and d["value"] > 0
+    assert d["buckets"]["count"] >= 1 and sum(d["buckets"]["bytes"]) > 0
+    assert d["comm"]["avg_backward_comm_ms"] > 0 and d["comm"]["timed_iterations"] >= 2
+    assert d["allreduce_busbw"] and all(p["busbw_GBps"] > 0 for p in d["allreduce_busbw"])
+    assert d["scaling_efficiency"] == pytest.approx(d["value"] / 2000.0, rel=1e-3)
+
+
+def test_self_launch_fails_when_a_rank_fails():
+    r = _run(extra_env={"XDDP_FAULT_INJECT": "rank=1,step=2,mode=exit,code=7"})
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "failed" in r.stderr
