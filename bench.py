@@ -72,6 +72,10 @@ def parse(argv=None):
     ap.add_argument("--busbw-iters", type=int, default=5, help="all-reduce bandwidth probe iterations (N>1)")
     ap.add_argument("--baseline-json", default=None, help="N=1 result line -> scaling_efficiency")
     ap.add_argument("--launch-timeout", type=float, default=1500.0, help="self-launch: kill children after this")
+    ap.add_argument("--tunableop", choices=["auto", "off", "use", "tune"], default="auto",
+                    help="hipBLASLt/rocBLAS GEMM solution selection via torch TunableOp: use = the tuned "
+                         "results shipped in tuning/tunableop (auto: for transformer models), tune = search "
+                         "and write gpurun_out/tunableop_<model>.csv")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     if a.batch_size is None:
@@ -172,6 +176,36 @@ def _install_miopen_tuning():
         if os.path.isdir(os.path.join(src, sub)) and var not in os.environ:
             shutil.copytree(os.path.join(src, sub), os.path.join(dst, sub))
             os.environ[var] = os.path.join(dst, sub)
+
+
+def _install_tunableop(args):
+    """GEMM tuning (MI355X-specific): torch's TunableOp benchmarks every rocBLAS/hipBLASLt
+    solution for each GEMM shape once; the winners for the transformer configs are shipped in
+    tuning/tunableop (made on MI355X with ``--tunableop tune``) and loaded read-only."""
+    mode = args.tunableop
+    if mode == "auto":
+        mode = "use" if (args.model.startswith("vit") or is_lm(args)) else "off"
+    if mode == "off" or args.device != "cuda":
+        return None
+    import shutil
+    import tempfile
+
+    name = f"tunableop_{args.model}.csv"
+    os.environ["PYTORCH_TUNABLEOP_ENABLED"] = "1"
+    if mode == "tune":
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        os.environ["PYTORCH_TUNABLEOP_TUNING"] = "1"
+        os.environ["PYTORCH_TUNABLEOP_FILENAME"] = os.path.join(REPO, "gpurun_out", name)
+        return "tune"
+    src = os.path.join(REPO, "tuning", "tunableop", name)
+    if not os.path.isfile(src):
+        os.environ["PYTORCH_TUNABLEOP_ENABLED"] = "0"
+        return None
+    dst = os.path.join(tempfile.mkdtemp(prefix=f"xddp_tunableop_{os.environ.get('LOCAL_RANK', '0')}_"), name)
+    shutil.copy(src, dst)
+    os.environ["PYTORCH_TUNABLEOP_TUNING"] = "0"
+    os.environ["PYTORCH_TUNABLEOP_FILENAME"] = dst
+    return "use"
 
 
 # ------------------------------------------------------------------------------ model / data
@@ -281,6 +315,7 @@ def main(argv=None):
         os.environ["MASTER_PORT"] = str(_free_port())
     if args.device == "cuda":
         _install_miopen_tuning()
+    tunableop = _install_tunableop(args)
     sys.path.insert(0, REPO)
 
     import torch
@@ -450,6 +485,7 @@ def main(argv=None):
                 "micro_batches": micro,
                 "hip_graphs": bool(args.graphs),
                 "rccl_env_defaults": rccl_env,
+                "gemm_tuning": tunableop or "off",
             },
             "final_loss": round(final_loss, 4),
             "scaling_efficiency": eff,
@@ -464,6 +500,8 @@ def main(argv=None):
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    if tunableop == "tune":
+        torch.cuda.tunable.write_file()
     dist.destroy_process_group()
     return 0
 
@@ -479,11 +517,11 @@ def diagnostics(args, ddp, step, sync, dist, device, world):
     out = {"nranks": int(pg.comm.size()), "comm_backend": pg.backend}
     sizes = list(red.bucket_sizes_bytes())
     out["buckets"] = {"count": len(sizes), "bytes": sizes, **ddp.bucket_plan.as_dict()}
-    if args.graphs:
+    if args.graphs or args.diag_steps <= 0:
         return out
     red.reset_runtime_stats()
     ddp._set_ddp_runtime_logging_sample_rate(1)
-    for _ in range(max(2, args.diag_steps) + 1):  # the last step harvests the previous one's timers
+    for _ in range(args.diag_steps + 1):  # the last step harvests the previous one's timers
         step()
         sync()  # timers are harvested at the next forward only once their events completed
     d = ddp._get_ddp_logging_data()

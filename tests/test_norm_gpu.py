@@ -80,7 +80,7 @@ def test_batchnorm_large_mean_offset_stable():
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("shape", [(4, 7, 1024), (3, 4096), (5, 40), (2, 3, 8192)])
+@pytest.mark.parametrize("shape", [(4, 7, 1024), (3, 4096), (5, 40), (2, 3, 8192), (32, 197, 1024), (1100, 4096)])
 def test_layernorm(dt, shape):
     torch.manual_seed(0)
     D = shape[-1]
