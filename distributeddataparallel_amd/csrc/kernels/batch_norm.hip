@@ -679,7 +679,7 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
 // part [groups, C, 2] = (sum g, sum g·(x - mean)) -> (coef [3, C] = (k1, k2, k3 - k2·mean), dw, db).
 std::vector<at::Tensor> bn_backward_from_partials(const at::Tensor& part, int64_t M,
                                                   const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
-                                                  const at::Tensor& invstd, bool need_dweight) {
+                                                  const at::Tensor& invstd, bool need_dweight, bool fold_mean) {
   TORCH_CHECK(part.is_cuda() && part.dim() == 3 && part.size(2) == 2 && part.scalar_type() == at::kFloat &&
                   part.is_contiguous(),
               "bn_backward_from_partials: partials must be float [groups, C, 2]");
@@ -697,10 +697,32 @@ std::vector<at::Tensor> bn_backward_from_partials(const at::Tensor& part, int64_
                        (int)part.size(0), (int)C, M, has_w ? reinterpret_cast<const W*>(weight->data_ptr()) : nullptr,
                        invstd.data_ptr<float>(), dw.defined() ? reinterpret_cast<W*>(dw.data_ptr()) : nullptr,
                        db.defined() ? reinterpret_cast<W*>(db.data_ptr()) : nullptr, coef.data_ptr<float>(),
-                       mean.data_ptr<float>());
+                       fold_mean ? mean.data_ptr<float>() : nullptr);
     XDDP_HIP_CHECK(hipGetLastError());
   });
   return {coef, dw, db};
+}
+
+at::Tensor bn_backward_elem(const at::Tensor& g_in, const at::Tensor& x, const at::Tensor& mean, const at::Tensor& coef) {
+  check_nhwc(x);
+  auto g = g_in.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(g.sizes() == x.sizes() && g.scalar_type() == x.scalar_type(), "bn_backward_elem: g must match x");
+  const int64_t C = x.size(1), M = x.numel() / C;
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.numel() >= 3 * C && coef.is_contiguous() &&
+                  mean.scalar_type() == at::kFloat && mean.numel() == C,
+              "bn_backward_elem: float coef [3, C] and mean [C] expected");
+  auto dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  const int64_t nvec = M * C / 8;
+  dispatch_act(x.scalar_type(), [&](auto tag_t) {
+    using T = decltype(tag_t);
+    hipLaunchKernelGGL((bn_bwd_elem_kernel<T, 0, false, false>), dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
+                       reinterpret_cast<const T*>(g.data_ptr()), nullptr, reinterpret_cast<const T*>(x.data_ptr()),
+                       nullptr, nullptr, reinterpret_cast<T*>(dx.data_ptr()), nullptr, nvec, (int)C,
+                       mean.data_ptr<float>(), coef.data_ptr<float>(), nullptr);
+    XDDP_HIP_CHECK(hipGetLastError());
+  });
+  return dx;
 }
 
 }  // namespace kernels

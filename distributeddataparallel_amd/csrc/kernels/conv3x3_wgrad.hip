@@ -1,0 +1,302 @@
+// 3x3 convolution weight gradient (NHWC, bf16, pad 1, stride 1 or 2) on gfx950 MFMA.
+//
+//   dW[n][r][s][c] = sum over output pixels p of dY[p][n] · X[in(p) + (r-1, s-1)][c]
+//
+// The reduction runs over B·OH·OW output pixels, the output is tiny (N x 9·Cin). MIOpen runs it
+// as a split-K implicit GEMM whose column tiles each see one tap, re-reading dY for every tap and
+// zero-filling its atomically accumulated output first (~2 ms of a ResNet-50 bs256 step). Here a
+// block owns a 64 (n) x 9 (taps) x 64 (c) output tile and walks the pixels in 8x8 output patches:
+// per patch it stages the dY patch (64 pixels x 64 n) and the X halo that all 9 taps read
+// (10x10 pixels at stride 1, 17x17 at stride 2) ONCE, and every tap's MFMAs read their shifted
+// pixel rows out of that halo. Per 64-pixel step: 21 KB (stride 1) staged for 4.7 MFLOP.
+//
+// * Both operands go global -> LDS with global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip);
+//   a wave-instruction fills 8 pixel rows of 128 B (64 channels). Rows outside the image (or past
+//   the patch grid) read a zero line instead of branching. Three (stride 1) or two (stride 2)
+//   LDS stages, counted `s_waitcnt vmcnt` + raw s_barrier.
+// * MFMA operands are read with gfx950's transposing ds_read_b64_tr_b16: the staged rows are
+//   pixel-major ([pixel][channel], as in HBM) and the MFMA wants channel-major fragments with the
+//   pixels along K. Bank conflicts are avoided by an XOR swizzle of the 32-B chunk pair on the
+//   pixel's 2-D coordinates ((x & 3) ^ (y & 1)): the 4 rows one 16-lane group reads land on
+//   distinct banks, and the two groups of a half-wave (adjacent pixel rows) on complementary
+//   ones. At stride 2 the halo is stored phase-split (even/odd rows and columns), so the 4 pixels
+//   a group reads are consecutive LDS rows as at stride 1.
+// * 4 waves; wave w owns input channels c0 + 16w..+15 for all 64 n and all 9 taps: 36 MFMA tiles,
+//   144 fp32 accumulators per lane (one 256-thread block per SIMD pair).
+// * Each block reduces its patch range into an fp32 slab; a second kernel sums the slabs (no
+//   zero-fill, no atomics, bitwise reproducible) and casts to the weight dtype.
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include "common.h"
+#include "kernels/dev_utils.h"
+
+namespace xddp {
+namespace kernels {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+using dev::f32x4;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int kP = 8;  // output patch edge (8x8 = 64 pixels = two 32-deep MFMA k-steps)
+
+__device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
+// XOR applied to a row's 32-B chunk-pair index (0..3), from the pixel's 2-D LDS coordinates
+__device__ __forceinline__ int swp(int y, int x) { return (x & 3) ^ (y & 1); }
+
+template <int ST>
+struct Halo {
+  // phases: 1 (stride 1) or 4 (stride 2: (row parity, column parity)); each phase an IYN x 10 grid
+  static constexpr int PHASES = ST == 1 ? 1 : 4;
+  static constexpr int IYN = ST == 1 ? kP + 2 : kP + 1;  // 10 | 9 (valid columns: the same)
+  static constexpr int IXW = 10;                         // row pitch of a phase grid (even: see swp)
+  static constexpr int ROWS = PHASES * IYN * IXW;        // 100 | 360 LDS rows
+  static constexpr int INSTR = (ROWS + 7) / 8;           // DMA wave-instructions (8 rows each)
+  static constexpr int PER_WAVE = (INSTR + 3) / 4;       // 4 | 12
+  static constexpr int BROWS = PER_WAVE * 32;            // 128 | 384 rows reserved
+  static constexpr int STAGES = ST == 1 ? 3 : 2;
+  static constexpr int STAGE = (64 + BROWS) * 128;       // bytes per stage
+  // LDS row of halo pixel (hy, hx) (0 <= hy < (kP-1)·ST+3)
+  __device__ static int row(int hy, int hx) {
+    if (ST == 1) return hy * IXW + hx;
+    return (((hy & 1) * 2 + (hx & 1)) * IYN + (hy >> 1)) * IXW + (hx >> 1);
+  }
+  __device__ static int ycoord(int hy) { return ST == 1 ? hy : hy >> 1; }
+  __device__ static int xcoord(int hx) { return ST == 1 ? hx : hx >> 1; }
+};
+
+template <int ST>
+__global__ __launch_bounds__(256, ST == 1 ? 2 : 1) void conv3x3_wgrad_kernel(
+    const uint16_t* __restrict__ dY, const uint16_t* __restrict__ X, float* __restrict__ ws,
+    const uint16_t* __restrict__ zeros, int N, int C, int IH, int IW, int OH, int OW, int pgh, int pgw,
+    int npatch, int ntiles, int splits) {
+  using H = Halo<ST>;
+  constexpr int STG = H::STAGES, LPS = 2 + H::PER_WAVE;  // DMA instructions per stage per wave
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wg = dev::xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wg % ntiles, sidx = wg / ntiles;  // XCD neighbours: same pixels, other tiles
+  const int ctiles = C >> 6;
+  const int n0 = (tile / ctiles) * 64, c0 = (tile % ctiles) * 64;
+  const int p_begin = (int)((int64_t)npatch * sidx / splits), p_end = (int)((int64_t)npatch * (sidx + 1) / splits);
+
+  // per-lane DMA row decode (patch-relative), fixed for the whole kernel
+  const int pos = lane & 7;  // 16-B slot this lane fills in its 128-B LDS row
+  int a_py[2], a_px[2], a_chunk[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (wid * 2 + i) * 8 + (lane >> 3);  // patch pixel 0..63
+    a_py[i] = r >> 3;
+    a_px[i] = r & 7;
+    a_chunk[i] = pos ^ (2 * swp(a_py[i], a_px[i]));
+  }
+  int b_hy[H::PER_WAVE], b_hx[H::PER_WAVE], b_chunk[H::PER_WAVE];
+#pragma unroll
+  for (int i = 0; i < H::PER_WAVE; ++i) {
+    const int r = (wid * H::PER_WAVE + i) * 8 + (lane >> 3);  // LDS row
+    const int ph = r / (H::IYN * H::IXW), rem = r - ph * (H::IYN * H::IXW);
+    const int iy = rem / H::IXW, ix = rem - iy * H::IXW;
+    const int hy = ST == 1 ? iy : 2 * iy + (ph >> 1), hx = ST == 1 ? ix : 2 * ix + (ph & 1);
+    const bool ok = r < H::ROWS && ix < (ST == 1 ? H::IXW : H::IYN) && hy < (kP - 1) * ST + 3 &&
+                    hx < (kP - 1) * ST + 3;
+    b_hy[i] = ok ? hy : -100000;  // invalid rows always read the zero line
+    b_hx[i] = hx;
+    b_chunk[i] = pos ^ (2 * swp(iy, ix));
+  }
+
+  auto issue = [&](int p, int buf) {
+    uint8_t* A = smem + buf * H::STAGE;
+    uint8_t* B = A + 64 * 128;
+    const int per_img = pgh * pgw;
+    const int b = p / per_img, pr = p - b * per_img, oy0 = (pr / pgw) * kP, ox0 = (pr % pgw) * kP;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int oy = oy0 + a_py[i], ox = ox0 + a_px[i];
+      const bool ok = oy < OH && ox < OW;
+      const uint16_t* src = ok ? dY + (((int64_t)b * OH + oy) * OW + ox) * N + n0 + a_chunk[i] * 8 : zeros;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(A + (wid * 2 + i) * 1024), 16, 0, 0);
+    }
+    const int gy0 = oy0 * ST - 1, gx0 = ox0 * ST - 1;
+#pragma unroll
+    for (int i = 0; i < H::PER_WAVE; ++i) {
+      const int gy = gy0 + b_hy[i], gx = gx0 + b_hx[i];
+      const bool ok = (unsigned)gy < (unsigned)IH && (unsigned)gx < (unsigned)IW;
+      const uint16_t* src = ok ? X + (((int64_t)b * IH + gy) * IW + gx) * C + c0 + b_chunk[i] * 8 : zeros;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(B + (wid * H::PER_WAVE + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read addressing: group g (lane >> 4) = patch row within the k-step, lane (4q + p)
+  // supplies pixel column q (+4 for the second read) and bytes 8p of its 32-B chunk pair
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const int np = p_end - p_begin;
+  for (int k = 0; k < STG - 1 && k < np; ++k) issue(p_begin + k, k);
+  for (int k = 0; k < np; ++k) {
+    // retire patch k's stage (later stages may stay in flight), then make every wave's DMA visible
+    const int ahead = min(STG - 2, np - 1 - k);
+    if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (k + STG - 1 < np) issue(p_begin + k + STG - 1, (k + STG - 1) % STG);
+    const uint8_t* A = smem + (k % STG) * H::STAGE;
+    const uint8_t* B = A + 64 * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int py = ks * 4 + g;
+      bf16x8 a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int x0 = q4, x1 = 4 + q4;
+        const v4s v8[2] = {lds_tr16(A + (py * 8 + x0) * 128 + ((i ^ swp(py, x0)) * 32) + 8 * p4),
+                           lds_tr16(A + (py * 8 + x1) * 128 + ((i ^ swp(py, x1)) * 32) + 8 * p4)};
+        a[i] = __builtin_bit_cast(bf16x8, v8);
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int r = t / 3, s = t % 3;
+        const int hy = py * ST + r, hx0 = q4 * ST + s, hx1 = (4 + q4) * ST + s;
+        const int y = H::ycoord(hy), x0 = H::xcoord(hx0), x1 = H::xcoord(hx1);
+        const v4s v8[2] = {lds_tr16(B + H::row(hy, hx0) * 128 + ((wid ^ swp(y, x0)) * 32) + 8 * p4),
+                           lds_tr16(B + H::row(hy, hx1) * 128 + ((wid ^ swp(y, x1)) * 32) + 8 * p4)};
+        const bf16x8 b = __builtin_bit_cast(bf16x8, v8);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][t], 0, 0, 0);
+      }
+    }
+  }
+  // fp32 slab ws[sidx][n][tap][c]: lane holds n = n0 + 16i + 4(lane >> 4) + r, c = c0 + 16·wid + (lane & 15)
+  float* out = ws + (int64_t)sidx * N * 9 * C;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + 16 * i + 4 * (lane >> 4) + r;
+        out[((int64_t)n * 9 + t) * C + c0 + 16 * wid + (lane & 15)] = acc[i][t][r];
+      }
+}
+
+// dW = sum of the S slabs, cast to the weight dtype (4 elements per lane, slab sum split 8 ways)
+template <typename W>
+__global__ __launch_bounds__(512) void slab_sum_kernel(const float* __restrict__ ws, int S, int64_t nk,
+                                                       W* __restrict__ dw) {
+  __shared__ f32x4 red[8][64];
+  const int c = threadIdx.x & 63, gi = threadIdx.x >> 6;
+  const int64_t v = (int64_t)blockIdx.x * 64 + c;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+  if (v * 4 < nk) {
+    const float* p = ws + v * 4;
+    int s = gi;
+    for (; s + 8 < S; s += 16) {
+      a0 += *reinterpret_cast<const f32x4*>(p + (int64_t)s * nk);
+      a1 += *reinterpret_cast<const f32x4*>(p + (int64_t)(s + 8) * nk);
+    }
+    for (; s < S; s += 8) a0 += *reinterpret_cast<const f32x4*>(p + (int64_t)s * nk);
+  }
+  red[gi][c] = a0 + a1;
+  __syncthreads();
+  if (gi == 0 && v * 4 < nk) {
+    f32x4 acc = red[0][c];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) acc += red[i][c];
+    dev::Elem<W, float>::st(dw, v * 4 + 0, acc.x);
+    dev::Elem<W, float>::st(dw, v * 4 + 1, acc.y);
+    dev::Elem<W, float>::st(dw, v * 4 + 2, acc.z);
+    dev::Elem<W, float>::st(dw, v * 4 + 3, acc.w);
+  }
+}
+
+const uint16_t* zero_line_w(const at::Tensor& like) {
+  static at::Tensor* z[64] = {};  // never freed: a static tensor would outlive the HIP runtime
+  const int d = like.device().index();
+  TORCH_CHECK(d >= 0 && d < 64, "conv3x3_wgrad: device index out of range");
+  if (!z[d]) z[d] = new at::Tensor(at::zeros({128}, like.options().dtype(at::kBFloat16)));
+  return reinterpret_cast<const uint16_t*>(z[d]->data_ptr());
+}
+
+int cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+}  // namespace
+
+// dy [B, N, OH, OW], x [B, C, IH, IW] (bf16 channels_last, pad 1, stride 1|2) -> dW [N, C, 3, 3]
+// channels_last (OHWI memory) in w_like's dtype.
+at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 &&
+                  dy.dim() == 4 && x.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_wgrad_patch: bf16 channels_last 4-D GPU tensors expected");
+  TORCH_CHECK(stride == 1 || stride == 2, "conv3x3_wgrad_patch: stride 1 or 2");
+  const int64_t B = x.size(0), C = x.size(1), IH = x.size(2), IW = x.size(3), N = dy.size(1);
+  const int64_t OH = (IH - 1) / stride + 1, OW = (IW - 1) / stride + 1;
+  TORCH_CHECK(dy.size(0) == B && dy.size(2) == OH && dy.size(3) == OW, "conv3x3_wgrad_patch: dy/x shape mismatch");
+  TORCH_CHECK(N % 64 == 0 && C % 64 == 0, "conv3x3_wgrad_patch: channel counts must be multiples of 64");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 40) && dy.numel() < (int64_t(1) << 40), "conv3x3_wgrad_patch: too large");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) % 16) == 0 && (reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16) == 0,
+              "conv3x3_wgrad_patch: 16-B aligned operands required");
+  const int pgh = (int)((OH + kP - 1) / kP), pgw = (int)((OW + kP - 1) / kP);
+  const int64_t npatch64 = B * pgh * pgw;
+  TORCH_CHECK(npatch64 > 0 && npatch64 < (int64_t(1) << 31), "conv3x3_wgrad_patch: bad patch count");
+  const int npatch = (int)npatch64;
+  const int ntiles = (int)((N / 64) * (C / 64));
+  const int per_cu = stride == 1 ? 2 : 1;  // resident blocks per CU (LDS: 72 KB | 112 KB per block)
+  int splits = std::max(1, std::min(npatch, (cu_count() * per_cu + ntiles - 1) / ntiles));
+  if (const char* e = std::getenv("XDDP_WGRAD3_SPLITS")) splits = std::max(1, std::min(npatch, std::atoi(e)));
+  auto ws = at::empty({splits, N, 9, C}, dy.options().dtype(at::kFloat));
+  auto dw = at::empty({N, C, 3, 3}, dy.options().dtype(w_like.scalar_type()).memory_format(at::MemoryFormat::ChannelsLast));
+  auto stream = c10::hip::getCurrentHIPStream(dy.device().index()).stream();
+  const uint16_t* zeros = zero_line_w(x);
+  auto go = [&](auto kern, size_t lds) {
+    static size_t lds_set = 0;
+    if (lds > 65536 && lds > lds_set) {
+      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      lds_set = lds;
+    }
+    hipLaunchKernelGGL(kern, dim3(ntiles * splits), dim3(256), lds, stream,
+                       reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                       ws.data_ptr<float>(), zeros, (int)N, (int)C, (int)IH, (int)IW, (int)OH, (int)OW, pgh, pgw,
+                       npatch, ntiles, splits);
+    XDDP_HIP_CHECK(hipGetLastError());
+  };
+  if (stride == 1) go(conv3x3_wgrad_kernel<1>, (size_t)Halo<1>::STAGES * Halo<1>::STAGE);
+  else go(conv3x3_wgrad_kernel<2>, (size_t)Halo<2>::STAGES * Halo<2>::STAGE);
+  const int64_t nk = N * 9 * C;
+  const int grid = (int)((nk / 4 + 63) / 64);
+  auto red = [&](auto tag) {
+    using W = decltype(tag);
+    hipLaunchKernelGGL((slab_sum_kernel<W>), dim3(grid), dim3(512), 0, stream, ws.data_ptr<float>(), splits, nk,
+                       reinterpret_cast<W*>(dw.data_ptr()));
+    XDDP_HIP_CHECK(hipGetLastError());
+  };
+  switch (w_like.scalar_type()) {
+    case at::kBFloat16: red(dev::bf16_t{}); break;
+    case at::kFloat: red(float{}); break;
+    case at::kHalf: red(dev::f16_t{}); break;
+    default: TORCH_CHECK(false, "conv3x3_wgrad_patch: unsupported weight dtype");
+  }
+  return dw;
+}
+
+}  // namespace kernels
+}  // namespace xddp

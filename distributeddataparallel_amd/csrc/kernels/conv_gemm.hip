@@ -62,12 +62,17 @@ __device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
 // g — that block's d(residual) / BN-backward input — and reduced per channel into the previous
 // BN's backward partials (sum g, sum g·(y - mean)) in bn_bwd_finalize's [groups][C][2] layout.
 // The previous block's separate BN-backward reduce pass (which re-read both gradients) is gone.
+// Second form (add = bits = nullptr, ss set): the input-gradient GEMM of a bottleneck's conv3,
+// whose input is relu(bn2(y2)) with a single consumer: g = dX masked by relu(y2·s + t) > 0 (the
+// mask recomputed from the BN input and its scale/shift), reduced into bn2's backward partials —
+// bn2's separate BN-backward reduce pass over (dX, y2) is gone.
 struct EpiBN {
   const uint16_t* add;
   const uint16_t* y;
   const uint8_t* bits;
   const float* mean;
   float* part;
+  const float* ss;  // [2][C] scale, shift (mask recompute form)
 };
 
 struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every stride-th pixel)
@@ -89,8 +94,12 @@ struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every st
 // BT: the B operand is given K-major (Wt[k][n], e.g. the forward weight W[n_out][k_in] used as Wᵀ by
 // the input-gradient GEMM): staged as [64 k][BN n] rows (padded 32 B) and read into fragments with
 // the transposing ds_read_b64_tr_b16, so no transposed weight copy is made.
-template <int BM, int BN, int WM, int WN, int PRO, bool STATS, bool STRIDED, bool BT = false, bool EPI = false>
-__global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
+// OCC: waves per SIMD the register budget is sized for. 4 (default) = two 8-wave blocks per CU
+// within 128 VGPRs (some variants spill a few registers to scratch); 2 = one block per CU with up
+// to 256 VGPRs and no spills (XDDP_GEMM_OCC=2; the persistent grid shrinks to one block per CU).
+template <int BM, int BN, int WM, int WN, int PRO, bool STATS, bool STRIDED, bool BT = false, bool EPI = false,
+          int OCC = 4>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, int64_t M, int N,
     int K, RowMap rm, const float* __restrict__ pro_ss, float* __restrict__ part, int mtiles, int ntiles,
     int groups, const uint16_t* __restrict__ X2, EpiBN epi) {
@@ -141,10 +150,15 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
   // PRO: the per-input-channel coefficients for all K channels, staged once into LDS after the
   // two operand buffers (kept out of the VGPRs that the MFMA phase needs)
   float* pro_lds = reinterpret_cast<float*>(smem + 2 * BUF);
+  // EPI mask-recompute form: this N tile's (scale, shift) of the masked BN, after the coefficients
+  float* epi_ss_lds = pro_lds + (PRO == 3 ? 5 : PRO == 2 ? 3 : PRO == 1 ? 2 : 0) * K;
+  if (EPI && epi.ss) {
+    for (int i = tid; i < 2 * BN; i += NT) epi_ss_lds[i] = epi.ss[(i >= BN ? N - BN : 0) + n0 + i];
+  }
   if (PRO) {
     for (int i = tid; i < (PRO == 3 ? 5 : PRO == 2 ? 3 : 2) * K; i += NT) pro_lds[i] = pro_ss[i];
-    lds_barrier();
   }
+  if (PRO || (EPI && epi.ss)) lds_barrier();
   const uint16_t* arow[AR];
   const int64_t dx2 = PRO >= 2 ? X2 - X : 0;  // the second A source at the same element offsets
   // Rows past M load row M-1 (clamped, branch-free: a per-row "load or zero" select makes hipcc
@@ -308,15 +322,23 @@ __global__ __launch_bounds__(64 * WM * WN, 4) void conv1x1_gemm_kernel(
         u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
         if (EPI) {
           const int64_t e0 = (m0 + row) * N + n0 + cc * 8;
-          const u32x4 ad = *reinterpret_cast<const u32x4*>(epi.add + e0);
           const u32x4 yv = *reinterpret_cast<const u32x4*>(epi.y + e0);
-          const uint32_t mb = epi.bits[e0 >> 3];
+          const bool form1 = epi.bits != nullptr;  // uniform per launch
+          const u32x4 ad = form1 ? *reinterpret_cast<const u32x4*>(epi.add + e0) : u32x4{0, 0, 0, 0};
+          const uint32_t mb = form1 ? epi.bits[e0 >> 3] : 0u;
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
             float g0 = __uint_as_float(v[h] << 16) + __uint_as_float(ad[h] << 16);
             float g1 = __uint_as_float(v[h] & 0xffff0000u) + __uint_as_float(ad[h] & 0xffff0000u);
-            g0 = ((mb >> (2 * h)) & 1u) ? g0 : 0.f;
-            g1 = ((mb >> (2 * h + 1)) & 1u) ? g1 : 0.f;
+            if (form1) {
+              g0 = ((mb >> (2 * h)) & 1u) ? g0 : 0.f;
+              g1 = ((mb >> (2 * h + 1)) & 1u) ? g1 : 0.f;
+            } else {
+              const float2 sc = *reinterpret_cast<const float2*>(epi_ss_lds + cc * 8 + 2 * h);
+              const float2 sh = *reinterpret_cast<const float2*>(epi_ss_lds + BN + cc * 8 + 2 * h);
+              g0 = fmaf(__uint_as_float(yv[h] << 16), sc.x, sh.x) > 0.f ? g0 : 0.f;
+              g1 = fmaf(__uint_as_float(yv[h] & 0xffff0000u), sc.y, sh.y) > 0.f ? g1 : 0.f;
+            }
             v[h] = dev::pack_bf16x2(g0, g1);
             g0 = __uint_as_float(v[h] << 16);  // the sums see g at storage precision
             g1 = __uint_as_float(v[h] & 0xffff0000u);
@@ -720,7 +742,7 @@ int num_cus() {
   return n;
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int OCC>
 void launch_gemm(int pro, bool stats, bool bt, dim3 grid, size_t lds, hipStream_t s, const uint16_t* x,
                  const uint16_t* w, uint16_t* y, int64_t M, int N, int K, RowMap rm, const float* pss, float* part,
                  int mt, int nt, int groups, const uint16_t* x2, const EpiBN& epi) {
@@ -734,15 +756,16 @@ void launch_gemm(int pro, bool stats, bool bt, dim3 grid, size_t lds, hipStream_
                        epi);
   };
 #define XDDP_G(P, S)                                                                                       \
-  if (rm.stride > 1) go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, true>);                                   \
-  else go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, false>)
+  if (rm.stride > 1) go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, true, false, false, OCC>);                \
+  else go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, false, false, false, OCC>)
   if (bt) {  // input gradient on the untransposed weight: stride 1, no statistics
-    if (epi.part) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 0, false, false, true, true>);
-    else if (pro == 3) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 3, false, false, true>);
-    else if (pro == 2) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 2, false, false, true>);
-    else go(conv1x1_gemm_kernel<BM, BN, WM, WN, 0, false, false, true>);
-  } else if (pro == 3) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 3, false, false>);  // stride-1 input gradient only
-  else if (pro == 2) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 2, false, false>);
+    if (epi.part && pro == 2) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 2, false, false, true, true, OCC>);
+    else if (epi.part) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 0, false, false, true, true, OCC>);
+    else if (pro == 3) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 3, false, false, true, false, OCC>);
+    else if (pro == 2) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 2, false, false, true, false, OCC>);
+    else go(conv1x1_gemm_kernel<BM, BN, WM, WN, 0, false, false, true, false, OCC>);
+  } else if (pro == 3) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 3, false, false, false, false, OCC>);  // stride-1 dgrad only
+  else if (pro == 2) go(conv1x1_gemm_kernel<BM, BN, WM, WN, 2, false, false, false, false, OCC>);
   else if (pro == 1) { if (stats) XDDP_G(1, true); else XDDP_G(1, false); }
   else { if (stats) XDDP_G(0, true); else XDDP_G(0, false); }
 #undef XDDP_G
@@ -758,7 +781,8 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
                                      const c10::optional<at::Tensor>& prologue_ss, bool stats,
                                      const c10::optional<at::Tensor>& prologue_y, bool w_t,
                                      const c10::optional<at::Tensor>& epi_add, const c10::optional<at::Tensor>& epi_y,
-                                     const c10::optional<at::Tensor>& epi_bits, const c10::optional<at::Tensor>& epi_mean) {
+                                     const c10::optional<at::Tensor>& epi_bits, const c10::optional<at::Tensor>& epi_mean,
+                                     const c10::optional<at::Tensor>& epi_ss) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16, "conv1x1_gemm: x must be 4-D bf16 on GPU");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv1x1_gemm: x must be channels_last");
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 1 && w.size(3) == 1 && w.scalar_type() == at::kBFloat16,
@@ -786,16 +810,26 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
                 "conv1x1_gemm: prologue_y must match x (bf16 channels_last), stride 1, no stats");
   auto y = at::empty({B, N, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
-  const bool epi_on = epi_add.has_value() && epi_add->defined();
+  const bool epi_form1 = epi_add.has_value() && epi_add->defined();
+  const bool epi_form2 = !epi_form1 && epi_ss.has_value() && epi_ss->defined();
+  const bool epi_on = epi_form1 || epi_form2;
   if (epi_on) {
-    TORCH_CHECK(w_t && pro == 0, "conv1x1_gemm: the BN-reduce epilogue needs w_t and no prologue");
-    TORCH_CHECK(epi_add->sizes() == y.sizes() && epi_add->scalar_type() == at::kBFloat16 &&
-                    epi_add->is_contiguous(at::MemoryFormat::ChannelsLast) && epi_y.has_value() &&
-                    epi_y->sizes() == y.sizes() && epi_y->scalar_type() == at::kBFloat16 &&
-                    epi_y->is_contiguous(at::MemoryFormat::ChannelsLast) && epi_bits.has_value() &&
-                    epi_bits->scalar_type() == at::kByte && epi_bits->numel() * 8 == y.numel() &&
-                    epi_mean.has_value() && epi_mean->scalar_type() == at::kFloat && epi_mean->numel() == N,
-                "conv1x1_gemm: epilogue tensors must match the output (bf16 channels_last, uint8 bits, float mean)");
+    TORCH_CHECK(w_t && (pro == 0 || (epi_form2 && pro == 2)),
+                "conv1x1_gemm: the BN-reduce epilogue needs w_t (and no prologue, or the BN-backward one with "
+                "the mask-recompute epilogue)");
+    TORCH_CHECK(epi_y.has_value() && epi_y->sizes() == y.sizes() && epi_y->scalar_type() == at::kBFloat16 &&
+                    epi_y->is_contiguous(at::MemoryFormat::ChannelsLast) && epi_mean.has_value() &&
+                    epi_mean->scalar_type() == at::kFloat && epi_mean->numel() == N && epi_mean->is_contiguous(),
+                "conv1x1_gemm: epilogue y / mean must match the output (bf16 channels_last, float mean)");
+    if (epi_form1) {
+      TORCH_CHECK(epi_add->sizes() == y.sizes() && epi_add->scalar_type() == at::kBFloat16 &&
+                      epi_add->is_contiguous(at::MemoryFormat::ChannelsLast) && epi_bits.has_value() &&
+                      epi_bits->scalar_type() == at::kByte && epi_bits->numel() * 8 == y.numel(),
+                  "conv1x1_gemm: epilogue add / bits must match the output (bf16 channels_last, uint8 bits)");
+    } else {
+      TORCH_CHECK(epi_ss->scalar_type() == at::kFloat && epi_ss->numel() >= 2 * N && epi_ss->is_contiguous(),
+                  "conv1x1_gemm: epilogue scale/shift must be float [2, N]");
+    }
   }
   const int BM = 128, BN = (N % 128 == 0) ? 128 : 64;
   const int mtiles = (int)((M + BM - 1) / BM), ntiles = (int)(N / BN);
@@ -804,30 +838,38 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
     const char* e = std::getenv("XDDP_GEMM_BLOCKS_PER_CU");
     return e ? std::max(1, std::atoi(e)) : 2;  // persistent: one resident round (2 blocks per CU) measured best
   }();
-  const int target = num_cus() * blocks_per_cu;
+  static const int occ = [] {
+    const char* e = std::getenv("XDDP_GEMM_OCC");
+    return e && std::atoi(e) == 2 ? 2 : 4;
+  }();
+  const int target = num_cus() * (occ == 2 ? 1 : blocks_per_cu);
   int groups = std::max(1, std::min(mtiles, (target + ntiles - 1) / ntiles));
   at::Tensor part = stats ? at::empty({groups, 3, N}, x.options().dtype(at::kFloat))
                           : (epi_on ? at::empty({groups, N, 2}, x.options().dtype(at::kFloat)) : at::Tensor());
-  EpiBN epi{nullptr, nullptr, nullptr, nullptr, nullptr};
-  if (epi_on)
+  EpiBN epi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (epi_form1)
     epi = EpiBN{reinterpret_cast<const uint16_t*>(epi_add->data_ptr()), reinterpret_cast<const uint16_t*>(epi_y->data_ptr()),
-                epi_bits->data_ptr<uint8_t>(), epi_mean->data_ptr<float>(), part.data_ptr<float>()};
+                epi_bits->data_ptr<uint8_t>(), epi_mean->data_ptr<float>(), part.data_ptr<float>(), nullptr};
+  else if (epi_form2)
+    epi = EpiBN{nullptr, reinterpret_cast<const uint16_t*>(epi_y->data_ptr()), nullptr, epi_mean->data_ptr<float>(),
+                part.data_ptr<float>(), epi_ss->data_ptr<float>()};
   RowMap rm{(int)OH, (int)OW, (int)IH, (int)IW, (int)stride};
   const dim3 grid(groups * ntiles);
   const size_t bbytes = w_t ? (size_t)64 * (BN * 2 + 32) : (size_t)BN * 128;
-  const size_t lds = 2 * ((size_t)BM * 128 + bbytes) + (pro ? ncoef * K * sizeof(float) : 0);
+  const size_t lds = 2 * ((size_t)BM * 128 + bbytes) + (pro ? ncoef * K * sizeof(float) : 0) +
+                     (epi_form2 ? 2 * (size_t)BN * sizeof(float) : 0);
   const auto* x2p = pro >= 2 ? reinterpret_cast<const uint16_t*>(prologue_y->data_ptr()) : nullptr;
   const auto* xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
   const auto* wp = reinterpret_cast<const uint16_t*>(wc.data_ptr());
   auto* yp = reinterpret_cast<uint16_t*>(y.data_ptr());
   const float* pss = pro ? prologue_ss->data_ptr<float>() : nullptr;
   float* pp = stats ? part.data_ptr<float>() : nullptr;  // (EPI partials travel in epi)
-  if (BN == 128)
-    launch_gemm<128, 128, 4, 2>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles,
-                                ntiles, groups, x2p, epi);
-  else
-    launch_gemm<128, 64, 8, 1>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles,
-                               ntiles, groups, x2p, epi);
+#define XDDP_LG(BN_, WM_, WN_, OCC_)                                                                            \
+  launch_gemm<128, BN_, WM_, WN_, OCC_>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, \
+                                        mtiles, ntiles, groups, x2p, epi)
+  if (BN == 128) { if (occ == 2) XDDP_LG(128, 4, 2, 2); else XDDP_LG(128, 4, 2, 4); }
+  else { if (occ == 2) XDDP_LG(64, 8, 1, 2); else XDDP_LG(64, 8, 1, 4); }
+#undef XDDP_LG
   return {y, part};
 }
 

@@ -27,16 +27,22 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
                                      const c10::optional<at::Tensor>& prologue_ss, bool stats,
                                      const c10::optional<at::Tensor>& prologue_y, bool w_t,
                                      const c10::optional<at::Tensor>& epi_add, const c10::optional<at::Tensor>& epi_y,
-                                     const c10::optional<at::Tensor>& epi_bits, const c10::optional<at::Tensor>& epi_mean);
+                                     const c10::optional<at::Tensor>& epi_bits, const c10::optional<at::Tensor>& epi_mean,
+                                     const c10::optional<at::Tensor>& epi_ss);
 // BN backward from external (sum g, sum g·(x - mean)) partials [groups, C, 2]: (coef [3, C] with the
 // mean folded in, dweight, dbias)
 std::vector<at::Tensor> bn_backward_from_partials(const at::Tensor& part, int64_t M,
                                                   const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
-                                                  const at::Tensor& invstd, bool need_dweight);
+                                                  const at::Tensor& invstd, bool need_dweight, bool fold_mean);
+// dx = k1·g + k2·(x - mean) + k3 per channel (coef [3, C] unfolded): the BN-backward elementwise
+// pass on an already-masked gradient g
+at::Tensor bn_backward_elem(const at::Tensor& g, const at::Tensor& x, const at::Tensor& mean, const at::Tensor& coef);
 // 3x3 pad-1 conv (stride 1/2) as an implicit MFMA GEMM (csrc/kernels/conv3x3.hip)
 std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats);
 at::Tensor conv3x3_rot_weight(const at::Tensor& w);
 at::Tensor conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like);
+// 3x3 weight gradient over 8x8 output patches with a shared X halo (csrc/kernels/conv3x3_wgrad.hip)
+at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like);
 at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,
                          const c10::optional<at::Tensor>& prologue_y, const c10::optional<at::Tensor>& coef);
 std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M,

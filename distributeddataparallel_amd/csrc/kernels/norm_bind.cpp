@@ -18,12 +18,15 @@ void bind_norm_kernels(py::module_& m) {
         py::arg("save_mask"), py::arg("num_batches_tracked"));
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("prologue_ss"),
         py::arg("stats"), py::arg("prologue_y") = py::none(), py::arg("w_t") = false, py::arg("epi_add") = py::none(),
-        py::arg("epi_y") = py::none(), py::arg("epi_bits") = py::none(), py::arg("epi_mean") = py::none());
+        py::arg("epi_y") = py::none(), py::arg("epi_bits") = py::none(), py::arg("epi_mean") = py::none(),
+        py::arg("epi_ss") = py::none());
   m.def("bn_backward_from_partials", &bn_backward_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),
-        py::arg("mean"), py::arg("invstd"), py::arg("need_dweight"));
+        py::arg("mean"), py::arg("invstd"), py::arg("need_dweight"), py::arg("fold_mean") = true);
+  m.def("bn_backward_elem", &bn_backward_elem, py::arg("g"), py::arg("x"), py::arg("mean"), py::arg("coef"));
   m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"));
   m.def("conv3x3_rot_weight", &conv3x3_rot_weight, py::arg("w"));
   m.def("conv3x3_wgrad", &conv3x3_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"));
+  m.def("conv3x3_wgrad_patch", &conv3x3_wgrad_patch, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"));
   m.def("conv1x1_wgrad", &conv1x1_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"),
         py::arg("prologue_y") = py::none(), py::arg("coef") = py::none());
   m.def("bn_stats_from_partials", &bn_stats_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),

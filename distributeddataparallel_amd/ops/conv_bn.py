@@ -46,10 +46,31 @@ class EpiLink:
         self.y = self.bits = self.mean = self.add = self.part = None
 
 
+class BNReLULink:
+    """Backward hand-off from a bottleneck's conv3 to the conv2 (3x3) + BN2 + ReLU that produced
+    its input (a single consumer). conv3's input-gradient GEMM masks its output by BN2's ReLU
+    (recomputed from y2 and BN2's scale/shift) and reduces BN2's backward partials in its epilogue
+    (``conv1x1_gemm(..., epi_ss=...)``, csrc/kernels/conv_gemm.hip EpiBN second form); BN2's
+    backward then skips its reduce pass over (dout, y2). ``g`` is the exact tensor handed to
+    autograd: if the gradient that reaches BN2 is any other tensor (another consumer's gradient
+    was summed in), the partials do not describe it and BN2 falls back to its own reduce."""
+
+    __slots__ = ("y", "mean", "ss", "part", "g")
+
+    def __init__(self, y, mean, ss):
+        self.y, self.mean, self.ss = y, mean, ss
+        self.part = self.g = None
+
+
+def _same_tensor(a, b) -> bool:
+    return a is not None and b is not None and a.data_ptr() == b.data_ptr() and a.shape == b.shape and \
+        a.stride() == b.stride()
+
+
 class _Conv1x1BN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, residual, relu, dual,
-                stride, link_out, link_x, link_res):
+                stride, link_out, link_x, link_res, link_in):
         C = load()
         ctx.set_materialize_grads(False)
         y, part = C.conv1x1_gemm(x, w, stride, None, True)
@@ -60,7 +81,7 @@ class _Conv1x1BN(torch.autograd.Function):
         out, bits = C.bn_apply(y, ss, residual, relu, keep_mask, nbt)
         ctx.relu, ctx.has_res, ctx.stride = relu, residual is not None, stride
         ctx.save_for_backward(x, w, y, bits if keep_mask else None, weight, mean, invstd, ss)
-        ctx.link_out, ctx.link_x, ctx.link_res = link_out, link_x, link_res
+        ctx.link_out, ctx.link_x, ctx.link_res, ctx.link_in = link_out, link_x, link_res, link_in
         if link_out is not None:
             if keep_mask and dual:
                 link_out.y, link_out.bits, link_out.mean = y, bits, mean
@@ -85,7 +106,7 @@ class _Conv1x1BN(torch.autograd.Function):
         if dout is None:
             dout, dout2 = dout2, None
         if dout is None:
-            return (None,) * 17
+            return (None,) * 18
         need_bn_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         s = ctx.stride
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
@@ -99,7 +120,7 @@ class _Conv1x1BN(torch.autograd.Function):
             dres = g if need_dres else None
             dx = dw = None
             if s == 1 and need_x and _dgrad_gemm():
-                dx = _dgrad(C, g, w, coef, y)
+                dx = _dgrad_in(ctx, C, g, w, coef, y)
             if need_w and s == 1 and _wgrad_gemm():
                 dw = C.conv1x1_wgrad(g, x, 1, w, y, coef)
             if (need_x and dx is None) or (need_w and dw is None):
@@ -121,7 +142,7 @@ class _Conv1x1BN(torch.autograd.Function):
             coef, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu, need_dres,
                                                      need_bn_w, dout2, bits, True)
             g = dres if need_dres else dout.contiguous(memory_format=torch.channels_last)
-            dx = _dgrad(C, g, w, coef, y)
+            dx = _dgrad_in(ctx, C, g, w, coef, y)
             dw = C.conv1x1_wgrad(g, x, 1, w, y, coef)
             return _grads(ctx, dx, dw, dw_bn, db_bn, dres)
         dy, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu, need_dres,
@@ -137,7 +158,7 @@ class _Conv1x1BN(torch.autograd.Function):
                 dx, lx.part = C.conv1x1_gemm(dy, w, 1, None, False, None, True, lx.add, lx.y, lx.bits, lx.mean)
                 lx.add = None
             else:
-                dx = _dgrad(C, dy, w, None, None)
+                dx = _dgrad_in(ctx, C, dy, w, None, None)
             need_x = False
         if need_w and _wgrad_gemm():
             # dW[N, K] = dYᵀ[N, M] · X[M, K] (strided pixel rows for the downsample): 14 % less
@@ -153,16 +174,28 @@ class _Conv1x1BN(torch.autograd.Function):
 
 
 def _grads(ctx, dx, dw, dw_bn, db_bn, dres):
-    """The 17 input gradients of _Conv1x1BN; a linked residual gradient goes to the consumer link."""
+    """The 18 input gradients of _Conv1x1BN; a linked residual gradient goes to the consumer link."""
     if dres is not None and ctx.link_res is not None:
         ctx.link_res.add, dres = dres, None
     return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
-            None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None, None, None, None)
+            None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None, None, None, None,
+            None)
+
+
+def _dgrad_in(ctx, C, g, w, coef, y):
+    """Stride-1 input gradient; with a BNReLULink on the input, also the producer's masked BN-backward
+    partials (epilogue second form)."""
+    li = ctx.link_in
+    if li is None or not _epi() or os.environ.get("XDDP_CONV_EPI2", "1") == "0":
+        return _dgrad(C, g, w, coef, y)
+    dx, li.part = C.conv1x1_gemm(g, w, 1, coef, False, y, True, None, li.y, None, li.mean, li.ss)
+    li.g = dx
+    return dx
 
 
 class _Conv3x3BNReLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, stride):
+    def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, stride, link):
         C = load()
         ctx.set_materialize_grads(False)
         y, part = C.conv3x3_forward(x, w, stride, True)
@@ -172,31 +205,49 @@ class _Conv3x3BNReLU(torch.autograd.Function):
         out, _ = C.bn_apply(y, ss, None, True, False, nbt)
         ctx.stride = stride
         ctx.save_for_backward(x, w, y, weight, mean, invstd, ss)
+        ctx.link = link
+        if link is not None:
+            link.y, link.mean, link.ss = y, mean, ss
         return out
 
     @staticmethod
     def backward(ctx, dout):
         if dout is None:
-            return (None,) * 11
+            return (None,) * 12
         C = load()
         x, w, y, weight, mean, invstd, ss = ctx.saved_tensors
         need_bn_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
-        # ReLU mask recomputed from y·scale + shift inside the BN backward (no mask tensor kept)
-        dy, dw_bn, db_bn, _ = C.bn_backward(dout.contiguous(memory_format=torch.channels_last), y, None, weight,
-                                            mean, invstd, ss, True, False, need_bn_w, None, None)
+        lk = ctx.link
+        part = lk.part if (lk is not None and _same_tensor(dout, lk.g)) else None
+        if lk is not None:
+            lk.y = lk.mean = lk.ss = lk.part = lk.g = None
+        if part is not None:
+            # dout is already masked by this BN's ReLU and its backward partials were reduced by
+            # conv3's input-gradient epilogue: only the finalize + the elementwise pass remain
+            M = y.numel() // y.size(1)
+            coef, dw_bn, db_bn = C.bn_backward_from_partials(part, M, weight, mean, invstd, need_bn_w, False)
+            dy = C.bn_backward_elem(dout, y, mean, coef)
+        else:
+            # ReLU mask recomputed from y·scale + shift inside the BN backward (no mask tensor kept)
+            dy, dw_bn, db_bn, _ = C.bn_backward(dout.contiguous(memory_format=torch.channels_last), y, None, weight,
+                                                mean, invstd, ss, True, False, need_bn_w, None, None)
         s = ctx.stride
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dx = dw = None
         if need_x and s == 1:
             dx = C.conv3x3_forward(dy, C.conv3x3_rot_weight(w), 1, False)[0]
             need_x = False
+        if need_w and _wgrad3():
+            # 8x8 output patches sharing one staged X halo across the 9 taps (conv3x3_wgrad.hip)
+            dw = C.conv3x3_wgrad_patch(dy, x, s, w)
+            need_w = False
         if need_x or need_w:
             gx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
                                                             [need_x, need_w, False])
             dx = gx if need_x else dx
-            dw = gw if need_w else None
+            dw = gw if need_w else dw
         return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
 def _dgrad(C, g, w, coef, y):
@@ -218,6 +269,11 @@ def _epi() -> bool:
     """XDDP_CONV_EPI=0 keeps the previous block's BN-backward reduce pass separate instead of
     folding it into the next block's conv1 input-gradient GEMM epilogue (A/B switch)."""
     return os.environ.get("XDDP_CONV_EPI", "1") != "0"
+
+
+def _wgrad3() -> bool:
+    """XDDP_CONV3X3_WGRAD=0 sends the bottleneck 3x3 weight gradient back to MIOpen (A/B switch)."""
+    return os.environ.get("XDDP_CONV3X3_WGRAD", "1") != "0"
 
 
 def _dgrad_gemm() -> bool:
@@ -263,8 +319,13 @@ def conv3x3_bn_relu(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module):
     """``relu(bn(conv3x3(x)))`` on the implicit-GEMM kernel with BN statistics from its epilogue."""
     if not (_conv3x3() and conv.kernel_size == (3, 3) and conv_bn_supported(x, conv, bn)):
         return bn(conv(x), relu=True)
-    return _Conv3x3BNReLU.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), int(conv.stride[0]))
+    link = BNReLULink(None, None, None) if _epi() else None
+    out = _Conv3x3BNReLU.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                               bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), int(conv.stride[0]),
+                               link)
+    if link is not None:
+        out._xddp_bnr = link
+    return out
 
 
 def conv1x1_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, residual: Optional[torch.Tensor] = None,
@@ -280,9 +341,10 @@ def conv1x1_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, residual: Op
             and residual.is_contiguous(memory_format=torch.channels_last))):
         return bn(conv(x), residual=residual, relu=relu, dual_output=dual_output)
     link_out = EpiLink() if (dual_output and residual is not None and relu and _epi()) else None
+    link_in = getattr(x, "_xddp_bnr", None) if conv.stride[0] == 1 else None
     out = _Conv1x1BN.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                            bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), residual, relu,
-                           dual_output, int(conv.stride[0]), link_out, link_x, link_res)
+                           dual_output, int(conv.stride[0]), link_out, link_x, link_res, link_in)
     if link_out is not None:
         out[0]._xddp_epi = link_out
     return out

@@ -86,3 +86,28 @@ def test_conv3x3_bn_relu_forward_backward(stride):
     assert rel(bn.weight.grad, gr.grad) < 2e-2
     assert rel(bn.bias.grad, br.grad) < 2e-2
     assert int(bn.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("b,cin,h,w,cout,s", [
+    (2, 64, 16, 16, 64, 1),     # exact 8x8 patch grid
+    (3, 64, 14, 14, 128, 1),    # partial patches (14 = 8 + 6), 2 n-tiles
+    (2, 128, 9, 7, 64, 1),      # odd spatial size, 2 c-tiles
+    (2, 64, 15, 15, 64, 2),     # strided, odd input size (phase-split halo)
+    (2, 128, 28, 28, 128, 2),   # strided, ResNet-50 layer2 entry shape (reduced batch)
+    (1, 512, 7, 7, 512, 1),     # one partial patch per image, 64 tiles
+    (4, 64, 56, 56, 64, 1),     # ResNet-50 layer1 shape (reduced batch): many splits
+])
+def test_conv3x3_wgrad_patch_matches_conv2d(b, cin, h, w, cout, s):
+    """8x8-patch 3x3 weight gradient (csrc/kernels/conv3x3_wgrad.hip) vs fp32 PyTorch."""
+    torch.manual_seed(1)
+    x = _cl(torch.randn(b, cin, h, w, device="cuda"))
+    oh, ow = (h - 1) // s + 1, (w - 1) // s + 1
+    dy = _cl(torch.randn(b, cout, oh, ow, device="cuda"))
+    wt = _cl(torch.randn(cout, cin, 3, 3, device="cuda"))
+    dw = C.conv3x3_wgrad_patch(dy, x, s, wt)
+    assert dw.shape == wt.shape and dw.dtype == wt.dtype and dw.is_contiguous(memory_format=torch.channels_last)
+    ref = torch.nn.grad.conv2d_weight(x.float(), wt.shape, dy.float(), stride=s, padding=1)
+    torch.testing.assert_close(dw.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+    # fp32 output: no bf16 rounding of the result, only the inputs' (exact products, fp32 sums)
+    dw32 = C.conv3x3_wgrad_patch(dy, x, s, wt.float())
+    torch.testing.assert_close(dw32, ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())

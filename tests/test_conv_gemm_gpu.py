@@ -214,7 +214,7 @@ def test_dgrad_bn_reduce_epilogue(b, cin, h, w, cout):
     weight = torch.rand(cout, device="cuda") + 0.5
     invstd = torch.rand(cout, device="cuda") + 0.5
     M = b * h * w
-    coef, dwt, dbs = C.bn_backward_from_partials(part, M, weight, mean, invstd, True)
+    coef, dwt, dbs = C.bn_backward_from_partials(part, M, weight, mean, invstd, True, True)
     torch.testing.assert_close(dbs, sd, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dwt, sdx * invstd, rtol=1e-4, atol=1e-4)
     k1, k2 = weight * invstd, -weight * invstd ** 3 * sdx / M
@@ -238,6 +238,76 @@ def test_bottleneck_epilogue_handoff_matches_separate_pass(monkeypatch):
 
     def run(flag):
         monkeypatch.setenv("XDDP_CONV_EPI", flag)
+        m.load_state_dict(sd)
+        m.zero_grad()
+        loss = F.cross_entropy(m(x).float(), y)
+        loss.backward()
+        return loss.item(), torch.cat([p.grad.float().flatten() for p in m.parameters()])
+
+    l1, g1 = run("1")
+    l0, g0 = run("0")
+    assert abs(l1 - l0) < 1e-6 * max(1.0, abs(l0))
+    assert ((g1 - g0).norm() / g0.norm()).item() < 2e-2
+    assert F.cosine_similarity(g1, g0, dim=0).item() > 0.999
+
+
+@pytest.mark.parametrize("pro", [False, True])
+@pytest.mark.parametrize("b,cin,h,w,cout", [(2, 256, 14, 14, 64), (3, 128, 9, 7, 128), (2, 64, 8, 8, 256)])
+def test_dgrad_bn_mask_recompute_epilogue(pro, b, cin, h, w, cout):
+    """EPI second form (conv3 input gradient -> BN2 backward): g = [relu(y2·s + t) > 0]·dX with
+    dX = dY·W (optionally dY = k1·g3 + k2·y3 + k3 formed in the prologue), stored, plus per-channel
+    (sum g, sum g·(y2 - mean)) partials — against fp32 PyTorch of the same math."""
+    torch.manual_seed(7)
+    dy = _x(b, cin, h, w)
+    wf = (torch.randn(cin, cout, 1, 1, device="cuda") / cin ** 0.5).to(torch.bfloat16)
+    y2 = _x(b, cout, h, w, offset=0.2)
+    ss = torch.stack([torch.rand(cout, device="cuda") + 0.5, torch.randn(cout, device="cuda") * 0.3]).contiguous()
+    mean = y2.float().mean((0, 2, 3))
+    if pro:
+        y3 = _x(b, cin, h, w, offset=-0.1)
+        coef = torch.stack([torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.1,
+                            torch.randn(cin, device="cuda") * 0.05]).contiguous()
+        g, part = C.conv1x1_gemm(dy, wf, 1, coef, False, y3, True, None, y2, None, mean, ss)
+        src = (coef[0].view(1, -1, 1, 1) * dy.float() + coef[1].view(1, -1, 1, 1) * y3.float()
+               + coef[2].view(1, -1, 1, 1)).to(torch.bfloat16).float()
+    else:
+        g, part = C.conv1x1_gemm(dy, wf, 1, None, False, None, True, None, y2, None, mean, ss)
+        src = dy.float()
+    keep = (y2.float() * ss[0].view(1, -1, 1, 1) + ss[1].view(1, -1, 1, 1)) > 0
+    ref = torch.where(keep, F.conv_transpose2d(src, wf.float()), 0.0)
+    torch.testing.assert_close(g.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+    sd, sdx = part.sum(0).unbind(1)
+    gq = g.float()
+    torch.testing.assert_close(sd, gq.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(sdx, (gq * (y2.float() - mean.view(1, -1, 1, 1))).sum((0, 2, 3)), rtol=1e-3,
+                               atol=1e-2)
+    # the unfolded finalize + elementwise pass = the full BN backward on the masked gradient
+    weight = torch.rand(cout, device="cuda") + 0.5
+    invstd = torch.rand(cout, device="cuda") + 0.5
+    M = b * h * w
+    coef2, _, _ = C.bn_backward_from_partials(part, M, weight, mean, invstd, False, False)
+    dx = C.bn_backward_elem(g, y2, mean, coef2)
+    xh = (y2.float() - mean.view(1, -1, 1, 1)) * invstd.view(1, -1, 1, 1)
+    want = weight.view(1, -1, 1, 1) * invstd.view(1, -1, 1, 1) * (
+        gq - (sd / M).view(1, -1, 1, 1) - xh * (sdx * invstd / M).view(1, -1, 1, 1))
+    torch.testing.assert_close(dx.float(), want, rtol=2e-2, atol=2e-2 * want.abs().max().item())
+
+
+def test_bottleneck_bn2_fold_matches_separate_pass(monkeypatch):
+    """conv3's input-gradient epilogue folding BN2's backward reduce (XDDP_CONV_EPI2=1) gives the
+    same gradients as BN2's own reduce pass (=0)."""
+    from distributeddataparallel_amd.models.resnet import Bottleneck, ResNet
+    from distributeddataparallel_amd.ops import FusedBatchNorm2d
+
+    torch.manual_seed(8)
+    m = ResNet(Bottleneck, [2, 2, 1, 1], norm_layer=FusedBatchNorm2d).cuda().to(torch.bfloat16)
+    m = m.to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 64, 64, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (4,), device="cuda")
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+
+    def run(flag):
+        monkeypatch.setenv("XDDP_CONV_EPI2", flag)
         m.load_state_dict(sd)
         m.zero_grad()
         loss = F.cross_entropy(m(x).float(), y)
