@@ -242,7 +242,8 @@ int cu_count() {
 
 // dy [B, N, OH, OW], x [B, C, IH, IW] (bf16 channels_last, pad 1, stride 1|2) -> dW [N, C, 3, 3]
 // channels_last (OHWI memory) in w_like's dtype.
-at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like) {
+at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,
+                               int64_t splits_req) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 &&
                   dy.dim() == 4 && x.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -262,7 +263,7 @@ at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_
   const int ntiles = (int)((N / 64) * (C / 64));
   const int per_cu = stride == 1 ? 2 : 1;  // resident blocks per CU (LDS: 72 KB | 112 KB per block)
   int splits = std::max(1, std::min(npatch, (cu_count() * per_cu + ntiles - 1) / ntiles));
-  if (const char* e = std::getenv("XDDP_WGRAD3_SPLITS")) splits = std::max(1, std::min(npatch, std::atoi(e)));
+  if (splits_req > 0) splits = (int)std::min<int64_t>(npatch, splits_req);
   auto ws = at::empty({splits, N, 9, C}, dy.options().dtype(at::kFloat));
   auto dw = at::empty({N, C, 3, 3}, dy.options().dtype(w_like.scalar_type()).memory_format(at::MemoryFormat::ChannelsLast));
   auto stream = c10::hip::getCurrentHIPStream(dy.device().index()).stream();

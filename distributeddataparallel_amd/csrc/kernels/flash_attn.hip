@@ -1,0 +1,700 @@
+// Flash attention (forward + backward) for gfx950 MFMA, bf16 in/out, fp32 softmax statistics:
+// the ViT-L/16 (D = 64, 197 tokens, non-causal) and Llama-3-8B (D = 128, causal, GQA 32:8)
+// configs of BASELINE.json. torch's SDPA on this ROCm build runs AOTriton kernels at ~13 % (fwd)
+// and ~7 % (bwd) of the MI355X bf16 MFMA peak at Llama's shape; these are written for CDNA4
+// directly.
+//
+// Layout: q, k, v, o are [B, S, H, D] with D contiguous and any B/S/H strides (so the projection
+// outputs are used as views and o comes out ready for the output projection, no transposes).
+// GQA: q head h reads kv head h / (Hq / Hkv).
+//
+// Forward (one workgroup = 8 waves = 256 query rows of one (batch, head); wave = 32 rows; two
+// waves per SIMD so one wave's softmax / LDS / load waits hide under the other's MFMAs):
+// * swapped scores: S^T = K·Q^T on mfma_f32_32x32x16_bf16 with K as the A operand (from LDS) and
+//   Q^T as the B operand (Q kept in registers), so a lane owns ONE query row (lane & 31) and half
+//   of a 32-key tile: the row max / sum are in-lane plus one exchange with lane ^ 32;
+// * O is accumulated transposed, O^T = V^T·P^T, with V^T as the A operand read by gfx950's
+//   transposing ds_read_b64_tr_b16 and P^T (the score accumulator, rounded to bf16) as the B
+//   operand: the accumulator layout of S^T IS the B-operand layout when the PV reduction walks
+//   the keys in the order the lanes hold them (lane group g holds keys 4g..4g+3, 8+4g..8+4g+3 of
+//   each 16), and V's rows are read in that same order. O^T's lane also owns one query row, so
+//   the online-softmax rescale is a per-lane scalar;
+// * K/V tiles (64 keys) are register-staged: the next tile's global loads are issued before the
+//   current tile's MFMAs and written to LDS after them (one LDS buffer, two barriers per tile).
+//   Every LDS tile uses one XOR chunk swizzle (uswz) that is conflict-free for both the b128 row
+//   reads and the transposed reads, so a tile is staged once whichever way it is read;
+// * softmax in the exp2 domain (scale·log2 e folded in, v_exp_f32), LSE = m + log2(l) saved.
+//
+// Backward: preprocess delta = rowsum(dO·O); dK/dV kernel (one workgroup = 128 keys of one
+// (batch, kv head), two 4-wave groups splitting the (query head, 32-row query tile) items of the
+// GQA group and causal mask, LDS-DMA double-buffered Q / dO tiles; S = Q·K^T and dP = dO·V^T
+// with the KEY on the lane, so P and dS are directly the B operands of dV^T += dO^T·P and
+// dK^T += Q^T·dS); dQ kernel (8 waves x 32 query rows; S^T and dP^T with the query on the lane,
+// dQ^T += K^T·dS^T). No atomics: dQ and dK/dV are separate passes (S and dP are recomputed in
+// both), each bitwise reproducible.
+//
+// MI355X, Llama-3-8B shape (B1 S4096 H32/8 D128 causal): fwd 0.358 ms, fwd+bwd 1.434 ms vs torch
+// SDPA (AOTriton) 0.421 / 2.272 ms; ViT-L/16 (B64 S197 H16 D64): 0.038 / 0.278 vs 0.061 / 0.349 ms
+// (profiles/r2_flash_attn.txt).
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include "common.h"
+#include "kernels/dev_utils.h"
+
+namespace xddp {
+namespace kernels {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+using dev::u32x4;
+
+constexpr int kBK = 64;   // keys per K/V tile
+constexpr float kNegInf = -1e30f;
+
+__device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
+
+// 16-B chunk XOR swizzle of a row-major [rows][D] LDS tile, conflict-free for BOTH read patterns
+// used on it: ds_read_b128 row fragments (16 consecutive rows at one chunk) and ds_read_b64_tr_b16
+// transposed fragments (4 consecutive rows x 4 consecutive chunks per half-wave). So a tile is
+// staged once and read both ways (the dQ / dK,dV GEMMs read the same Q, dO, K tiles transposed).
+template <int D>
+__device__ __forceinline__ int uswz(int row, int chunk) {
+  return chunk ^ (D == 128 ? (4 * (row & 3) | ((row >> 2) & 3)) : (4 * ((row >> 1) & 1) | ((row >> 2) & 3)));
+}
+
+// keys (or queries) held by lane group g (= lane >> 5) in element e (0..7) of a 16-wide k-step
+// of a 32x32 accumulator: 4g + (e & 3) + 8 (e >> 2)
+__device__ __forceinline__ int kappa(int g, int e) { return 4 * g + (e & 3) + 8 * (e >> 2); }
+
+struct Strides {
+  int64_t b, s, h;
+};
+
+// A fragment of a row-major tile in LDS: rows r0 + (lane & 31), 8 elements from column 16 ks + 8 (lane >> 5)
+template <int D>
+__device__ __forceinline__ bf16x8 ld_rowfrag(const uint8_t* T, int r, int ks, int lane) {
+  const int chunk = 2 * ks + (lane >> 5);
+  return *reinterpret_cast<const bf16x8*>(T + r * (D * 2) + uswz<D>(r, chunk) * 16);
+}
+
+// transposed fragment: element e of lane l = T[rows rbase + kappa(g, e)][col cbase + (l & 31)]
+template <int D>
+__device__ __forceinline__ bf16x8 ld_trfrag(const uint8_t* T, int rbase, int cbase, int lane) {
+  const int g = lane >> 5, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const int col = cbase + 16 * ((lane >> 4) & 1) + 4 * p4;  // 4 bf16 = 8 B per lane
+  const int r0 = rbase + 4 * g + q4, r1 = r0 + 8;
+  const int c0 = col >> 3, off = (col & 7) * 2;
+  const v4s lo = lds_tr16(T + r0 * (D * 2) + uswz<D>(r0, c0) * 16 + off);
+  const v4s hi = lds_tr16(T + r1 * (D * 2) + uswz<D>(r1, c0) * 16 + off);
+  const v4s v8[2] = {lo, hi};
+  return __builtin_bit_cast(bf16x8, v8);
+}
+
+// register-staged tile load: rows [r0, r0 + 64) of a [B, S, H, D] tensor (zero past `rows`)
+template <int D, int NTH = 256>
+struct TileRegs {
+  static constexpr int CH = kBK * D / 8 / NTH;  // 16-B chunks per thread
+  u32x4 v[CH];
+  __device__ void load(const uint16_t* base, int64_t ss, int r0, int rows, int tid) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int q = tid + NTH * i, r = q / (D / 8), c = q % (D / 8);
+      v[i] = (r0 + r < rows) ? *reinterpret_cast<const u32x4*>(base + (int64_t)(r0 + r) * ss + c * 8)
+                             : u32x4{0, 0, 0, 0};
+    }
+  }
+  __device__ void store(uint8_t* T, int tid) const {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int q = tid + NTH * i, r = q / (D / 8), c = q % (D / 8);
+      *reinterpret_cast<u32x4*>(T + r * (D * 2) + uswz<D>(r, c) * 16) = v[i];
+    }
+  }
+};
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// ------------------------------------------------------------------------------------------ fwd
+// NW waves x 32 query rows per workgroup. At NW = 8 two waves share each SIMD, so one wave's
+// softmax, LDS reads and global-load waits overlap the other's MFMAs (at 4 waves, one per SIMD,
+// the kernel ran ~12K cycles per K/V tile against ~1K of MFMA work).
+template <int D, bool CAUSAL, int NW>
+__global__ __launch_bounds__(64 * NW) void fa_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+                                                        const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
+                                                        float* __restrict__ LSE, int Sq, int Sk, int Hq, int Hkv,
+                                                        Strides qs, Strides ks, Strides vs, Strides os,
+                                                        float scale_log2) {
+  constexpr int QPW = 1, KS = D / 16, NT = D / 32, BQ = 32 * NW;
+  __shared__ __attribute__((aligned(16))) uint8_t Kt[kBK * D * 2];
+  __shared__ __attribute__((aligned(16))) uint8_t Vt[kBK * D * 2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 5;
+  const int bh = blockIdx.y, b = bh / Hq, h = bh % Hq, hk = h / (Hq / Hkv);
+  const int nqb = gridDim.x;
+  const int qb = CAUSAL ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;  // heaviest causal blocks first
+  const int q0 = qb * BQ, qw = q0 + 32 * w;                             // wave rows [qw, qw + 32)
+  const uint16_t* Qb = Q + b * qs.b + h * qs.h;
+  const uint16_t* Kb = K + b * ks.b + hk * ks.h;
+  const uint16_t* Vb = V + b * vs.b + hk * vs.h;
+
+  int qrow[QPW];
+  bf16x8 qf[QPW][KS];
+  f32x16 acc_o[QPW][NT];
+  float m_run[QPW], l_run[QPW];
+#pragma unroll
+  for (int u = 0; u < QPW; ++u) {
+    qrow[u] = qw + 32 * u + (lane & 31);
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      qf[u][s] = qrow[u] < Sq ? *reinterpret_cast<const bf16x8*>(Qb + (int64_t)qrow[u] * qs.s + 16 * s + 8 * g)
+                              : bf16x8{};
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc_o[u][n][i] = 0.f;
+    m_run[u] = kNegInf;
+    l_run[u] = 0.f;
+  }
+
+  const int kend = CAUSAL ? min(Sk, q0 + BQ) : Sk;
+  const int ntiles = (kend + kBK - 1) / kBK;
+  TileRegs<D, 64 * NW> kr, vr;
+  kr.load(Kb, ks.s, 0, Sk, tid);
+  vr.load(Vb, vs.s, 0, Sk, tid);
+  for (int j = 0; j < ntiles; ++j) {
+    const int k0 = j * kBK;
+    kr.store(Kt, tid);
+    vr.store(Vt, tid);
+    lds_barrier();
+    if (j + 1 < ntiles) {  // next tile in flight during this tile's math
+      kr.load(Kb, ks.s, k0 + kBK, Sk, tid);
+      vr.load(Vb, vs.s, k0 + kBK, Sk, tid);
+    }
+    if (!CAUSAL || k0 <= qw + 32 * QPW - 1) {  // a wave whose rows all precede the tile skips it
+      f32x16 sc[QPW][2];
+#pragma unroll
+      for (int u = 0; u < QPW; ++u)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) sc[u][t][i] = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const bf16x8 kfr = ld_rowfrag<D>(Kt, 32 * t + (lane & 31), s, lane);
+#pragma unroll
+          for (int u = 0; u < QPW; ++u) sc[u][t] = mfma32(kfr, qf[u][s], sc[u][t]);
+        }
+      bf16x8 pf[QPW][4];
+#pragma unroll
+      for (int u = 0; u < QPW; ++u) {
+        // scale, mask, row max (in-lane over 32 keys, then lane ^ 32)
+        float mx = kNegInf;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = k0 + 32 * t + kappa(g, i & 7) + 16 * (i >> 3);
+            float v = sc[u][t][i] * scale_log2;
+            if (key >= Sk || (CAUSAL && key > qrow[u])) v = kNegInf;
+            sc[u][t][i] = v;
+            mx = fmaxf(mx, v);
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_run[u], mx);
+        const float alpha = __builtin_amdgcn_exp2f(m_run[u] - m_new);
+        float ls = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float p = __builtin_amdgcn_exp2f(sc[u][t][i] - m_new);
+            sc[u][t][i] = p;
+            ls += p;
+          }
+        l_run[u] = l_run[u] * alpha + ls;
+        m_run[u] = m_new;
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc_o[u][n][i] *= alpha;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int t = kk >> 1, hh = kk & 1;
+          uint32_t pk[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            pk[e] = dev::pack_bf16x2(sc[u][t][8 * hh + 2 * e], sc[u][t][8 * hh + 2 * e + 1]);
+          pf[u][kk] = __builtin_bit_cast(bf16x8, pk);
+        }
+      }
+      // O^T += V^T P^T over the 4 16-key steps of the tile; one V fragment for all QPW blocks
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const bf16x8 vfr = ld_trfrag<D>(Vt, 16 * kk, 32 * n, lane);
+#pragma unroll
+          for (int u = 0; u < QPW; ++u) acc_o[u][n] = mfma32(vfr, pf[u][kk], acc_o[u][n]);
+        }
+    }
+    lds_barrier();  // every wave is done with this tile before it is overwritten
+  }
+#pragma unroll
+  for (int u = 0; u < QPW; ++u) {
+    const float l_tot = l_run[u] + __shfl_xor(l_run[u], 32, 64);
+    if (qrow[u] < Sq) {
+      const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+      uint16_t* Ob = O + b * os.b + h * os.h + (int64_t)qrow[u] * os.s;
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // 4 consecutive d per store: d = 32n + 4g + 8q + 0..3
+          uint2 pk;
+          pk.x = dev::pack_bf16x2(acc_o[u][n][4 * q] * inv, acc_o[u][n][4 * q + 1] * inv);
+          pk.y = dev::pack_bf16x2(acc_o[u][n][4 * q + 2] * inv, acc_o[u][n][4 * q + 3] * inv);
+          *reinterpret_cast<uint2*>(Ob + 32 * n + 4 * g + 8 * q) = pk;
+        }
+      if (g == 0) LSE[(int64_t)bh * Sq + qrow[u]] = m_run[u] + log2f(fmaxf(l_tot, 1e-30f));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ bwd
+// delta[bh][q] = sum_d dO[q][d] · O[q][d] (fp32), one wave per query row
+template <int D>
+__global__ __launch_bounds__(256) void fa_bwd_pre_kernel(const uint16_t* __restrict__ O, const uint16_t* __restrict__ dO,
+                                                         float* __restrict__ delta, int Sq, int Hq, Strides os,
+                                                         Strides dos) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // over B*Hq*Sq (a multiple of 4)
+  const int q = (int)(row % Sq);
+  const int64_t bh = row / Sq;
+  const int b = (int)(bh / Hq), h = (int)(bh % Hq);
+  float s = 0.f;
+  if (lane * 2 < D) {
+    const uint32_t ov = *reinterpret_cast<const uint32_t*>(O + b * os.b + h * os.h + (int64_t)q * os.s + 2 * lane);
+    const uint32_t dv = *reinterpret_cast<const uint32_t*>(dO + b * dos.b + h * dos.h + (int64_t)q * dos.s + 2 * lane);
+    s = bf2f(ov & 0xffff) * bf2f(dv & 0xffff) + bf2f(ov >> 16) * bf2f(dv >> 16);
+  }
+  s = dev::wave_sum(s);
+  if (lane == 0) delta[row] = s;
+}
+
+// dQ: one workgroup = NW waves x 32 query rows of one (batch, q head); S^T and dP^T with the
+// query on the lane (as the forward), dQ^T += K^T · dS^T. NW = 8 pairs two waves per SIMD.
+template <int D, bool CAUSAL, int NW>
+__global__ __launch_bounds__(64 * NW) void fa_bwd_dq_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
+    uint16_t* __restrict__ dQ, int Sq, int Sk, int Hq, int Hkv, Strides qs, Strides ks, Strides vs, Strides dos,
+    Strides dqs, float scale_log2, float scale) {
+  constexpr int QPW = 1, KS = D / 16, NT = D / 32, BQ = 32 * NW;
+  __shared__ __attribute__((aligned(16))) uint8_t Kt[kBK * D * 2];  // row reads (S^T), transposed reads (dQ)
+  __shared__ __attribute__((aligned(16))) uint8_t Vt[kBK * D * 2];  // row reads (dP^T)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 5;
+  const int bh = blockIdx.y, b = bh / Hq, h = bh % Hq, hk = h / (Hq / Hkv);
+  const int qb = CAUSAL ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int q0 = qb * BQ, qw = q0 + 32 * w;
+  const uint16_t* Kb = K + b * ks.b + hk * ks.h;
+  const uint16_t* Vb = V + b * vs.b + hk * vs.h;
+  int qrow[QPW];
+  bf16x8 qf[QPW][KS], dof[QPW][KS];
+  float lse[QPW], dl[QPW];
+  f32x16 acc[QPW][NT];
+#pragma unroll
+  for (int u = 0; u < QPW; ++u) {
+    qrow[u] = qw + 32 * u + (lane & 31);
+    const bool ok = qrow[u] < Sq;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      qf[u][s] = ok ? *reinterpret_cast<const bf16x8*>(Q + b * qs.b + h * qs.h + (int64_t)qrow[u] * qs.s + 16 * s + 8 * g)
+                    : bf16x8{};
+      dof[u][s] = ok ? *reinterpret_cast<const bf16x8*>(dO + b * dos.b + h * dos.h + (int64_t)qrow[u] * dos.s + 16 * s +
+                                                        8 * g)
+                     : bf16x8{};
+    }
+    lse[u] = ok ? LSE[(int64_t)bh * Sq + qrow[u]] : 0.f;
+    dl[u] = ok ? delta[(int64_t)bh * Sq + qrow[u]] : 0.f;
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[u][n][i] = 0.f;
+  }
+  const int kend = CAUSAL ? min(Sk, q0 + BQ) : Sk;
+  const int ntiles = (kend + kBK - 1) / kBK;
+  TileRegs<D, 64 * NW> kr, vr;
+  kr.load(Kb, ks.s, 0, Sk, tid);
+  vr.load(Vb, vs.s, 0, Sk, tid);
+  for (int j = 0; j < ntiles; ++j) {
+    const int k0 = j * kBK;
+    kr.store(Kt, tid);
+    vr.store(Vt, tid);
+    lds_barrier();
+    if (j + 1 < ntiles) {
+      kr.load(Kb, ks.s, k0 + kBK, Sk, tid);
+      vr.load(Vb, vs.s, k0 + kBK, Sk, tid);
+    }
+    if (!CAUSAL || k0 <= qw + 31) {
+      // one 32-key half at a time keeps S^T / dP^T at 32 live registers
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x16 sc[QPW], dp[QPW];
+#pragma unroll
+        for (int u = 0; u < QPW; ++u)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) sc[u][i] = dp[u][i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const bf16x8 kfr = ld_rowfrag<D>(Kt, 32 * t + (lane & 31), s, lane);
+          const bf16x8 vfr = ld_rowfrag<D>(Vt, 32 * t + (lane & 31), s, lane);
+#pragma unroll
+          for (int u = 0; u < QPW; ++u) {
+            sc[u] = mfma32(kfr, qf[u][s], sc[u]);
+            dp[u] = mfma32(vfr, dof[u][s], dp[u]);
+          }
+        }
+        // dS^T = P^T (dP^T - delta), P^T = exp2(S^T c - lse); the softmax scale of dS folds into the end
+        bf16x8 sf[QPW][2];
+#pragma unroll
+        for (int u = 0; u < QPW; ++u) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = k0 + 32 * t + kappa(g, i & 7) + 16 * (i >> 3);
+            float p = __builtin_amdgcn_exp2f(sc[u][i] * scale_log2 - lse[u]);
+            if (key >= Sk || (CAUSAL && key > qrow[u])) p = 0.f;
+            sc[u][i] = p * (dp[u][i] - dl[u]);
+          }
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            uint32_t pk[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pk[e] = dev::pack_bf16x2(sc[u][8 * hh + 2 * e], sc[u][8 * hh + 2 * e + 1]);
+            sf[u][hh] = __builtin_bit_cast(bf16x8, pk);
+          }
+        }
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int n = 0; n < NT; ++n) {
+            const bf16x8 kt = ld_trfrag<D>(Kt, 32 * t + 16 * hh, 32 * n, lane);
+#pragma unroll
+            for (int u = 0; u < QPW; ++u) acc[u][n] = mfma32(kt, sf[u][hh], acc[u][n]);
+          }
+      }
+    }
+    lds_barrier();
+  }
+#pragma unroll
+  for (int u = 0; u < QPW; ++u) {
+    if (qrow[u] >= Sq) continue;
+    uint16_t* out = dQ + b * dqs.b + h * dqs.h + (int64_t)qrow[u] * dqs.s;
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint2 pk;
+        pk.x = dev::pack_bf16x2(acc[u][n][4 * q] * scale, acc[u][n][4 * q + 1] * scale);
+        pk.y = dev::pack_bf16x2(acc[u][n][4 * q + 2] * scale, acc[u][n][4 * q + 3] * scale);
+        *reinterpret_cast<uint2*>(out + 32 * n + 4 * g + 8 * q) = pk;
+      }
+  }
+}
+
+// dK, dV: one workgroup = 128 keys of one (batch, kv head), 8 waves in two groups of 4. Wave
+// (group G, index wq) owns keys k0 + 32 wq .. +31; the groups split the (query head of the GQA
+// group, 32-row query tile) work items (G takes items G, G + 2, ...), so two waves share each
+// SIMD, and sum their dK^T / dV^T accumulators through LDS at the end. Per item: S = Q·K^T and
+// dP = dO·V^T with the KEY on the lane (K fragments in registers, the V block in LDS), then
+// dV^T += dO^T·P and dK^T += Q^T·dS with P / dS as the B operands straight from their
+// accumulators. Q / dO / lse / delta tiles go global -> LDS by LDS-DMA (no VGPR staging), two
+// stages per group: item k + 1 is in flight while item k is computed; one barrier per item.
+// Registers: K 32 + dK^T 64 + dV^T 64 + S, dP 32 (D = 128) stay under the 256 of two waves/SIMD.
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
+    uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq, int Sk, int Hq, int Hkv, Strides qs, Strides ks,
+    Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale) {
+  constexpr int KS = D / 16, NT = D / 32, QB = 32;  // query rows per work item
+  constexpr int TILE = QB * D * 2;                  // bytes of one Q (or dO) tile
+  constexpr int STAGE = 2 * TILE + 2 * QB * 4;      // Q, dO, lse, delta
+  constexpr int VBLK = 128 * D * 2;                 // the workgroup's V rows
+  constexpr int RPI = 512 / D, NI = QB / RPI / 4;   // rows per 1-KB DMA instruction; instructions per wave
+  constexpr int RED = 4 * NT * 16 * 64 * 4;         // one accumulator set of group 1
+  static_assert(RED <= VBLK + 4 * STAGE, "group reduction must fit the LDS");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[VBLK + 4 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wq = w & 3, G = w >> 2, g = lane >> 5;
+  const int bhk = blockIdx.y, b = bhk / Hkv, hk = bhk % Hkv, grp = Hq / Hkv;
+  const int kb = CAUSAL ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int k0 = kb * 128, kw = k0 + 32 * wq, krow = kw + (lane & 31);
+  uint8_t* Vblk = smem;
+  {  // V rows [k0, k0 + 128) -> LDS (rows past Sk read row Sk - 1; their P, dS are masked to 0)
+    constexpr int VI = 128 / RPI / 8;
+    const uint16_t* Vb = V + b * vs.b + hk * vs.h;
+#pragma unroll
+    for (int i = 0; i < VI; ++i) {
+      const int ins = w * VI + i, r = ins * RPI + lane / (D / 8);
+      const int c = uswz<D>(r, lane % (D / 8));
+      const int64_t row = min(k0 + r, Sk - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Vb + row * vs.s + c * 8), (lds_ptr_t)(Vblk + ins * 1024), 16, 0,
+                                       0);
+    }
+  }
+  bf16x8 kf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+    kf[s] = krow < Sk ? *reinterpret_cast<const bf16x8*>(K + b * ks.b + hk * ks.h + (int64_t)krow * ks.s + 16 * s + 8 * g)
+                      : bf16x8{};
+  f32x16 adk[NT], adv[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) adk[n][i] = adv[n][i] = 0.f;
+  const int qstart = CAUSAL ? (k0 / QB) * QB : 0;
+  const int nqt = (Sq - qstart + QB - 1) / QB;
+  const int total = grp * nqt, niter = (total + 1) / 2;
+  uint8_t* gsm = smem + VBLK + G * 2 * STAGE;
+  auto issue = [&](int it, int st) {  // rows past Sq read row Sq - 1 (masked below)
+    const int h = hk * grp + it / nqt, qt0 = qstart + (it % nqt) * QB;
+    uint8_t* S = gsm + st * STAGE;
+    const uint16_t* Qb = Q + b * qs.b + h * qs.h;
+    const uint16_t* Db = dO + b * dos.b + h * dos.h;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int ins = wq * NI + i, r = ins * RPI + lane / (D / 8);
+      const int c = uswz<D>(r, lane % (D / 8));  // the logical chunk that lands at this lane's slot
+      const int64_t row = min(qt0 + r, Sq - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Qb + row * qs.s + c * 8), (lds_ptr_t)(S + ins * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(Db + row * dos.s + c * 8), (lds_ptr_t)(S + TILE + ins * 1024), 16,
+                                       0, 0);
+    }
+    if (wq < 2) {  // 32 lse / delta values: lanes 32..63 duplicate the last row (harmless, in bounds)
+      const float* src = (wq == 0 ? LSE : delta) + ((int64_t)b * Hq + h) * Sq + min(qt0 + (lane & 31), Sq - 1);
+      if (lane < 32)
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(S + 2 * TILE + wq * QB * 4), 4, 0, 0);
+    }
+  };
+  if (G < total) issue(G, 0);
+  for (int k = 0; k < niter; ++k) {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int it = G + 2 * k;
+    if (it + 2 < total) issue(it + 2, (k + 1) & 1);  // into the stage item k - 1 was computed from
+    const int qt0 = qstart + (it % nqt) * QB;
+    if (it < total && (!CAUSAL || qt0 + QB - 1 >= kw)) {
+      const uint8_t* Qt = gsm + (k & 1) * STAGE;
+      const uint8_t* Dt = Qt + TILE;
+      const float* lse_s = reinterpret_cast<const float*>(Qt + 2 * TILE);
+      const float* dl_s = lse_s + QB;
+      f32x16 sc, dp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sc[i] = dp[i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        sc = mfma32(ld_rowfrag<D>(Qt, lane & 31, s, lane), kf[s], sc);
+        dp = mfma32(ld_rowfrag<D>(Dt, lane & 31, s, lane), ld_rowfrag<D>(Vblk, 32 * wq + (lane & 31), s, lane), dp);
+      }
+      // element i: query qt0 + kappa(g, i&7) + 16(i>>3), key krow
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int ql = kappa(g, i & 7) + 16 * (i >> 3);
+        const int q = qt0 + ql;
+        float p = __builtin_amdgcn_exp2f(sc[i] * scale_log2 - lse_s[ql]);
+        if (q >= Sq || krow >= Sk || (CAUSAL && krow > q)) p = 0.f;
+        sc[i] = p;
+        dp[i] = p * (dp[i] - dl_s[ql]);
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        uint32_t pk[4], dk4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pk[e] = dev::pack_bf16x2(sc[8 * hh + 2 * e], sc[8 * hh + 2 * e + 1]);
+          dk4[e] = dev::pack_bf16x2(dp[8 * hh + 2 * e], dp[8 * hh + 2 * e + 1]);
+        }
+        const bf16x8 pf = __builtin_bit_cast(bf16x8, pk), sf = __builtin_bit_cast(bf16x8, dk4);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          adv[n] = mfma32(ld_trfrag<D>(Dt, 16 * hh, 32 * n, lane), pf, adv[n]);
+          adk[n] = mfma32(ld_trfrag<D>(Qt, 16 * hh, 32 * n, lane), sf, adk[n]);
+        }
+      }
+    }
+  }
+  // group 1 hands its partial dK^T, then dV^T, to group 0 through the (now idle) LDS
+  float* red = reinterpret_cast<float*>(smem) + wq * (NT * 16 * 64) + lane;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    f32x16* acc = pass == 0 ? adk : adv;
+    if (G == 1) {
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[(n * 16 + i) * 64] = acc[n][i];
+    }
+    __syncthreads();
+    if (G == 0) {
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[n][i] += red[(n * 16 + i) * 64];
+    }
+  }
+  if (G == 1 || krow >= Sk) return;
+  uint16_t* ok = dK + b * dks.b + hk * dks.h + (int64_t)krow * dks.s;
+  uint16_t* ov = dV + b * dvs.b + hk * dvs.h + (int64_t)krow * dvs.s;
+#pragma unroll
+  for (int n = 0; n < NT; ++n)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint2 a, c;
+      a.x = dev::pack_bf16x2(adk[n][4 * q] * scale, adk[n][4 * q + 1] * scale);
+      a.y = dev::pack_bf16x2(adk[n][4 * q + 2] * scale, adk[n][4 * q + 3] * scale);
+      c.x = dev::pack_bf16x2(adv[n][4 * q], adv[n][4 * q + 1]);
+      c.y = dev::pack_bf16x2(adv[n][4 * q + 2], adv[n][4 * q + 3]);
+      *reinterpret_cast<uint2*>(ok + 32 * n + 4 * g + 8 * q) = a;
+      *reinterpret_cast<uint2*>(ov + 32 * n + 4 * g + 8 * q) = c;
+    }
+}
+
+Strides strides_of(const at::Tensor& t) { return Strides{t.stride(0), t.stride(1), t.stride(2)}; }
+
+void check_bshd(const at::Tensor& t, const char* name, int64_t D) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4, "flash_attn: ", name,
+              " must be a bf16 [B, S, H, D] GPU tensor");
+  TORCH_CHECK(t.size(3) == D && t.stride(3) == 1, "flash_attn: ", name, " must have a contiguous last dim of ", D);
+  TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              "flash_attn: ", name, " needs 16-B aligned rows");
+}
+
+}  // namespace
+
+// q [B, Sq, Hq, D], k / v [B, Sk, Hkv, D] -> (o [B, Sq, Hq, D], lse [B, Hq, Sq] fp32, log2 domain)
+std::vector<at::Tensor> flash_attn_forward(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, bool causal,
+                                           double scale) {
+  const int64_t D = q.size(3);
+  TORCH_CHECK(D == 64 || D == 128, "flash_attn: head dim 64 or 128");
+  check_bshd(q, "q", D);
+  check_bshd(k, "k", D);
+  check_bshd(v, "v", D);
+  const int64_t B = q.size(0), Sq = q.size(1), Hq = q.size(2), Sk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(k.sizes() == v.sizes() && k.size(0) == B && Hq % Hkv == 0, "flash_attn: q/k/v shape mismatch");
+  TORCH_CHECK(!causal || Sq == Sk, "flash_attn: causal needs Sq == Sk");
+  TORCH_CHECK(Sq > 0 && Sk > 0 && B * Hq < 65536 && Sq < (1 << 30), "flash_attn: bad size");
+  auto o = at::empty({B, Sq, Hq, D}, q.options());
+  auto lse = at::empty({B, Hq, Sq}, q.options().dtype(at::kFloat));
+  auto stream = c10::hip::getCurrentHIPStream(q.device().index()).stream();
+  // 8 waves (256 query rows) per workgroup; 4 when 256-row blocks would leave CUs idle
+  static const int nw_env = [] {
+    const char* e = std::getenv("XDDP_FA_WAVES");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int64_t wg8 = ((Sq + 255) / 256) * B * Hq;
+  const int nw = nw_env == 4 || nw_env == 8 ? nw_env : (wg8 >= 256 ? 8 : 4);
+  const dim3 grid((unsigned)((Sq + 32 * nw - 1) / (32 * nw)), (unsigned)(B * Hq));
+  const float sl2 = (float)(scale * 1.4426950408889634);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, reinterpret_cast<const uint16_t*>(q.data_ptr()),
+                       reinterpret_cast<const uint16_t*>(k.data_ptr()), reinterpret_cast<const uint16_t*>(v.data_ptr()),
+                       reinterpret_cast<uint16_t*>(o.data_ptr()), lse.data_ptr<float>(), (int)Sq, (int)Sk, (int)Hq,
+                       (int)Hkv, strides_of(q), strides_of(k), strides_of(v), strides_of(o), sl2);
+    XDDP_HIP_CHECK(hipGetLastError());
+  };
+#define XDDP_FA(D_, C_) \
+  if (nw == 8) go(fa_fwd_kernel<D_, C_, 8>); else go(fa_fwd_kernel<D_, C_, 4>)
+  if (D == 128) { if (causal) { XDDP_FA(128, true); } else { XDDP_FA(128, false); } }
+  else { if (causal) { XDDP_FA(64, true); } else { XDDP_FA(64, false); } }
+#undef XDDP_FA
+  return {o, lse};
+}
+
+// -> (dq, dk, dv) in the layouts of q, k, v ([B, S, H, D] contiguous)
+std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
+                                            const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse,
+                                            bool causal, double scale) {
+  const int64_t D = q.size(3);
+  TORCH_CHECK(D == 64 || D == 128, "flash_attn: head dim 64 or 128");
+  check_bshd(q, "q", D);
+  check_bshd(k, "k", D);
+  check_bshd(v, "v", D);
+  check_bshd(o, "o", D);
+  check_bshd(dout, "dout", D);
+  const int64_t B = q.size(0), Sq = q.size(1), Hq = q.size(2), Sk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && lse.is_contiguous() &&
+                  lse.numel() == B * Hq * Sq && lse.scalar_type() == at::kFloat,
+              "flash_attn backward: shape mismatch");
+  auto dq = at::empty({B, Sq, Hq, D}, q.options());
+  auto dk = at::empty({B, Sk, Hkv, D}, k.options());
+  auto dv = at::empty({B, Sk, Hkv, D}, v.options());
+  auto delta = at::empty({B, Hq, Sq}, q.options().dtype(at::kFloat));
+  auto stream = c10::hip::getCurrentHIPStream(q.device().index()).stream();
+  const int64_t rows = B * Hq * Sq;
+  {  // delta: one wave per query row
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
+                         reinterpret_cast<const uint16_t*>(o.data_ptr()),
+                         reinterpret_cast<const uint16_t*>(dout.data_ptr()), delta.data_ptr<float>(), (int)Sq, (int)Hq,
+                         strides_of(o), strides_of(dout));
+      XDDP_HIP_CHECK(hipGetLastError());
+    };
+    TORCH_CHECK(rows % 4 == 0, "flash_attn backward: B*H*S must be a multiple of 4");
+    if (D == 128) go(fa_bwd_pre_kernel<128>); else go(fa_bwd_pre_kernel<64>);
+  }
+  const float sl2 = (float)(scale * 1.4426950408889634), sc = (float)scale;
+  {
+    static const int nw_env = [] {
+      const char* e = std::getenv("XDDP_FA_WAVES");
+      return e ? std::atoi(e) : 0;
+    }();
+    const int64_t wg8 = ((Sq + 255) / 256) * B * Hq;
+    const int nw = nw_env == 4 || nw_env == 8 ? nw_env : (wg8 >= 256 ? 8 : 4);
+    const dim3 grid((unsigned)((Sq + 32 * nw - 1) / (32 * nw)), (unsigned)(B * Hq));
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, reinterpret_cast<const uint16_t*>(q.data_ptr()),
+                         reinterpret_cast<const uint16_t*>(k.data_ptr()), reinterpret_cast<const uint16_t*>(v.data_ptr()),
+                         reinterpret_cast<const uint16_t*>(dout.data_ptr()), lse.data_ptr<float>(),
+                         delta.data_ptr<float>(), reinterpret_cast<uint16_t*>(dq.data_ptr()), (int)Sq, (int)Sk,
+                         (int)Hq, (int)Hkv, strides_of(q), strides_of(k), strides_of(v), strides_of(dout),
+                         strides_of(dq), sl2, sc);
+      XDDP_HIP_CHECK(hipGetLastError());
+    };
+#define XDDP_FA(D_, C_) \
+  if (nw == 8) go(fa_bwd_dq_kernel<D_, C_, 8>); else go(fa_bwd_dq_kernel<D_, C_, 4>)
+    if (D == 128) { if (causal) { XDDP_FA(128, true); } else { XDDP_FA(128, false); } }
+    else { if (causal) { XDDP_FA(64, true); } else { XDDP_FA(64, false); } }
+#undef XDDP_FA
+  }
+  {
+    const dim3 grid((unsigned)((Sk + 127) / 128), (unsigned)(B * Hkv));
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, grid, dim3(512), 0, stream, reinterpret_cast<const uint16_t*>(q.data_ptr()),
+                         reinterpret_cast<const uint16_t*>(k.data_ptr()), reinterpret_cast<const uint16_t*>(v.data_ptr()),
+                         reinterpret_cast<const uint16_t*>(dout.data_ptr()), lse.data_ptr<float>(),
+                         delta.data_ptr<float>(), reinterpret_cast<uint16_t*>(dk.data_ptr()),
+                         reinterpret_cast<uint16_t*>(dv.data_ptr()), (int)Sq, (int)Sk, (int)Hq, (int)Hkv, strides_of(q),
+                         strides_of(k), strides_of(v), strides_of(dout), strides_of(dk), strides_of(dv), sl2, sc);
+      XDDP_HIP_CHECK(hipGetLastError());
+    };
+    if (D == 128) { if (causal) go(fa_bwd_dkdv_kernel<128, true>); else go(fa_bwd_dkdv_kernel<128, false>); }
+    else { if (causal) go(fa_bwd_dkdv_kernel<64, true>); else go(fa_bwd_dkdv_kernel<64, false>); }
+  }
+  return {dq, dk, dv};
+}
+
+}  // namespace kernels
+}  // namespace xddp

@@ -42,7 +42,8 @@ std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w
 at::Tensor conv3x3_rot_weight(const at::Tensor& w);
 at::Tensor conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like);
 // 3x3 weight gradient over 8x8 output patches with a shared X halo (csrc/kernels/conv3x3_wgrad.hip)
-at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like);
+at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,
+                               int64_t splits = -1);
 at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,
                          const c10::optional<at::Tensor>& prologue_y, const c10::optional<at::Tensor>& coef);
 std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M,
@@ -66,6 +67,13 @@ at::Tensor maxpool_backward(const at::Tensor& dy, const at::Tensor& idx, const a
 at::Tensor rope(const at::Tensor& x, const at::Tensor& cosv, const at::Tensor& sinv, bool backward);
 at::Tensor swiglu_forward(const at::Tensor& a, const at::Tensor& b);
 std::vector<at::Tensor> swiglu_backward(const at::Tensor& g, const at::Tensor& a, const at::Tensor& b);
+
+// flash attention, [B, S, H, D] bf16 (csrc/kernels/flash_attn.hip)
+std::vector<at::Tensor> flash_attn_forward(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, bool causal,
+                                           double scale);
+std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
+                                            const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse,
+                                            bool causal, double scale);
 
 void bind_norm_kernels(pybind11::module_& m);
 

@@ -26,12 +26,17 @@ void bind_norm_kernels(py::module_& m) {
   m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"));
   m.def("conv3x3_rot_weight", &conv3x3_rot_weight, py::arg("w"));
   m.def("conv3x3_wgrad", &conv3x3_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"));
-  m.def("conv3x3_wgrad_patch", &conv3x3_wgrad_patch, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"));
+  m.def("conv3x3_wgrad_patch", &conv3x3_wgrad_patch, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"),
+        py::arg("splits") = -1);
   m.def("conv1x1_wgrad", &conv1x1_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"),
         py::arg("prologue_y") = py::none(), py::arg("coef") = py::none());
   m.def("bn_stats_from_partials", &bn_stats_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"),
         py::arg("momentum"), py::arg("cumulative"), py::arg("eps"), py::arg("group_minor") = false);
+  m.def("flash_attn_forward", &flash_attn_forward, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
+        py::arg("scale"));
+  m.def("flash_attn_backward", &flash_attn_backward, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
+        py::arg("o"), py::arg("lse"), py::arg("causal"), py::arg("scale"));
   m.def("rope", &rope, py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("backward") = false);
   m.def("swiglu_forward", &swiglu_forward, py::arg("a"), py::arg("b"));
   m.def("swiglu_backward", &swiglu_backward, py::arg("grad"), py::arg("a"), py::arg("b"));

@@ -1,9 +1,8 @@
 """Llama-3 decoder (8B config) — BASELINE.json config 5 (Llama-3-8B bf16 pure DDP).
 
 RMSNorm on xddp's fused kernel, rotary embeddings and the SwiGLU gate on fused HIP kernels
-(``ops/transformer.py``: one pass each instead of ~10 / 3 PyTorch ops), grouped-query attention
-through ``F.scaled_dot_product_attention`` (causal; K/V heads are shared by ``enable_gqa`` rather
-than materialised by ``repeat_interleave``). Pure DDP sizing on MI355X: 8.03B
+(``ops/transformer.py``: one pass each instead of ~10 / 3 PyTorch ops), grouped-query causal attention
+on xddp's gfx950 flash-attention kernels (``ops/attention.py``: K/V heads shared, not repeated). Pure DDP sizing on MI355X: 8.03B
 params → 16 GB bf16 params + 16 GB bf16 grads (bucket views) + 96 GB fp32 master/Adam ≈ 128 GB
 of the 288 GB HBM3E, leaving room for activations (optionally checkpointed per layer).
 ``XDDP_FUSED_TRANSFORMER=0`` selects the PyTorch reference ops (A/B and parity tests).
@@ -17,6 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.attention import flash_attention
 from ..ops.layer_norm import FusedRMSNorm
 from ..ops.transformer import rope, rope_reference, swiglu
 
@@ -62,16 +62,20 @@ class Attention(nn.Module):
         B, S, _ = x.shape
         rot = rope if _fused() else rope_reference
         # rotate in the projection's [B, S, H, Dh] layout, then move heads forward for attention
-        q = rot(self.wq(x).view(B, S, self.h, self.hd), cos, sin).transpose(1, 2)
-        k = rot(self.wk(x).view(B, S, self.kvh, self.hd), cos, sin).transpose(1, 2)
-        v = self.wv(x).view(B, S, self.kvh, self.hd).transpose(1, 2)
-        if self.kvh != self.h and not _fused():
+        q = rot(self.wq(x).view(B, S, self.h, self.hd), cos, sin)
+        k = rot(self.wk(x).view(B, S, self.kvh, self.hd), cos, sin)
+        v = self.wv(x).view(B, S, self.kvh, self.hd)
+        if _fused():
+            # gfx950 flash attention in the projections' [B, S, H, Dh] layout (GQA without
+            # materialised K/V repeats; output already in the o-projection's layout)
+            o = flash_attention(q, k, v, causal=True)
+            return self.wo(o.reshape(B, S, -1))
+        q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+        if self.kvh != self.h:
             rep = self.h // self.kvh
             k = k.repeat_interleave(rep, dim=1)
             v = v.repeat_interleave(rep, dim=1)
-            o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-        else:
-            o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=self.kvh != self.h)
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
         return self.wo(o.transpose(1, 2).reshape(B, S, -1))
 
 

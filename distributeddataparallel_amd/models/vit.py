@@ -1,7 +1,7 @@
 """Vision Transformer (ViT-B/16, ViT-L/16, ...) — BASELINE.json config 4 (ViT-L/16 bf16 DDP).
 
-Pre-norm encoder blocks with xddp's fused LayerNorm kernel, attention through
-``F.scaled_dot_product_attention`` (flash path on ROCm), GELU MLP. Random init; the
+Pre-norm encoder blocks with xddp's fused LayerNorm kernel, attention on xddp's gfx950 flash
+attention kernels (``ops/attention.py``; SDPA fallback), GELU MLP, patch embedding as one GEMM. Random init; the
 structure/parameter count matches torchvision's ``vit_l_16`` (304,326,632 params at 1000
 classes).
 """
@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.attention import flash_attention
 from ..ops.layer_norm import FusedLayerNorm
 
 __all__ = ["VisionTransformer", "vit_b_16", "vit_l_16", "vit_tiny"]
@@ -25,9 +26,11 @@ class _Attention(nn.Module):
 
     def forward(self, x):
         B, N, D = x.shape
-        qkv = self.in_proj(x).view(B, N, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
-        o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
-        return self.out_proj(o.transpose(1, 2).reshape(B, N, D))
+        # q/k/v are strided [B, N, H, Dh] views of the fused projection; the flash kernel reads them
+        # in place and writes [B, N, H, Dh], which is already the out-projection's input layout
+        qkv = self.in_proj(x).view(B, N, 3, self.heads, D // self.heads)
+        o = flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2])
+        return self.out_proj(o.reshape(B, N, D))
 
 
 class EncoderBlock(nn.Module):

@@ -186,7 +186,11 @@ def _dgrad_in(ctx, C, g, w, coef, y):
     """Stride-1 input gradient; with a BNReLULink on the input, also the producer's masked BN-backward
     partials (epilogue second form)."""
     li = ctx.link_in
-    if li is None or not _epi() or os.environ.get("XDDP_CONV_EPI2", "1") == "0":
+    # XDDP_CONV_EPI2=1 opts in. Off by default: measured 10,534 vs 10,808 img/s (ResNet-50 bs256,
+    # MI355X) — the masked-reduce epilogue on top of the BN-backward prologue pushes the dgrad GEMM
+    # past its 128-VGPR budget (45 spilled registers at 2 blocks/CU), costing more than BN2's
+    # separate reduce pass.
+    if li is None or not _epi() or os.environ.get("XDDP_CONV_EPI2", "0") != "1":
         return _dgrad(C, g, w, coef, y)
     dx, li.part = C.conv1x1_gemm(g, w, 1, coef, False, y, True, None, li.y, None, li.mean, li.ss)
     li.g = dx
@@ -237,8 +241,11 @@ class _Conv3x3BNReLU(torch.autograd.Function):
         if need_x and s == 1:
             dx = C.conv3x3_forward(dy, C.conv3x3_rot_weight(w), 1, False)[0]
             need_x = False
-        if need_w and _wgrad3():
-            # 8x8 output patches sharing one staged X halo across the 9 taps (conv3x3_wgrad.hip)
+        if need_w and _wgrad3() and (s == 1 or os.environ.get("XDDP_CONV3X3_WGRAD_S2", "0") == "1"):
+            # 8x8 output patches sharing one staged X halo across the 9 taps (conv3x3_wgrad.hip):
+            # 96-98 us vs MIOpen's 120-182 us per stride-1 ResNet-50 shape (bs256); the stride-2
+            # variant (phase-split halo) loses (175-193 vs 120-134 us), MIOpen keeps those
+            # (scripts/wgrad3_bench.py, profiles/r2_wgrad3_bench.txt)
             dw = C.conv3x3_wgrad_patch(dy, x, s, w)
             need_w = False
         if need_x or need_w:
