@@ -366,6 +366,7 @@ class RcclComm : public Comm {
     int64_t last_peer_poll = 0;
     while (!wd_stop_) {
       heartbeat_ = now_ns();
+      bool poll_peers = false;
       {
         std::unique_lock<std::mutex> g(wd_mu_);
         wd_cv_.wait_for(g, std::chrono::milliseconds(100), [&] { return wd_stop_.load(); });
@@ -393,14 +394,19 @@ class RcclComm : public Comm {
         // store whether a peer has already failed
         if (err_->load() == 0 && now - oldest > 1000000000LL && now - last_peer_poll > 1000000000LL) {
           last_peer_poll = now;
-          try {
-            if (store_->check({"rccl/error"})) {
-              reason = "peer error: " + store_->get("rccl/error");
-              std::cerr << "[xddp rank " << rank_ << "] watchdog: " << reason << "; aborting communicator\n";
-              err_->store(3);
-            }
-          } catch (...) {
+          poll_peers = true;
+        }
+      }
+      // the store round trip runs without wd_mu_: collectives launched meanwhile
+      // (finish_launch) must not wait on a slow or vanished store host
+      if (poll_peers) {
+        try {
+          if (store_->check({"rccl/error"})) {
+            reason = "peer error: " + store_->get("rccl/error");
+            std::cerr << "[xddp rank " << rank_ << "] watchdog: " << reason << "; aborting communicator\n";
+            err_->store(3);
           }
+        } catch (...) {
         }
       }
       if (err_->load() == 0 && comm_ && !aborted_ && !destroyed_) {

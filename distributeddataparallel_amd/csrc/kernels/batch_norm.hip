@@ -125,7 +125,9 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
 // One 64-lane wave per 8-channel vector: lanes stride over the row-block partials (4 loads in
 // flight), then a 6-step xor-shuffle butterfly of plain adds — no LDS, no barriers.
 // Lane j < 8 finalizes channel cv*8+j (mean, invstd, running-stat EMA, scale/shift).
-template <typename T, typename W>
+// MOMENTS: write this rank's (count, mean, M2) to mean_out as [3, C] and stop (SyncBatchNorm merges
+// the ranks' moments before any coefficient exists).
+template <typename T, typename W, bool MOMENTS = false>
 __global__ __launch_bounds__(64) void bn_stats_finalize_kernel(
     const float* __restrict__ part, int rblocks, int C, int64_t M, const T* __restrict__ x,
     const W* __restrict__ weight, const W* __restrict__ bias, W* running_mean, W* running_var,
@@ -173,6 +175,12 @@ __global__ __launch_bounds__(64) void bn_stats_finalize_kernel(
   const float dm = S * inv_m;
   const float var = fmaxf(SS * inv_m - dm * dm, 0.f);
   const float mean = Elem<T, float>::ld(x, c) + dm;
+  if (MOMENTS) {
+    mean_out[c] = (float)M;
+    mean_out[C + c] = mean;
+    mean_out[2 * C + c] = var * (float)M;
+    return;
+  }
   const float inv = rsqrtf(var + eps);
   mean_out[c] = mean;
   invstd_out[c] = inv;
@@ -529,6 +537,55 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
     });
   });
   return {y, mean, invstd, ss, mask_bits};
+}
+
+// Per-channel (count, mean, M2) of an NHWC activation as float [3, C] — one rank's share of a
+// SyncBatchNorm's statistics (merged across ranks by bn_stats_from_partials).
+at::Tensor bn_moments(const at::Tensor& x) {
+  check_nhwc(x);
+  const int64_t C = x.size(1), M = x.size(0) * x.size(2) * x.size(3);
+  TORCH_CHECK(M > 0, "bn_moments on empty input");
+  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  auto fopt = x.options().dtype(at::kFloat);
+  auto out = at::empty({3, C}, fopt);
+  Geo g = make_geo(M, (int)C);
+  auto part = at::empty({(int64_t)g.rblocks, C, 2}, fopt);
+  dispatch_act(x.scalar_type(), [&](auto tag_t) {
+    using T = decltype(tag_t);
+    const size_t lds = (size_t)kBlock * 16 * sizeof(float);
+    hipLaunchKernelGGL((bn_stats_kernel<T>), dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds, stream,
+                       reinterpret_cast<const T*>(x.data_ptr()), M, (int)C, g.rows_per, part.data_ptr<float>());
+    XDDP_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL((bn_stats_finalize_kernel<T, float, true>), dim3(C / 8), dim3(64), 0, stream,
+                       part.data_ptr<float>(), g.rblocks, (int)C, M, reinterpret_cast<const T*>(x.data_ptr()), nullptr,
+                       nullptr, nullptr, nullptr, nullptr, 0.f, false, 0.f, out.data_ptr<float>(), nullptr, nullptr,
+                       nullptr);
+    XDDP_HIP_CHECK(hipGetLastError());
+  });
+  return out;
+}
+
+// Per-row-block BN-backward partial sums (sum dy, sum dy·(x - mean)) as float [blocks, C, 2] (the
+// layout bn_backward_from_partials reads): the local half of a SyncBatchNorm backward.
+at::Tensor bn_grad_partials(const at::Tensor& dy_in, const at::Tensor& x, const at::Tensor& mean) {
+  check_nhwc(x);
+  auto dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "dy must match x");
+  TORCH_CHECK(mean.is_cuda() && mean.scalar_type() == at::kFloat && mean.numel() == x.size(1), "mean: float [C]");
+  const int64_t C = x.size(1), M = x.size(0) * x.size(2) * x.size(3);
+  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  Geo g = make_geo(M, (int)C);
+  auto part = at::empty({(int64_t)g.rblocks, C, 2}, x.options().dtype(at::kFloat));
+  dispatch_act(x.scalar_type(), [&](auto tag_t) {
+    using T = decltype(tag_t);
+    const size_t lds = (size_t)kBlock * 8 * 2 * sizeof(float);
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, 0, false, false>), dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds,
+                       stream, reinterpret_cast<const T*>(dy.data_ptr()), nullptr,
+                       reinterpret_cast<const T*>(x.data_ptr()), nullptr, nullptr, nullptr, M, (int)C, g.rows_per,
+                       mean.data_ptr<float>(), nullptr, part.data_ptr<float>());
+    XDDP_HIP_CHECK(hipGetLastError());
+  });
+  return part;
 }
 
 // Apply pass only, with coefficients computed elsewhere (e.g. from a conv epilogue's partial

@@ -20,6 +20,9 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy, const at::Tensor& x, c
                                     const at::Tensor& invstd, const c10::optional<at::Tensor>& ss, bool relu,
                                     bool need_dres, bool need_dweight, const c10::optional<at::Tensor>& dy2,
                                     const c10::optional<at::Tensor>& mask_bits, bool coef_only);
+// SyncBatchNorm halves: one rank's (count, mean, M2) [3, C]; one rank's backward sums [blocks, C, 2]
+at::Tensor bn_moments(const at::Tensor& x);
+at::Tensor bn_grad_partials(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& mean);
 std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, const c10::optional<at::Tensor>& residual,
                                  bool relu, bool save_mask, const c10::optional<at::Tensor>& num_batches_tracked);
 // 1x1 conv as an MFMA GEMM with BN prologue (previous BN's apply+ReLU) / epilogue (stats partials)

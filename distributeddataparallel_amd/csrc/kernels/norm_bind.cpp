@@ -23,6 +23,8 @@ void bind_norm_kernels(py::module_& m) {
   m.def("bn_backward_from_partials", &bn_backward_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),
         py::arg("mean"), py::arg("invstd"), py::arg("need_dweight"), py::arg("fold_mean") = true);
   m.def("bn_backward_elem", &bn_backward_elem, py::arg("g"), py::arg("x"), py::arg("mean"), py::arg("coef"));
+  m.def("bn_moments", &bn_moments, py::arg("x"));
+  m.def("bn_grad_partials", &bn_grad_partials, py::arg("dy"), py::arg("x"), py::arg("mean"));
   m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"));
   m.def("conv3x3_rot_weight", &conv3x3_rot_weight, py::arg("w"));
   m.def("conv3x3_wgrad", &conv3x3_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"));

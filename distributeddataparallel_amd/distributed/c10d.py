@@ -569,20 +569,29 @@ def barrier(group=None, async_op=False, device_ids=None):
 
 
 def monitored_barrier(group=None, timeout=None, wait_all_ranks=False):
-    """Store-based barrier that names the ranks that failed to arrive (CPU-side)."""
+    """Store-based barrier that names the ranks that failed to arrive (CPU-side).
+
+    Every rank keeps its own per-group generation count (all ranks call barriers in the same
+    order, so the counts agree): a rank that leaves barrier k early can never rejoin barrier k's
+    key. Each rank also marks its own arrival key, so a timeout names the missing ranks (all of
+    them with ``wait_all_ranks``, else the first)."""
+    import time
+
     pg = _resolve(group)
     timeout = timeout or pg.timeout
     store = pg.store
-    gen = store.add("monitored_barrier/gen", 0) // max(pg.size(), 1)
+    gen = getattr(pg, "_monitored_barrier_gen", 0)
+    pg._monitored_barrier_gen = gen + 1
     key = f"monitored_barrier/{gen}"
+    store.set(f"{key}/{pg.rank()}", "1")
     store.add(key, 1)
-    store.add("monitored_barrier/gen", 1)
-    import time
-
     deadline = time.time() + timeout.total_seconds()
     while store.add(key, 0) < pg.size():
         if time.time() > deadline:
-            raise RuntimeError(f"monitored_barrier timed out: {store.add(key, 0)}/{pg.size()} ranks arrived")
+            missing = [r for r in range(pg.size()) if not store.check([f"{key}/{r}"])]
+            named = missing if wait_all_ranks else missing[:1]
+            raise RuntimeError(f"monitored_barrier timed out after {timeout.total_seconds():.1f} s: "
+                               f"{store.add(key, 0)}/{pg.size()} ranks arrived; missing ranks {named}")
         time.sleep(0.005)
 
 

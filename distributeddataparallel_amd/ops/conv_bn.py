@@ -38,12 +38,17 @@ class EpiLink:
     GEMM folds ``add``, the producer's ReLU mask and the producer's BN-backward reduction into its
     epilogue (``conv1x1_gemm(..., epi_*)``), leaving the BN partials here (``part``). The producer's
     backward then starts from the finished gradient g and the partials: its separate reduce pass
-    over (dout, dout2, y, mask) is gone (csrc/kernels/conv_gemm.hip, EpiBN)."""
+    over (dout, dout2, y, mask) is gone (csrc/kernels/conv_gemm.hip, EpiBN).
 
-    __slots__ = ("y", "bits", "mean", "add", "part")
+    ``g`` is the exact tensor conv1's backward returned. If the gradient reaching the producer is
+    any other tensor (a third consumer of the block output — a feature hook, an auxiliary loss —
+    had its gradient summed in), the partials do not describe it and the producer falls back to
+    its own masked reduce over the sum (exact: g is already masked, and masking is idempotent)."""
+
+    __slots__ = ("y", "bits", "mean", "add", "part", "g")
 
     def __init__(self):
-        self.y = self.bits = self.mean = self.add = self.part = None
+        self.y = self.bits = self.mean = self.add = self.part = self.g = None
 
 
 class BNReLULink:
@@ -99,10 +104,14 @@ class _Conv1x1BN(torch.autograd.Function):
         epi_part = None
         if lo is not None:  # the next block's conv1 took (or left) the identity-path gradient
             if lo.part is not None:
-                epi_part, dout2 = lo.part, None
+                if dout2 is None and _same_tensor(dout, lo.g):
+                    epi_part = lo.part
+                elif dout2 is not None:  # an extra consumer of the residual alias
+                    dout = dout2 if dout is None else dout + dout2
+                dout2 = None  # (the identity-path gradient is inside g already)
             elif lo.add is not None:
                 dout2 = lo.add if dout2 is None else dout2 + lo.add
-            lo.y = lo.bits = lo.mean = lo.add = lo.part = None
+            lo.y = lo.bits = lo.mean = lo.add = lo.part = lo.g = None
         if dout is None:
             dout, dout2 = dout2, None
         if dout is None:
@@ -156,7 +165,7 @@ class _Conv1x1BN(torch.autograd.Function):
                 # the previous block's output gradient: dX + identity-path gradient, masked by its
                 # ReLU and reduced into its BN-backward partials in this GEMM's epilogue
                 dx, lx.part = C.conv1x1_gemm(dy, w, 1, None, False, None, True, lx.add, lx.y, lx.bits, lx.mean)
-                lx.add = None
+                lx.add, lx.g = None, dx
             else:
                 dx = _dgrad_in(ctx, C, dy, w, None, None)
             need_x = False

@@ -4,8 +4,15 @@
 Forward: per-rank (count, mean, M2) in fp32 → one all-gather of a [3, C] block per rank →
 Chan-merged global mean/var (numerically safe, no sum-of-squares cancellation) → normalize
 (+ running-stat EMA with the global unbiased variance). Backward: per-rank Σdy and
-Σdy·(x-mean) → one all-reduce of a [2, C] block → dx. Works on both backends (CPU tensors on
-``cpu``, GPU tensors on ``rccl``).
+Σdy·(x-mean) → one all-reduce of a [C, 2] block → dx; dweight / dbias stay local (DDP averages
+them with the other gradients), as in the reference.
+
+GPU NHWC inputs (channels_last, C % 8 == 0) run on the fused BN kernels of
+``csrc/kernels/batch_norm.hip``: ``bn_moments`` (one stats pass) → RCCL all-gather →
+``bn_stats_from_partials`` (the ranks are the groups of its Chan merge; also the running-stat
+update) → ``bn_apply``; backward ``bn_grad_partials`` (one reduce pass) → RCCL all-reduce →
+``bn_backward_from_partials`` → ``bn_backward_elem``. Three activation passes in all, no fp32
+copies of the activation. Other inputs (CPU, NCHW) use the eager fp32 path below.
 """
 from __future__ import annotations
 
@@ -73,6 +80,49 @@ class _SyncBN(torch.autograd.Function):
         return dx.to(x.dtype), dw, db, None, None, None, None, None
 
 
+def _native_ok(x: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dim() == 4 and x.shape[1] % 8 == 0 and x.numel() > 0
+            and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
+            and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0)
+
+
+class _SyncBNNative(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, pg):
+        from .._native import load
+
+        C = load()
+        local = C.bn_moments(x)  # [3, C]: count, mean, M2
+        gathered = torch.empty((pg.size(),) + tuple(local.shape), device=x.device, dtype=torch.float32)
+        pg.allgather_into_tensor(gathered, local).wait()
+        M = int(x.numel() // x.shape[1]) * pg.size()  # equal shards (the counts in `gathered` are exact)
+        mean, invstd, ss = C.bn_stats_from_partials(gathered, M, weight, bias, running_mean, running_var, None,
+                                                    momentum, False, eps)
+        y, _ = C.bn_apply(x, ss, None, False, False, None)
+        ctx.save_for_backward(x, weight, mean, invstd)
+        ctx.pg, ctx.M = pg, M
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .._native import load
+
+        C = load()
+        x, weight, mean, invstd = ctx.saved_tensors
+        part = C.bn_grad_partials(dy, x, mean)  # [blocks, C, 2]: sum dy, sum dy·(x - mean)
+        local = part.sum(0, keepdim=True)
+        total = local.clone()
+        work = ctx.pg.allreduce(total)
+        dw = db = None
+        need_w = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        if need_w:  # local dweight / dbias, computed while the all-reduce is in flight
+            _, dw, db = C.bn_backward_from_partials(local, x.numel() // x.shape[1], weight, mean, invstd, True, False)
+        work.wait()
+        coef, _, _ = C.bn_backward_from_partials(total, ctx.M, weight, mean, invstd, False, False)
+        dx = C.bn_backward_elem(dy.contiguous(memory_format=torch.channels_last), x, mean, coef)
+        return dx, dw, db, None, None, None, None, None
+
+
 class SyncBatchNorm(nn.modules.batchnorm._BatchNorm):
     def __init__(self, num_features, eps=1e-5, momentum: Optional[float] = 0.1, affine=True,
                  track_running_stats=True, process_group=None, device=None, dtype=None):
@@ -99,6 +149,8 @@ class SyncBatchNorm(nn.modules.batchnorm._BatchNorm):
         pg = self.process_group if self.process_group is not None else xdist.get_default_group()
         rm = self.running_mean if self.track_running_stats else None
         rv = self.running_var if self.track_running_stats else None
+        if _native_ok(x):
+            return _SyncBNNative.apply(x, self.weight, self.bias, rm, rv, self.eps, mom, pg)
         return _SyncBN.apply(x, self.weight, self.bias, rm, rv, self.eps, mom, pg)
 
     @classmethod

@@ -2,4 +2,4 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export XDDP_NO_AUTOBUILD=1
-timeout -k 10 300 python scripts/gemm_bench.py > gpurun_out/gemm_bench.log 2>&1; rc=$?; cat gpurun_out/gemm_bench.log; exit $rc
+GEMM_SET=resnet timeout -k 10 300 python scripts/gemm_bench.py > gpurun_out/gemm_bench_r50.log 2>&1; rc=$?; cat gpurun_out/gemm_bench_r50.log; exit $rc

@@ -329,3 +329,41 @@ def _w_future(rank, world):
 
 def test_work_future_and_wait_timeout():
     run_ranks(_w_future, world=2)
+
+
+def _w_monitored_barrier(rank, world):
+    import time
+
+    from distributeddataparallel_amd import distributed as dist
+
+    # back-to-back barriers with a slow rank: a fast rank must never pass barrier k+1 early
+    arrive = []
+    for k in range(4):
+        if rank == 1:
+            time.sleep(0.2)
+        dist.monitored_barrier(timeout=datetime.timedelta(seconds=20))
+        arrive.append(time.time())
+    from distributeddataparallel_amd.distributed.c10d import _resolve
+
+    store = _resolve(None).store
+    # publish rank 1's exit times; rank 0 must leave every barrier after rank 1 reached it
+    store.set(f"mb_test/{rank}", ",".join(f"{t:.6f}" for t in arrive))
+    dist.barrier()
+    if rank == 0:
+        raw = store.get("mb_test/1")
+        other = [float(t) for t in (raw.decode() if isinstance(raw, bytes) else raw).split(",")]
+        for k in range(4):
+            assert arrive[k] >= other[k] - 0.15, (k, arrive, other)
+    # a missing rank is named
+    if rank == 0:
+        try:
+            dist.monitored_barrier(timeout=datetime.timedelta(seconds=0.5), wait_all_ranks=True)
+        except RuntimeError as e:
+            assert "missing ranks [1]" in str(e), str(e)
+        else:
+            raise AssertionError("expected a timeout")
+    dist.barrier()
+
+
+def test_monitored_barrier_generations_and_missing_ranks():
+    run_ranks(_w_monitored_barrier, world=2)
