@@ -63,6 +63,11 @@ std::vector<at::Tensor> ln_backward(const at::Tensor& dy, const at::Tensor& x, c
                                     bool need_dgamma, bool need_dbeta);
 
 std::vector<at::Tensor> maxpool_forward(const at::Tensor& x, int64_t k, int64_t stride, int64_t pad);
+// ResNet stem bn1 -> ReLU -> maxpool(3, 2, 1) without the normalized activation (csrc/kernels/pool.hip)
+std::vector<at::Tensor> stem_pool_forward(const at::Tensor& x, const at::Tensor& ss);
+at::Tensor stem_pool_bn_backward(const at::Tensor& dy, const c10::optional<at::Tensor>& dy2, const at::Tensor& idx,
+                                 const at::Tensor& x, const at::Tensor& ss, const at::Tensor& mean,
+                                 const c10::optional<at::Tensor>& coef);
 at::Tensor maxpool_backward(const at::Tensor& dy, const at::Tensor& idx, const at::Tensor& x_like, int64_t k,
                             int64_t stride, int64_t pad, const c10::optional<at::Tensor>& dy2);
 

@@ -42,6 +42,9 @@ void bind_norm_kernels(py::module_& m) {
   m.def("rope", &rope, py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("backward") = false);
   m.def("swiglu_forward", &swiglu_forward, py::arg("a"), py::arg("b"));
   m.def("swiglu_backward", &swiglu_backward, py::arg("grad"), py::arg("a"), py::arg("b"));
+  m.def("stem_pool_forward", &stem_pool_forward, py::arg("x"), py::arg("scale_shift"));
+  m.def("stem_pool_bn_backward", &stem_pool_bn_backward, py::arg("dy"), py::arg("dy2"), py::arg("idx"), py::arg("x"),
+        py::arg("scale_shift"), py::arg("mean"), py::arg("coef") = py::none());
   m.def("maxpool_forward", &maxpool_forward, py::arg("x"), py::arg("kernel"), py::arg("stride"), py::arg("pad"));
   m.def("maxpool_backward", &maxpool_backward, py::arg("dy"), py::arg("idx"), py::arg("x_like"), py::arg("kernel"),
         py::arg("stride"), py::arg("pad"), py::arg("dy2") = py::none());

@@ -180,6 +180,218 @@ __global__ __launch_bounds__(256) void maxpool_bwd_k3s2p1_kernel(const T* __rest
   }
 }
 
+// ------------------------------------------------------------------ stem: BN + ReLU + max-pool
+// The ResNet stem's bn1 -> ReLU -> maxpool(3, 2, 1) without its 411 MB (bs256) normalized
+// activation ever existing in HBM: the forward pools relu(y·scale + shift) straight from the conv
+// output y (one read of y, pooled output + byte argmax written); the backward's two passes
+// (BN-backward partial sums, then dX) rebuild the pooled gradient per 2x2 quad from (dy, argmax)
+// and the ReLU mask from y, so neither the maxpool gradient nor the masked BN gradient is written.
+
+template <typename T>
+__device__ __forceinline__ float rnd(float v) {  // round to the storage precision of T
+  if constexpr (__is_same(T, bf16_t)) return dev::bf16_to_f32(dev::f32_to_bf16(v));
+  else if constexpr (__is_same(T, f16_t)) return dev::f16_to_f32(dev::f32_to_f16(v));
+  else return v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void stem_pool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ scale,
+                                                            const float* __restrict__ shift, T* __restrict__ y,
+                                                            uint8_t* __restrict__ idx, int N, int H, int W, int C,
+                                                            int OH, int OW) {
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * OH * OW * cv;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(t % cv) * 8;
+    int64_t r = t / cv;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int n = (int)(r / OH);
+    float sc[8], sh[8], m[8];
+    int am[8];
+    Vec8<float>::ld(scale + c0, sc);
+    Vec8<float>::ld(shift + c0, sh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      m[j] = -INFINITY;
+      am[j] = 0;
+    }
+    // branch-free window: the 9 loads are issued together (out-of-image taps read a clamped
+    // in-image pixel and are masked out of the max). A strip walker that carries the shared
+    // window row (6 loads per output instead of 9) measured slower: 178 vs 149 us at bs256.
+    const int h0 = oh * 2 - 1, w0 = ow * 2 - 1;
+    float v[9][8];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int h = min(max(h0 + kh, 0), H - 1), w = min(max(w0 + kw, 0), W - 1);
+        Vec8<T>::ld(x + (((int64_t)n * H + h) * W + w) * C + c0, v[kh * 3 + kw]);
+      }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const bool in = (unsigned)(h0 + kh) < (unsigned)H && (unsigned)(w0 + kw) < (unsigned)W;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // the value the unfused stack pools: BN + ReLU output rounded to storage precision
+          const float a = rnd<T>(fmaxf(fmaf(v[kh * 3 + kw][j], sc[j], sh[j]), 0.f));
+          if (in && (a > m[j] || isnan(a))) {  // first max wins; NaN propagates (torch semantics)
+            m[j] = a;
+            am[j] = kh * 3 + kw;
+          }
+        }
+      }
+    const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c0;
+    Vec8<T>::st(y + o, m);
+    uint64_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) packed |= (uint64_t)(am[j] & 0xff) << (8 * j);
+    *reinterpret_cast<uint64_t*>(idx + o) = packed;
+  }
+}
+
+// ELEM = false: per-block partials (sum g, sum g·(y - mean)) [blocks][C][2] of the masked BN
+// gradient g = [y·scale + shift > 0] · maxpool_backward(dy + dy2); ELEM = true: the BN-backward
+// input gradient dX = k1·g + k2·(y - mean) + k3 (coef [3, C], unfolded).
+// A lane owns 8 channels of a vertical strip of 2x2 input quads (h = 2t, 2t+1; w = 2u, 2u+1) for
+// t in [t0, t0 + kStrip): quad row t is covered by the pooling windows of rows t and t+1, so the
+// lane walks down the strip carrying window row t+1 (argmax + dy) into the next quad row — each
+// window is fetched twice (by the strips u and u-1, adjacent lanes) instead of four times by
+// scattered quads, and the work of a block stays inside one XCD's L2. The lane's channel chunk
+// is fixed (256 % (C / 8) == 0), so its BN sums stay in registers.
+constexpr int kStrip = 14;
+
+template <typename T>
+struct PoolWin {  // two adjacent pooling windows (u, u+1) of one window row, dy + dy2 summed
+  uint64_t packed[2];
+  float g[2][8];
+  __device__ __forceinline__ void load(const T* dy, const T* dy2, const uint8_t* idx, int n, int oh, int u, int OH,
+                                       int OW, int C, int c0) {
+    const int ohc = min(oh, OH - 1);
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const int64_t o = (((int64_t)n * OH + ohc) * OW + min(u + d, OW - 1)) * C + c0;
+      packed[d] = *reinterpret_cast<const uint64_t*>(idx + o);
+      Vec8<T>::ld(dy + o, g[d]);
+      if (dy2) {
+        float g2[8];
+        Vec8<T>::ld(dy2 + o, g2);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[d][j] += g2[j];
+      }
+      if (oh >= OH || u + d >= OW) packed[d] = ~0ull;  // no window: matches no position
+    }
+  }
+};
+
+template <typename T, bool ELEM>
+__global__ __launch_bounds__(256) void stem_pool_bn_bwd_kernel(
+    const T* __restrict__ dy, const T* __restrict__ dy2, const uint8_t* __restrict__ idx, const T* __restrict__ y,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
+    const float* __restrict__ coef, float* __restrict__ part, T* __restrict__ dx, int N, int H, int W, int C, int OH,
+    int OW) {
+  const int cv = C / 8;
+  const int QH = (H + 1) / 2, QW = (W + 1) / 2, NS = (QH + kStrip - 1) / kStrip;
+  const int64_t total = (int64_t)N * NS * QW * cv;
+  const int64_t q = (int64_t)dev::xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const int c0 = (int)(threadIdx.x % cv) * 8;
+  float sc[8], sh[8], mu[8], k1[8], k2[8], k3[8], s1[8], s2[8];
+  Vec8<float>::ld(scale + c0, sc);
+  Vec8<float>::ld(shift + c0, sh);
+  Vec8<float>::ld(mean + c0, mu);
+  if (ELEM) {
+    Vec8<float>::ld(coef + c0, k1);
+    Vec8<float>::ld(coef + C + c0, k2);
+    Vec8<float>::ld(coef + 2 * C + c0, k3);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  if (q < total) {
+    int64_t r = q / cv;
+    const int u = (int)(r % QW);
+    r /= QW;
+    const int strip = (int)(r % NS);
+    const int n = (int)(r / NS);
+    const int t0 = strip * kStrip, t1 = min(t0 + kStrip, QH);
+    PoolWin<T> top, bot;
+    top.load(dy, dy2, idx, n, t0, u, OH, OW, C, c0);
+    for (int t = t0; t < t1; ++t) {
+      bot.load(dy, dy2, idx, n, t + 1, u, OH, OW, C, c0);
+      float yq[4][8];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int h = min(2 * t + (d >> 1), H - 1), w = min(2 * u + (d & 1), W - 1);
+        Vec8<T>::ld(y + (((int64_t)n * H + h) * W + w) * C + c0, yq[d]);
+      }
+      float acc[4][8];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[a][j] = 0.f;
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+        for (int dw = 0; dw < 2; ++dw) {
+          const PoolWin<T>& win = dh ? bot : top;
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+              // input (2t + a, 2u + b) sits at offset (1 + a - 2dh, 1 + b - 2dw) of window (t + dh, u + dw)
+              const int kh = 1 + a - 2 * dh, kw = 1 + b - 2 * dw;
+              if (kh < 0 || kw < 0) continue;  // compile-time after unrolling
+              const int pos = kh * 3 + kw;
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                if ((int)((win.packed[dw] >> (8 * j)) & 0xff) == pos) acc[a * 2 + b][j] += win.g[dw][j];
+            }
+        }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int h = 2 * t + a, w = 2 * u + b;
+          if (h >= H || w >= W) continue;
+          const float* yv = yq[a * 2 + b];
+          float out[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            // g at the precision the unfused maxpool backward stores it, masked by the ReLU
+            const float g = fmaf(yv[j], sc[j], sh[j]) > 0.f ? rnd<T>(acc[a * 2 + b][j]) : 0.f;
+            const float dd = yv[j] - mu[j];
+            if (ELEM) {
+              out[j] = fmaf(k1[j], g, fmaf(k2[j], dd, k3[j]));
+            } else {
+              s1[j] += g;
+              s2[j] = fmaf(g, dd, s2[j]);
+            }
+          }
+          if (ELEM) dev::st8_stream(dx + (((int64_t)n * H + h) * W + w) * C + c0, out);
+        }
+      top = bot;
+    }
+  }
+  if (ELEM) return;
+  // block reduce over the lanes sharing c0 (256 / cv of them), then [block][C][2] partials
+  __shared__ float red[256][17];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[threadIdx.x][j] = s1[j];
+    red[threadIdx.x][8 + j] = s2[j];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C * 2; i += blockDim.x) {  // i = channel * 2 + which
+    const int c = i >> 1, which = i & 1, chunk = c / 8, j = c % 8;
+    float v = 0.f;
+    for (int l = chunk; l < (int)blockDim.x; l += cv) v += red[l][which * 8 + j];
+    part[((int64_t)blockIdx.x * C + c) * 2 + which] = v;
+  }
+}
+
 template <typename F>
 void dispatch_pool(at::ScalarType st, F&& f) {
   switch (st) {
@@ -250,6 +462,71 @@ at::Tensor maxpool_backward(const at::Tensor& dy_in, const at::Tensor& idx, cons
     XDDP_HIP_CHECK(hipGetLastError());
   });
   return dx;
+}
+
+// ResNet stem: maxpool(3, 2, 1) of relu(x·scale + shift) -> (pooled, byte argmax)
+std::vector<at::Tensor> stem_pool_forward(const at::Tensor& x, const at::Tensor& ss) {
+  check(x, 3);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(ss.is_cuda() && ss.scalar_type() == at::kFloat && ss.numel() == 2 * C && ss.is_contiguous(),
+              "stem_pool_forward: scale/shift must be float [2, C]");
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  auto y = at::empty({N, C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto idx = at::empty({N, OH, OW, C}, x.options().dtype(at::kByte));
+  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  const int64_t total = (int64_t)N * OH * OW * (C / 8);
+  if (total == 0) return {y, idx};
+  dispatch_pool(x.scalar_type(), [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL((stem_pool_fwd_kernel<T>), dim3(grid_for(total)), dim3(256), 0, stream,
+                       reinterpret_cast<const T*>(x.data_ptr()), ss.data_ptr<float>(), ss.data_ptr<float>() + C,
+                       reinterpret_cast<T*>(y.data_ptr()), idx.data_ptr<uint8_t>(), N, H, W, C, OH, OW);
+    XDDP_HIP_CHECK(hipGetLastError());
+  });
+  return {y, idx};
+}
+
+// Stem backward through maxpool(3, 2, 1) and the ReLU of bn(x): without coef, the BN-backward
+// partial sums [blocks, C, 2] (for bn_backward_from_partials); with coef [3, C] (unfolded), dX.
+at::Tensor stem_pool_bn_backward(const at::Tensor& dy_in, const c10::optional<at::Tensor>& dy2_in,
+                                 const at::Tensor& idx, const at::Tensor& x, const at::Tensor& ss,
+                                 const at::Tensor& mean, const c10::optional<at::Tensor>& coef) {
+  check(x, 3);
+  auto dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  at::Tensor dy2 = (dy2_in.has_value() && dy2_in->defined()) ? dy2_in->contiguous(at::MemoryFormat::ChannelsLast)
+                                                              : at::Tensor();
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dy.size(0) == N && dy.size(1) == C && dy.size(2) == OH && dy.size(3) == OW &&
+                  dy.scalar_type() == x.scalar_type() && idx.numel() == dy.numel(),
+              "stem_pool_bn_backward: dy / argmax do not match x");
+  if (dy2.defined()) TORCH_CHECK(dy2.sizes() == dy.sizes() && dy2.scalar_type() == dy.scalar_type(), "dy2 != dy");
+  TORCH_CHECK(ss.numel() == 2 * C && mean.numel() == C && ss.scalar_type() == at::kFloat &&
+                  mean.scalar_type() == at::kFloat, "stem_pool_bn_backward: ss [2, C], mean [C] float");
+  const bool elem = coef.has_value() && coef->defined();
+  if (elem) TORCH_CHECK(coef->numel() == 3 * C && coef->scalar_type() == at::kFloat, "coef must be float [3, C]");
+  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  const int64_t lanes = (int64_t)N * (((H + 1) / 2 + kStrip - 1) / kStrip) * ((W + 1) / 2) * (C / 8);
+  TORCH_CHECK(lanes < ((int64_t)1 << 31) - 256, "stem_pool_bn_backward: input too large");
+  const int grid = (int)((lanes + 255) / 256);
+  TORCH_CHECK(256 % (C / 8) == 0, "stem_pool_bn_backward: C / 8 must divide 256");
+  at::Tensor out = elem ? at::empty_like(x, at::MemoryFormat::ChannelsLast)
+                        : at::empty({grid, C, 2}, x.options().dtype(at::kFloat));
+  dispatch_pool(x.scalar_type(), [&](auto tag) {
+    using T = decltype(tag);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, stream, reinterpret_cast<const T*>(dy.data_ptr()),
+                         dy2.defined() ? reinterpret_cast<const T*>(dy2.data_ptr()) : nullptr, idx.data_ptr<uint8_t>(),
+                         reinterpret_cast<const T*>(x.data_ptr()), ss.data_ptr<float>(), ss.data_ptr<float>() + C,
+                         mean.data_ptr<float>(), elem ? coef->data_ptr<float>() : nullptr,
+                         elem ? nullptr : out.data_ptr<float>(), elem ? reinterpret_cast<T*>(out.data_ptr()) : nullptr,
+                         N, H, W, C, OH, OW);
+      XDDP_HIP_CHECK(hipGetLastError());
+    };
+    if (elem) go(stem_pool_bn_bwd_kernel<T, true>);
+    else go(stem_pool_bn_bwd_kernel<T, false>);
+  });
+  return out;
 }
 
 }  // namespace kernels

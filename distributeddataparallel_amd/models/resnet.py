@@ -33,6 +33,13 @@ def _conv_bn_fusion() -> bool:
     return os.environ.get("XDDP_CONV_BN_FUSION", "1") != "0"
 
 
+def _stem_fusion() -> bool:
+    """XDDP_STEM_FUSION=0 runs the stem's bn1 -> ReLU -> maxpool as separate kernels (A/B switch)."""
+    import os
+
+    return os.environ.get("XDDP_STEM_FUSION", "1") != "0"
+
+
 def _bn_relu(norm_layer, c):
     """Return (bn, act). A fused norm layer (``fuses_relu``) absorbs the ReLU."""
     bn = norm_layer(c)
@@ -172,8 +179,15 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.relu(self.bn1(self.conv1(x)))
-        x = self.maxpool(x)
+        x = self.conv1(x)
+        pooled = None
+        if getattr(self.bn1, "fuses_relu", False) and getattr(self.bn1, "relu", False) and \
+                getattr(self.maxpool, "dual_output", None) is not None and self.training and _stem_fusion():
+            # bn1 -> ReLU -> maxpool without the normalized activation in HBM (ops/pool.py)
+            from ..ops.pool import stem_bn_relu_maxpool
+
+            pooled = stem_bn_relu_maxpool(x, self.bn1, self.maxpool, dual=self.maxpool.dual_output)
+        x = pooled if pooled is not None else self.maxpool(self.relu(self.bn1(x)))
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)

@@ -7,7 +7,7 @@ import torch.nn.functional as F
 
 from .._native import load
 
-__all__ = ["FusedMaxPool2d"]
+__all__ = ["FusedMaxPool2d", "stem_bn_relu_maxpool"]
 
 
 class _MaxPool(torch.autograd.Function):
@@ -31,6 +31,59 @@ class _MaxPool(torch.autograd.Function):
             return None, None, None, None, None
         x_like = torch.empty(shape, device="meta")  # only the input shape is needed
         return load().maxpool_backward(dy, idx, x_like, k, s, p, dy2), None, None, None, None
+
+
+class _StemBNPool(torch.autograd.Function):
+    """bn (batch statistics) -> ReLU -> maxpool(3, 2, 1) with the normalized activation never
+    materialized (csrc/kernels/pool.hip, stem_*): forward = one stats pass over y + one fused
+    normalize/ReLU/pool pass; backward = partial-sums pass + dX pass, both rebuilding the pooled
+    gradient and the ReLU mask on the fly."""
+
+    @staticmethod
+    def forward(ctx, y, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, dual):
+        C = load()
+        ctx.set_materialize_grads(False)
+        M = y.numel() // y.shape[1]
+        moments = C.bn_moments(y)  # [3, C]
+        mean, invstd, ss = C.bn_stats_from_partials(moments.unsqueeze(0), M, weight, bias, running_mean, running_var,
+                                                    nbt, momentum, cma, eps)
+        if nbt is not None:
+            nbt.add_(1)
+        out, idx = C.stem_pool_forward(y, ss)
+        ctx.save_for_backward(y, idx, weight, mean, invstd, ss)
+        if dual:  # block-0 conv1 and its downsample: gradients summed in-kernel
+            return out, out.view_as(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy, dy2=None):
+        C = load()
+        y, idx, weight, mean, invstd, ss = ctx.saved_tensors
+        if dy is None:
+            dy, dy2 = dy2, None
+        if dy is None:
+            return (None,) * 10
+        M = y.numel() // y.shape[1]
+        need_w = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        part = C.stem_pool_bn_backward(dy, dy2, idx, y, ss, mean)
+        coef, dw, db = C.bn_backward_from_partials(part, M, weight, mean, invstd, need_w, False)
+        dx = C.stem_pool_bn_backward(dy, dy2, idx, y, ss, mean, coef) if ctx.needs_input_grad[0] else None
+        return (dx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None,
+                None, None, None, None, None, None, None)
+
+
+def stem_bn_relu_maxpool(y, bn, pool, dual: bool = False):
+    """``pool(relu(bn(y)))`` for a training-mode FusedBatchNorm2d and a 3x3/s2/p1 max-pool on an
+    NHWC tensor; returns ``None`` when the fused kernels do not cover the case (caller falls back)."""
+    k, s, p = _single(pool.kernel_size), _single(pool.stride), _single(pool.padding)
+    if not (bn.training and bn.track_running_stats and (k, s, p) == (3, 2, 1) and _single(pool.dilation) == 1
+            and not pool.ceil_mode and y.is_cuda and y.dim() == 4 and y.size(1) % 8 == 0 and 256 % (y.size(1) // 8) == 0
+            and y.is_contiguous(memory_format=torch.channels_last) and y.data_ptr() % 16 == 0
+            and y.dtype in (torch.bfloat16, torch.float16, torch.float32)):
+        return None
+    cma = bn.momentum is None
+    return _StemBNPool.apply(y, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                             0.0 if cma else float(bn.momentum), cma, float(bn.eps), dual)
 
 
 def _single(v):
