@@ -63,6 +63,10 @@ std::vector<at::Tensor> ln_backward(const at::Tensor& dy, const at::Tensor& x, c
                                     bool need_dgamma, bool need_dbeta);
 
 std::vector<at::Tensor> maxpool_forward(const at::Tensor& x, int64_t k, int64_t stride, int64_t pad);
+// ResNet stem 7x7/s2 conv (3 -> 64) with BN-statistics partials, and its weight gradient
+// (csrc/kernels/stem_conv.hip)
+std::vector<at::Tensor> stem_conv_forward(const at::Tensor& x, const at::Tensor& w);
+at::Tensor stem_conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w_like);
 // ResNet stem bn1 -> ReLU -> maxpool(3, 2, 1) without the normalized activation (csrc/kernels/pool.hip)
 std::vector<at::Tensor> stem_pool_forward(const at::Tensor& x, const at::Tensor& ss);
 at::Tensor stem_pool_bn_backward(const at::Tensor& dy, const c10::optional<at::Tensor>& dy2, const at::Tensor& idx,

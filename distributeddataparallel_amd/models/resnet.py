@@ -179,14 +179,22 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.conv1(x)
+        fused = (getattr(self.bn1, "fuses_relu", False) and getattr(self.bn1, "relu", False)
+                 and getattr(self.maxpool, "dual_output", None) is not None and self.training and _stem_fusion())
         pooled = None
-        if getattr(self.bn1, "fuses_relu", False) and getattr(self.bn1, "relu", False) and \
-                getattr(self.maxpool, "dual_output", None) is not None and self.training and _stem_fusion():
-            # bn1 -> ReLU -> maxpool without the normalized activation in HBM (ops/pool.py)
-            from ..ops.pool import stem_bn_relu_maxpool
+        if fused:
+            from ..ops.stem import resnet_stem, stem_supported
 
-            pooled = stem_bn_relu_maxpool(x, self.bn1, self.maxpool, dual=self.maxpool.dual_output)
+            if stem_supported(x, self.conv1, self.bn1, self.maxpool):
+                # conv (BN statistics in its epilogue) -> normalize/ReLU/pool: ops/stem.py
+                pooled = resnet_stem(x, self.conv1, self.bn1, self.maxpool, dual=self.maxpool.dual_output)
+        if pooled is None:
+            x = self.conv1(x)
+            if fused:
+                # bn1 -> ReLU -> maxpool without the normalized activation in HBM (ops/pool.py)
+                from ..ops.pool import stem_bn_relu_maxpool
+
+                pooled = stem_bn_relu_maxpool(x, self.bn1, self.maxpool, dual=self.maxpool.dual_output)
         x = pooled if pooled is not None else self.maxpool(self.relu(self.bn1(x)))
         x = self.layer1(x)
         x = self.layer2(x)

@@ -7,7 +7,7 @@ path, iters = sys.argv[1], int(sys.argv[2])
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 50
 g = collections.defaultdict(list)
 for x in csv.DictReader(open(path)):
-    n = x["Kernel_Name"].replace("void xddp::kernels::(anonymous namespace)::", "").replace("xddp::dev::bf16_t", "bf16")
+    n = x["Kernel_Name"].replace("void ", "", 1).replace("xddp::kernels::(anonymous namespace)::", "").replace("xddp::dev::bf16_t", "bf16")
     n = n.split("(")[0][:80]
     g[(n, x["Grid_Size_X"], x["Grid_Size_Y"], x["Workgroup_Size_X"])].append(int(x["End_Timestamp"]) - int(x["Start_Timestamp"]))
 tot = sum(sum(d) for d in g.values())

@@ -79,3 +79,98 @@ def test_stem_bn_relu_maxpool_matches_fp32(shape):
     assert rel(bn.running_mean, ref.running_mean) < 1e-4
     assert rel(bn.running_var, ref.running_var) < 1e-3
     assert int(bn.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("shape", [(4, 3, 224, 224), (2, 3, 57, 61)])
+def test_stem_conv_forward_and_wgrad_match_fp32(shape):
+    """stem_conv_forward (output + BN-statistics partials) and stem_conv_wgrad vs fp32 torch."""
+    from distributeddataparallel_amd._native import load
+
+    C = load()
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(shape, device="cuda", generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 7, 7, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+    w_cl = w.contiguous(memory_format=torch.channels_last)  # the model's weights are channels_last
+    y, part = C.stem_conv_forward(x, w_cl)
+    yr = F.conv2d(x.float(), w.float(), stride=2, padding=3)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+
+    def rel(a, b):
+        return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+    assert rel(y, yr) < 5e-3, rel(y, yr)
+    M = y.numel() // 64
+    mean, invstd, _ = C.bn_stats_from_partials(part, M, None, None, None, None, None, 0.0, False, 1e-5)
+    var_r, mean_r = torch.var_mean(y.float(), dim=(0, 2, 3), unbiased=False)
+    assert (mean - mean_r).abs().max().item() < 1e-3 * (var_r.sqrt().max().item() + 1)
+    assert rel(1.0 / invstd ** 2 - 1e-5, var_r) < 1e-3
+
+    dy = torch.randn(y.shape, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    dw = C.stem_conv_wgrad(dy, x, w_cl)
+    dwr = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), stride=2, padding=3)
+    assert dw.shape == w.shape and dw.dtype == w.dtype
+    assert rel(dw, dwr) < 1e-2, rel(dw, dwr)
+
+
+def test_resnet_stem_matches_unfused_stack():
+    """The whole own-kernel stem (ops/stem.py) vs the same model stem on MIOpen conv + the
+    unfused xddp BN / max-pool kernels: outputs and every parameter gradient."""
+    import os
+
+    from distributeddataparallel_amd.models import resnet50
+    from distributeddataparallel_amd.ops import FusedBatchNorm2d
+    from distributeddataparallel_amd.ops.stem import _Stem
+
+    torch.manual_seed(0)
+    m = resnet50(norm_layer=FusedBatchNorm2d).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(8, 3, 112, 112, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+
+    def stem_run(env):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            for p in (m.conv1.weight, m.bn1.weight, m.bn1.bias):
+                p.grad = None
+            calls = []
+            orig = _Stem.forward
+            _Stem.forward = staticmethod(lambda *a, **k: calls.append(1) or orig(*a, **k))
+            try:
+                out = m.maxpool(m.relu(m.bn1(m.conv1(x)))) if env.get("XDDP_STEM_FUSION") == "0" else None
+                if out is None:
+                    fused = type(m).forward  # run only the stem part of ResNet.forward
+                    del fused
+                    from distributeddataparallel_amd.ops.stem import resnet_stem, stem_supported
+
+                    if env.get("XDDP_STEM_CONV", "1") == "1":
+                        assert stem_supported(x, m.conv1, m.bn1, m.maxpool)
+                        out = resnet_stem(x, m.conv1, m.bn1, m.maxpool, dual=True)
+                    else:
+                        from distributeddataparallel_amd.ops.pool import stem_bn_relu_maxpool
+
+                        out = stem_bn_relu_maxpool(m.conv1(x), m.bn1, m.maxpool, dual=True)
+            finally:
+                _Stem.forward = staticmethod(orig)
+            o = out if isinstance(out, tuple) else (out,)
+            torch.autograd.backward(list(o), [torch.ones_like(t) * 0.01 for t in o])
+            return (o[0].float().clone(), m.conv1.weight.grad.float().clone(), m.bn1.weight.grad.float().clone(),
+                    m.bn1.bias.grad.float().clone(), len(calls))
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+    own = stem_run({"XDDP_STEM_CONV": "1"})
+    ref = stem_run({"XDDP_STEM_CONV": "0"})
+    assert own[4] == 1 and ref[4] == 0
+
+    def rel(a, b):
+        return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+    assert rel(own[0], ref[0]) < 2e-2
+    for a, b in zip(own[1:4], ref[1:4]):
+        assert rel(a, b) < 5e-2, rel(a, b)
