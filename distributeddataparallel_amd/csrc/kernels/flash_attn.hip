@@ -55,6 +55,7 @@ using dev::u32x4;
 
 constexpr int kBK = 64;   // keys per K/V tile
 constexpr float kNegInf = -1e30f;
+constexpr float kLazy = 8.f;  // log2-domain headroom before the running max is raised
 
 __device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
@@ -126,6 +127,28 @@ struct TileRegs {
 };
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// every wave's LDS-DMA for the current stage has landed and every wave is done with the previous
+// stage (whose buffer the next DMA overwrites)
+__device__ __forceinline__ void dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// K/V tile rows [r0, r0 + 64) of a [B, S, H, D] tensor -> LDS by LDS-DMA (1 KB per wave
+// instruction, lane i -> 16 B at slot i; the source chunk is pre-swizzled so the LDS image is the
+// uswz layout). Rows past `rows` read row rows - 1 (finite; the caller masks those keys).
+template <int D, int NW>
+__device__ __forceinline__ void dma_tile(const uint16_t* base, int64_t ss, int r0, int rows, uint8_t* T, int w,
+                                         int lane) {
+  constexpr int RPI = 512 / D, NI = kBK / RPI, PER = NI / NW;
+  static_assert(PER * NW == NI, "tile pieces must split evenly over the waves");
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int ins = w * PER + i, r = ins * RPI + lane / (D / 8);
+    const int c = uswz<D>(r, lane % (D / 8));
+    const int64_t row = min(r0 + r, rows - 1);
+    __builtin_amdgcn_global_load_lds((const void*)(base + row * ss + c * 8), (lds_ptr_t)(T + ins * 1024), 16, 0, 0);
+  }
+}
 
 // ------------------------------------------------------------------------------------------ fwd
 // NW waves x 32 query rows per workgroup. At NW = 8 two waves share each SIMD, so one wave's
@@ -136,162 +159,153 @@ __global__ __launch_bounds__(64 * NW) void fa_fwd_kernel(const uint16_t* __restr
                                                         const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
                                                         float* __restrict__ LSE, int Sq, int Sk, int Hq, int Hkv,
                                                         Strides qs, Strides ks, Strides vs, Strides os,
-                                                        float scale_log2) {
-  constexpr int QPW = 1, KS = D / 16, NT = D / 32, BQ = 32 * NW;
-  __shared__ __attribute__((aligned(16))) uint8_t Kt[kBK * D * 2];
-  __shared__ __attribute__((aligned(16))) uint8_t Vt[kBK * D * 2];
+                                                        float scale_log2, int nqb) {
+  constexpr int KS = D / 16, NT = D / 32, BQ = 32 * NW;
+  __shared__ __attribute__((aligned(16))) uint8_t KVs[2][2][kBK * D * 2];  // [stage][K, V]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 5;
   const int bh = blockIdx.y, b = bh / Hq, h = bh % Hq, hk = h / (Hq / Hkv);
-  const int nqb = gridDim.x;
-  const int qb = CAUSAL ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;  // heaviest causal blocks first
-  const int q0 = qb * BQ, qw = q0 + 32 * w;                             // wave rows [qw, qw + 32)
   const uint16_t* Qb = Q + b * qs.b + h * qs.h;
   const uint16_t* Kb = K + b * ks.b + hk * ks.h;
   const uint16_t* Vb = V + b * vs.b + hk * vs.h;
-
-  int qrow[QPW];
-  bf16x8 qf[QPW][KS];
-  f32x16 acc_o[QPW][NT];
-  float m_run[QPW], l_run[QPW];
+  // causal: a workgroup takes query blocks (nqb - 1 - x, x) — a heavy and a light one, the same
+  // total number of K/V tiles for every workgroup (one pass when they coincide)
+  const int npass = CAUSAL && (int)blockIdx.x != nqb - 1 - (int)blockIdx.x ? 2 : 1;
+#pragma unroll 1
+  for (int pass = 0; pass < npass; ++pass) {
+    const int qb = CAUSAL ? (pass == 0 ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x) : (int)blockIdx.x;
+    const int q0 = qb * BQ, qw = q0 + 32 * w;  // wave rows [qw, qw + 32)
+    const int qrow = qw + (lane & 31);
+    bf16x8 qf[KS];
+    f32x16 acc_o[NT];
 #pragma unroll
-  for (int u = 0; u < QPW; ++u) {
-    qrow[u] = qw + 32 * u + (lane & 31);
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-      qf[u][s] = qrow[u] < Sq ? *reinterpret_cast<const bf16x8*>(Qb + (int64_t)qrow[u] * qs.s + 16 * s + 8 * g)
-                              : bf16x8{};
+    for (int s2 = 0; s2 < KS; ++s2)
+      qf[s2] = qrow < Sq ? *reinterpret_cast<const bf16x8*>(Qb + (int64_t)qrow * qs.s + 16 * s2 + 8 * g) : bf16x8{};
 #pragma unroll
     for (int n = 0; n < NT; ++n)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc_o[u][n][i] = 0.f;
-    m_run[u] = kNegInf;
-    l_run[u] = 0.f;
-  }
+      for (int i = 0; i < 16; ++i) acc_o[n][i] = 0.f;
+    // m_run: the (scaled, log2-domain) reference max the accumulators are relative to. It is only
+    // raised when a row max exceeds it by more than kLazy (wave-uniform test), so most tiles skip
+    // the 64-multiply rescale; P = exp2(s - m_run) then stays below 2^kLazy (exact in fp32 / bf16 range).
+    float m_run = kNegInf, l_run = 0.f;
 
-  const int kend = CAUSAL ? min(Sk, q0 + BQ) : Sk;
-  const int ntiles = (kend + kBK - 1) / kBK;
-  TileRegs<D, 64 * NW> kr, vr;
-  kr.load(Kb, ks.s, 0, Sk, tid);
-  vr.load(Vb, vs.s, 0, Sk, tid);
-  for (int j = 0; j < ntiles; ++j) {
-    const int k0 = j * kBK;
-    kr.store(Kt, tid);
-    vr.store(Vt, tid);
-    lds_barrier();
-    if (j + 1 < ntiles) {  // next tile in flight during this tile's math
-      kr.load(Kb, ks.s, k0 + kBK, Sk, tid);
-      vr.load(Vb, vs.s, k0 + kBK, Sk, tid);
-    }
-    if (!CAUSAL || k0 <= qw + 32 * QPW - 1) {  // a wave whose rows all precede the tile skips it
-      f32x16 sc[QPW][2];
-#pragma unroll
-      for (int u = 0; u < QPW; ++u)
+    const int kend = CAUSAL ? min(Sk, q0 + BQ) : Sk;
+    const int ntiles = (kend + kBK - 1) / kBK;
+    dma_tile<D, NW>(Kb, ks.s, 0, Sk, KVs[0][0], w, lane);
+    dma_tile<D, NW>(Vb, vs.s, 0, Sk, KVs[0][1], w, lane);
+    for (int j = 0; j < ntiles; ++j) {
+      const int k0 = j * kBK;
+      dma_barrier();
+      if (j + 1 < ntiles) {  // next tile in flight during this tile's math
+        dma_tile<D, NW>(Kb, ks.s, k0 + kBK, Sk, KVs[(j + 1) & 1][0], w, lane);
+        dma_tile<D, NW>(Vb, vs.s, k0 + kBK, Sk, KVs[(j + 1) & 1][1], w, lane);
+      }
+      const uint8_t* Kt = KVs[j & 1][0];
+      const uint8_t* Vt = KVs[j & 1][1];
+      if (!CAUSAL || k0 <= qw + 31) {  // a wave whose rows all precede the tile skips it
+        f32x16 sc[2];
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) sc[u][t][i] = 0.f;
+          for (int i = 0; i < 16; ++i) sc[t][i] = 0.f;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const bf16x8 kfr = ld_rowfrag<D>(Kt, 32 * t + (lane & 31), s, lane);
-#pragma unroll
-          for (int u = 0; u < QPW; ++u) sc[u][t] = mfma32(kfr, qf[u][s], sc[u][t]);
-        }
-      bf16x8 pf[QPW][4];
-#pragma unroll
-      for (int u = 0; u < QPW; ++u) {
-        // scale, mask, row max (in-lane over 32 keys, then lane ^ 32)
+          for (int s2 = 0; s2 < KS; ++s2) sc[t] = mfma32(ld_rowfrag<D>(Kt, 32 * t + (lane & 31), s2, lane), qf[s2], sc[t]);
+        // masks only on the tiles that need them (the causal diagonal, the key tail): wave-uniform
+        const bool masked = k0 + kBK > Sk || (CAUSAL && k0 + kBK - 1 > qw);
         float mx = kNegInf;
+        {  // last visible key of this lane's row, tile-relative (no limit off the boundary)
+          const int lim = masked ? (CAUSAL ? min(qrow, Sk - 1) : Sk - 1) - k0 : (1 << 30);
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (32 * t + kappa(g, i & 7) + 16 * (i >> 3) > lim) sc[t][i] = kNegInf;
+        }
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = k0 + 32 * t + kappa(g, i & 7) + 16 * (i >> 3);
-            float v = sc[u][t][i] * scale_log2;
-            if (key >= Sk || (CAUSAL && key > qrow[u])) v = kNegInf;
-            sc[u][t][i] = v;
-            mx = fmaxf(mx, v);
-          }
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float m_new = fmaxf(m_run[u], mx);
-        const float alpha = __builtin_amdgcn_exp2f(m_run[u] - m_new);
+          for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[t][i]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;  // the scale is positive: max commutes
+        const bool raise = mx > m_run + kLazy;
+        if (__builtin_amdgcn_ballot_w64(raise) != 0) {  // some row of the wave needs a new reference
+          const float m_new = fmaxf(m_run, mx);
+          const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+          l_run *= alpha;
+#pragma unroll
+          for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc_o[n][i] *= alpha;
+          m_run = m_new;
+        }
+        bf16x8 pf[4];
         float ls = 0.f;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float p = __builtin_amdgcn_exp2f(sc[u][t][i] - m_new);
-            sc[u][t][i] = p;
-            ls += p;
-          }
-        l_run[u] = l_run[u] * alpha + ls;
-        m_run[u] = m_new;
-#pragma unroll
-        for (int n = 0; n < NT; ++n)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) acc_o[u][n][i] *= alpha;
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const int t = kk >> 1, hh = kk & 1;
           uint32_t pk[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            pk[e] = dev::pack_bf16x2(sc[u][t][8 * hh + 2 * e], sc[u][t][8 * hh + 2 * e + 1]);
-          pf[u][kk] = __builtin_bit_cast(bf16x8, pk);
+          for (int e = 0; e < 4; ++e) {
+            const float p0 = __builtin_amdgcn_exp2f(fmaf(sc[t][8 * hh + 2 * e], scale_log2, -m_run));
+            const float p1 = __builtin_amdgcn_exp2f(fmaf(sc[t][8 * hh + 2 * e + 1], scale_log2, -m_run));
+            ls += p0 + p1;
+            pk[e] = dev::pack_bf16x2(p0, p1);
+          }
+          pf[kk] = __builtin_bit_cast(bf16x8, pk);
         }
+        l_run += ls;
+        // O^T += V^T P^T over the 4 16-key steps of the tile
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int n = 0; n < NT; ++n) acc_o[n] = mfma32(ld_trfrag<D>(Vt, 16 * kk, 32 * n, lane), pf[kk], acc_o[n]);
       }
-      // O^T += V^T P^T over the 4 16-key steps of the tile; one V fragment for all QPW blocks
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          const bf16x8 vfr = ld_trfrag<D>(Vt, 16 * kk, 32 * n, lane);
-#pragma unroll
-          for (int u = 0; u < QPW; ++u) acc_o[u][n] = mfma32(vfr, pf[u][kk], acc_o[u][n]);
-        }
     }
-    lds_barrier();  // every wave is done with this tile before it is overwritten
-  }
-#pragma unroll
-  for (int u = 0; u < QPW; ++u) {
-    const float l_tot = l_run[u] + __shfl_xor(l_run[u], 32, 64);
-    if (qrow[u] < Sq) {
+    lds_barrier();  // (causal pairs) every wave is done with the stages before the next pass refills them
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    if (qrow < Sq) {
       const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-      uint16_t* Ob = O + b * os.b + h * os.h + (int64_t)qrow[u] * os.s;
+      uint16_t* Ob = O + b * os.b + h * os.h + (int64_t)qrow * os.s;
 #pragma unroll
       for (int n = 0; n < NT; ++n)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {  // 4 consecutive d per store: d = 32n + 4g + 8q + 0..3
           uint2 pk;
-          pk.x = dev::pack_bf16x2(acc_o[u][n][4 * q] * inv, acc_o[u][n][4 * q + 1] * inv);
-          pk.y = dev::pack_bf16x2(acc_o[u][n][4 * q + 2] * inv, acc_o[u][n][4 * q + 3] * inv);
+          pk.x = dev::pack_bf16x2(acc_o[n][4 * q] * inv, acc_o[n][4 * q + 1] * inv);
+          pk.y = dev::pack_bf16x2(acc_o[n][4 * q + 2] * inv, acc_o[n][4 * q + 3] * inv);
           *reinterpret_cast<uint2*>(Ob + 32 * n + 4 * g + 8 * q) = pk;
         }
-      if (g == 0) LSE[(int64_t)bh * Sq + qrow[u]] = m_run[u] + log2f(fmaxf(l_tot, 1e-30f));
+      if (g == 0) LSE[(int64_t)bh * Sq + qrow] = m_run + log2f(fmaxf(l_tot, 1e-30f));
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------ bwd
-// delta[bh][q] = sum_d dO[q][d] · O[q][d] (fp32), one wave per query row
+// delta[bh][q] = sum_d dO[q][d] · O[q][d] (fp32): D / 8 lanes per query row, 16-B loads, a
+// shuffle reduction inside each lane group (64 / (D / 8) rows per wave)
 template <int D>
 __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(const uint16_t* __restrict__ O, const uint16_t* __restrict__ dO,
-                                                         float* __restrict__ delta, int Sq, int Hq, Strides os,
-                                                         Strides dos) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // over B*Hq*Sq (a multiple of 4)
-  const int q = (int)(row % Sq);
-  const int64_t bh = row / Sq;
-  const int b = (int)(bh / Hq), h = (int)(bh % Hq);
+                                                         float* __restrict__ delta, int64_t rows, int Sq, int Hq,
+                                                         Strides os, Strides dos) {
+  constexpr int LPR = D / 8;  // lanes per row
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = t / LPR;
+  const int c = (int)(t % LPR) * 8;
   float s = 0.f;
-  if (lane * 2 < D) {
-    const uint32_t ov = *reinterpret_cast<const uint32_t*>(O + b * os.b + h * os.h + (int64_t)q * os.s + 2 * lane);
-    const uint32_t dv = *reinterpret_cast<const uint32_t*>(dO + b * dos.b + h * dos.h + (int64_t)q * dos.s + 2 * lane);
-    s = bf2f(ov & 0xffff) * bf2f(dv & 0xffff) + bf2f(ov >> 16) * bf2f(dv >> 16);
+  if (row < rows) {
+    const int q = (int)(row % Sq);
+    const int64_t bh = row / Sq;
+    const int b = (int)(bh / Hq), h = (int)(bh % Hq);
+    const dev::u32x4 ov = *reinterpret_cast<const dev::u32x4*>(O + b * os.b + h * os.h + (int64_t)q * os.s + c);
+    const dev::u32x4 dv = *reinterpret_cast<const dev::u32x4*>(dO + b * dos.b + h * dos.h + (int64_t)q * dos.s + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      s += bf2f(ov[e] & 0xffff) * bf2f(dv[e] & 0xffff) + bf2f(ov[e] >> 16) * bf2f(dv[e] >> 16);
   }
-  s = dev::wave_sum(s);
-  if (lane == 0) delta[row] = s;
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) s += __shfl_xor(s, o, 64);
+  if (row < rows && t % LPR == 0) delta[row] = s;
 }
 
 // dQ: one workgroup = NW waves x 32 query rows of one (batch, q head); S^T and dP^T with the
@@ -301,116 +315,100 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
     uint16_t* __restrict__ dQ, int Sq, int Sk, int Hq, int Hkv, Strides qs, Strides ks, Strides vs, Strides dos,
-    Strides dqs, float scale_log2, float scale) {
-  constexpr int QPW = 1, KS = D / 16, NT = D / 32, BQ = 32 * NW;
-  __shared__ __attribute__((aligned(16))) uint8_t Kt[kBK * D * 2];  // row reads (S^T), transposed reads (dQ)
-  __shared__ __attribute__((aligned(16))) uint8_t Vt[kBK * D * 2];  // row reads (dP^T)
+    Strides dqs, float scale_log2, float scale, int nqb) {
+  constexpr int KS = D / 16, NT = D / 32, BQ = 32 * NW;
+  // [stage][K (row reads for S^T, transposed reads for dQ), V (row reads for dP^T)]
+  __shared__ __attribute__((aligned(16))) uint8_t KVs[2][2][kBK * D * 2];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 5;
   const int bh = blockIdx.y, b = bh / Hq, h = bh % Hq, hk = h / (Hq / Hkv);
-  const int qb = CAUSAL ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
-  const int q0 = qb * BQ, qw = q0 + 32 * w;
   const uint16_t* Kb = K + b * ks.b + hk * ks.h;
   const uint16_t* Vb = V + b * vs.b + hk * vs.h;
-  int qrow[QPW];
-  bf16x8 qf[QPW][KS], dof[QPW][KS];
-  float lse[QPW], dl[QPW];
-  f32x16 acc[QPW][NT];
+  // causal: query blocks (nqb - 1 - x, x) per workgroup, as the forward
+  const int npass = CAUSAL && (int)blockIdx.x != nqb - 1 - (int)blockIdx.x ? 2 : 1;
+#pragma unroll 1
+  for (int pass = 0; pass < npass; ++pass) {
+    const int qb = CAUSAL ? (pass == 0 ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x) : (int)blockIdx.x;
+    const int q0 = qb * BQ, qw = q0 + 32 * w;
+    const int qrow = qw + (lane & 31);
+    const bool ok = qrow < Sq;
+    bf16x8 qf[KS], dof[KS];
 #pragma unroll
-  for (int u = 0; u < QPW; ++u) {
-    qrow[u] = qw + 32 * u + (lane & 31);
-    const bool ok = qrow[u] < Sq;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      qf[u][s] = ok ? *reinterpret_cast<const bf16x8*>(Q + b * qs.b + h * qs.h + (int64_t)qrow[u] * qs.s + 16 * s + 8 * g)
-                    : bf16x8{};
-      dof[u][s] = ok ? *reinterpret_cast<const bf16x8*>(dO + b * dos.b + h * dos.h + (int64_t)qrow[u] * dos.s + 16 * s +
-                                                        8 * g)
-                     : bf16x8{};
+    for (int s2 = 0; s2 < KS; ++s2) {
+      qf[s2] = ok ? *reinterpret_cast<const bf16x8*>(Q + b * qs.b + h * qs.h + (int64_t)qrow * qs.s + 16 * s2 + 8 * g)
+                  : bf16x8{};
+      dof[s2] = ok ? *reinterpret_cast<const bf16x8*>(dO + b * dos.b + h * dos.h + (int64_t)qrow * dos.s + 16 * s2 + 8 * g)
+                   : bf16x8{};
     }
-    lse[u] = ok ? LSE[(int64_t)bh * Sq + qrow[u]] : 0.f;
-    dl[u] = ok ? delta[(int64_t)bh * Sq + qrow[u]] : 0.f;
+    const float lse = ok ? LSE[(int64_t)bh * Sq + qrow] : 0.f;
+    const float dl = ok ? delta[(int64_t)bh * Sq + qrow] : 0.f;
+    f32x16 acc[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[u][n][i] = 0.f;
-  }
-  const int kend = CAUSAL ? min(Sk, q0 + BQ) : Sk;
-  const int ntiles = (kend + kBK - 1) / kBK;
-  TileRegs<D, 64 * NW> kr, vr;
-  kr.load(Kb, ks.s, 0, Sk, tid);
-  vr.load(Vb, vs.s, 0, Sk, tid);
-  for (int j = 0; j < ntiles; ++j) {
-    const int k0 = j * kBK;
-    kr.store(Kt, tid);
-    vr.store(Vt, tid);
-    lds_barrier();
-    if (j + 1 < ntiles) {
-      kr.load(Kb, ks.s, k0 + kBK, Sk, tid);
-      vr.load(Vb, vs.s, k0 + kBK, Sk, tid);
-    }
-    if (!CAUSAL || k0 <= qw + 31) {
-      // one 32-key half at a time keeps S^T / dP^T at 32 live registers
+      for (int i = 0; i < 16; ++i) acc[n][i] = 0.f;
+    const int kend = CAUSAL ? min(Sk, q0 + BQ) : Sk;
+    const int ntiles = (kend + kBK - 1) / kBK;
+    dma_tile<D, NW>(Kb, ks.s, 0, Sk, KVs[0][0], w, lane);
+    dma_tile<D, NW>(Vb, vs.s, 0, Sk, KVs[0][1], w, lane);
+    for (int j = 0; j < ntiles; ++j) {
+      const int k0 = j * kBK;
+      dma_barrier();
+      if (j + 1 < ntiles) {
+        dma_tile<D, NW>(Kb, ks.s, k0 + kBK, Sk, KVs[(j + 1) & 1][0], w, lane);
+        dma_tile<D, NW>(Vb, vs.s, k0 + kBK, Sk, KVs[(j + 1) & 1][1], w, lane);
+      }
+      const uint8_t* Kt = KVs[j & 1][0];
+      const uint8_t* Vt = KVs[j & 1][1];
+      if (!CAUSAL || k0 <= qw + 31) {
+        const bool masked = k0 + kBK > Sk || (CAUSAL && k0 + kBK - 1 > qw);  // wave-uniform
+        // one 32-key half at a time keeps S^T / dP^T at 32 live registers
+#pragma unroll 1
+        for (int t = 0; t < 2; ++t) {
+          f32x16 sc, dp;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        f32x16 sc[QPW], dp[QPW];
+          for (int i = 0; i < 16; ++i) sc[i] = dp[i] = 0.f;
 #pragma unroll
-        for (int u = 0; u < QPW; ++u)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) sc[u][i] = dp[u][i] = 0.f;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const bf16x8 kfr = ld_rowfrag<D>(Kt, 32 * t + (lane & 31), s, lane);
-          const bf16x8 vfr = ld_rowfrag<D>(Vt, 32 * t + (lane & 31), s, lane);
-#pragma unroll
-          for (int u = 0; u < QPW; ++u) {
-            sc[u] = mfma32(kfr, qf[u][s], sc[u]);
-            dp[u] = mfma32(vfr, dof[u][s], dp[u]);
+          for (int s2 = 0; s2 < KS; ++s2) {
+            sc = mfma32(ld_rowfrag<D>(Kt, 32 * t + (lane & 31), s2, lane), qf[s2], sc);
+            dp = mfma32(ld_rowfrag<D>(Vt, 32 * t + (lane & 31), s2, lane), dof[s2], dp);
           }
-        }
-        // dS^T = P^T (dP^T - delta), P^T = exp2(S^T c - lse); the softmax scale of dS folds into the end
-        bf16x8 sf[QPW][2];
-#pragma unroll
-        for (int u = 0; u < QPW; ++u) {
+          // dS^T = P^T (dP^T - delta), P^T = exp2(S^T c - lse); the softmax scale of dS folds into the end
+          // last visible key of this lane's row, relative to the half tile (no limit off the boundary)
+          const int lim = masked ? (CAUSAL ? min(qrow, Sk - 1) : Sk - 1) - k0 - 32 * t : (1 << 30);
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            const int key = k0 + 32 * t + kappa(g, i & 7) + 16 * (i >> 3);
-            float p = __builtin_amdgcn_exp2f(sc[u][i] * scale_log2 - lse[u]);
-            if (key >= Sk || (CAUSAL && key > qrow[u])) p = 0.f;
-            sc[u][i] = p * (dp[u][i] - dl[u]);
+            float p = __builtin_amdgcn_exp2f(fmaf(sc[i], scale_log2, -lse));
+            if (kappa(g, i & 7) + 16 * (i >> 3) > lim) p = 0.f;
+            sc[i] = p * (dp[i] - dl);
           }
+          bf16x8 sf[2];
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
             uint32_t pk[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) pk[e] = dev::pack_bf16x2(sc[u][8 * hh + 2 * e], sc[u][8 * hh + 2 * e + 1]);
-            sf[u][hh] = __builtin_bit_cast(bf16x8, pk);
+            for (int e = 0; e < 4; ++e) pk[e] = dev::pack_bf16x2(sc[8 * hh + 2 * e], sc[8 * hh + 2 * e + 1]);
+            sf[hh] = __builtin_bit_cast(bf16x8, pk);
           }
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = mfma32(ld_trfrag<D>(Kt, 32 * t + 16 * hh, 32 * n, lane), sf[hh], acc[n]);
         }
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-          for (int n = 0; n < NT; ++n) {
-            const bf16x8 kt = ld_trfrag<D>(Kt, 32 * t + 16 * hh, 32 * n, lane);
-#pragma unroll
-            for (int u = 0; u < QPW; ++u) acc[u][n] = mfma32(kt, sf[u][hh], acc[u][n]);
-          }
       }
     }
-    lds_barrier();
-  }
+    lds_barrier();  // (causal pairs) every wave is done with the stages before the next pass refills them
+    if (ok) {
+      uint16_t* out = dQ + b * dqs.b + h * dqs.h + (int64_t)qrow * dqs.s;
 #pragma unroll
-  for (int u = 0; u < QPW; ++u) {
-    if (qrow[u] >= Sq) continue;
-    uint16_t* out = dQ + b * dqs.b + h * dqs.h + (int64_t)qrow[u] * dqs.s;
+      for (int n = 0; n < NT; ++n)
 #pragma unroll
-    for (int n = 0; n < NT; ++n)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint2 pk;
-        pk.x = dev::pack_bf16x2(acc[u][n][4 * q] * scale, acc[u][n][4 * q + 1] * scale);
-        pk.y = dev::pack_bf16x2(acc[u][n][4 * q + 2] * scale, acc[u][n][4 * q + 3] * scale);
-        *reinterpret_cast<uint2*>(out + 32 * n + 4 * g + 8 * q) = pk;
-      }
+        for (int q = 0; q < 4; ++q) {
+          uint2 pk;
+          pk.x = dev::pack_bf16x2(acc[n][4 * q] * scale, acc[n][4 * q + 1] * scale);
+          pk.y = dev::pack_bf16x2(acc[n][4 * q + 2] * scale, acc[n][4 * q + 3] * scale);
+          *reinterpret_cast<uint2*>(out + 32 * n + 4 * g + 8 * q) = pk;
+        }
+    }
   }
 }
 
@@ -439,7 +437,9 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t smem[VBLK + 4 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wq = w & 3, G = w >> 2, g = lane >> 5;
   const int bhk = blockIdx.y, b = bhk / Hkv, hk = bhk % Hkv, grp = Hq / Hkv;
-  const int kb = CAUSAL ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  // causal: low key blocks see the most query tiles — dispatched first (pairing blocks per
+  // workgroup would halve the grid below the CU count at the Llama shape)
+  const int kb = (int)blockIdx.x;
   const int k0 = kb * 128, kw = k0 + 32 * wq, krow = kw + (lane & 31);
   uint8_t* Vblk = smem;
   {  // V rows [k0, k0 + 128) -> LDS (rows past Sk read row Sk - 1; their P, dS are masked to 0)
@@ -507,13 +507,13 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
         sc = mfma32(ld_rowfrag<D>(Qt, lane & 31, s, lane), kf[s], sc);
         dp = mfma32(ld_rowfrag<D>(Dt, lane & 31, s, lane), ld_rowfrag<D>(Vblk, 32 * wq + (lane & 31), s, lane), dp);
       }
-      // element i: query qt0 + kappa(g, i&7) + 16(i>>3), key krow
+      // element i: query qt0 + kappa(g, i&7) + 16(i>>3), key krow; visible iff lo <= ql < hi
+      const int lo = krow >= Sk ? (1 << 30) : (CAUSAL ? krow - qt0 : -1), hi = Sq - qt0;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int ql = kappa(g, i & 7) + 16 * (i >> 3);
-        const int q = qt0 + ql;
-        float p = __builtin_amdgcn_exp2f(sc[i] * scale_log2 - lse_s[ql]);
-        if (q >= Sq || krow >= Sk || (CAUSAL && krow > q)) p = 0.f;
+        float p = __builtin_amdgcn_exp2f(fmaf(sc[i], scale_log2, -lse_s[ql]));
+        if (ql < lo || ql >= hi) p = 0.f;
         sc[i] = p;
         dp[i] = p * (dp[i] - dl_s[ql]);
       }
@@ -606,13 +606,14 @@ std::vector<at::Tensor> flash_attn_forward(const at::Tensor& q, const at::Tensor
   }();
   const int64_t wg8 = ((Sq + 255) / 256) * B * Hq;
   const int nw = nw_env == 4 || nw_env == 8 ? nw_env : (wg8 >= 256 ? 8 : 4);
-  const dim3 grid((unsigned)((Sq + 32 * nw - 1) / (32 * nw)), (unsigned)(B * Hq));
+  const int nqb = (int)((Sq + 32 * nw - 1) / (32 * nw));
+  const dim3 grid((unsigned)(causal ? (nqb + 1) / 2 : nqb), (unsigned)(B * Hq));
   const float sl2 = (float)(scale * 1.4426950408889634);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, reinterpret_cast<const uint16_t*>(q.data_ptr()),
                        reinterpret_cast<const uint16_t*>(k.data_ptr()), reinterpret_cast<const uint16_t*>(v.data_ptr()),
                        reinterpret_cast<uint16_t*>(o.data_ptr()), lse.data_ptr<float>(), (int)Sq, (int)Sk, (int)Hq,
-                       (int)Hkv, strides_of(q), strides_of(k), strides_of(v), strides_of(o), sl2);
+                       (int)Hkv, strides_of(q), strides_of(k), strides_of(v), strides_of(o), sl2, nqb);
     XDDP_HIP_CHECK(hipGetLastError());
   };
 #define XDDP_FA(D_, C_) \
@@ -644,16 +645,16 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
   auto delta = at::empty({B, Hq, Sq}, q.options().dtype(at::kFloat));
   auto stream = c10::hip::getCurrentHIPStream(q.device().index()).stream();
   const int64_t rows = B * Hq * Sq;
-  {  // delta: one wave per query row
-    auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
+  {  // delta: D / 8 lanes per query row
+    auto go = [&](auto kern, int lpr) {
+      const int64_t threads = rows * lpr;
+      hipLaunchKernelGGL(kern, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream,
                          reinterpret_cast<const uint16_t*>(o.data_ptr()),
-                         reinterpret_cast<const uint16_t*>(dout.data_ptr()), delta.data_ptr<float>(), (int)Sq, (int)Hq,
-                         strides_of(o), strides_of(dout));
+                         reinterpret_cast<const uint16_t*>(dout.data_ptr()), delta.data_ptr<float>(), rows, (int)Sq,
+                         (int)Hq, strides_of(o), strides_of(dout));
       XDDP_HIP_CHECK(hipGetLastError());
     };
-    TORCH_CHECK(rows % 4 == 0, "flash_attn backward: B*H*S must be a multiple of 4");
-    if (D == 128) go(fa_bwd_pre_kernel<128>); else go(fa_bwd_pre_kernel<64>);
+    if (D == 128) go(fa_bwd_pre_kernel<128>, 16); else go(fa_bwd_pre_kernel<64>, 8);
   }
   const float sl2 = (float)(scale * 1.4426950408889634), sc = (float)scale;
   {
@@ -663,14 +664,15 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
     }();
     const int64_t wg8 = ((Sq + 255) / 256) * B * Hq;
     const int nw = nw_env == 4 || nw_env == 8 ? nw_env : (wg8 >= 256 ? 8 : 4);
-    const dim3 grid((unsigned)((Sq + 32 * nw - 1) / (32 * nw)), (unsigned)(B * Hq));
+    const int nqb = (int)((Sq + 32 * nw - 1) / (32 * nw));
+    const dim3 grid((unsigned)(causal ? (nqb + 1) / 2 : nqb), (unsigned)(B * Hq));
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, stream, reinterpret_cast<const uint16_t*>(q.data_ptr()),
                          reinterpret_cast<const uint16_t*>(k.data_ptr()), reinterpret_cast<const uint16_t*>(v.data_ptr()),
                          reinterpret_cast<const uint16_t*>(dout.data_ptr()), lse.data_ptr<float>(),
                          delta.data_ptr<float>(), reinterpret_cast<uint16_t*>(dq.data_ptr()), (int)Sq, (int)Sk,
                          (int)Hq, (int)Hkv, strides_of(q), strides_of(k), strides_of(v), strides_of(dout),
-                         strides_of(dq), sl2, sc);
+                         strides_of(dq), sl2, sc, nqb);
       XDDP_HIP_CHECK(hipGetLastError());
     };
 #define XDDP_FA(D_, C_) \
@@ -680,7 +682,8 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
 #undef XDDP_FA
   }
   {
-    const dim3 grid((unsigned)((Sk + 127) / 128), (unsigned)(B * Hkv));
+    const int nkb = (int)((Sk + 127) / 128);
+    const dim3 grid((unsigned)nkb, (unsigned)(B * Hkv));
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, grid, dim3(512), 0, stream, reinterpret_cast<const uint16_t*>(q.data_ptr()),
                          reinterpret_cast<const uint16_t*>(k.data_ptr()), reinterpret_cast<const uint16_t*>(v.data_ptr()),

@@ -67,6 +67,9 @@ std::vector<at::Tensor> maxpool_forward(const at::Tensor& x, int64_t k, int64_t 
 // (csrc/kernels/stem_conv.hip)
 std::vector<at::Tensor> stem_conv_forward(const at::Tensor& x, const at::Tensor& w);
 at::Tensor stem_conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w_like);
+at::Tensor stem_conv_wgrad_fused(const at::Tensor& dyp, const c10::optional<at::Tensor>& dyp2, const at::Tensor& idx,
+                                 const at::Tensor& y, const at::Tensor& x, const at::Tensor& w_like,
+                                 const at::Tensor& ss, const at::Tensor& mean, const at::Tensor& coef);
 // ResNet stem bn1 -> ReLU -> maxpool(3, 2, 1) without the normalized activation (csrc/kernels/pool.hip)
 std::vector<at::Tensor> stem_pool_forward(const at::Tensor& x, const at::Tensor& ss);
 at::Tensor stem_pool_bn_backward(const at::Tensor& dy, const c10::optional<at::Tensor>& dy2, const at::Tensor& idx,

@@ -44,6 +44,8 @@ void bind_norm_kernels(py::module_& m) {
   m.def("swiglu_backward", &swiglu_backward, py::arg("grad"), py::arg("a"), py::arg("b"));
   m.def("stem_conv_forward", &stem_conv_forward, py::arg("x"), py::arg("w"));
   m.def("stem_conv_wgrad", &stem_conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("w_like"));
+  m.def("stem_conv_wgrad_fused", &stem_conv_wgrad_fused, py::arg("dyp"), py::arg("dyp2"), py::arg("idx"), py::arg("y"),
+        py::arg("x"), py::arg("w_like"), py::arg("scale_shift"), py::arg("mean"), py::arg("coef"));
   m.def("stem_pool_forward", &stem_pool_forward, py::arg("x"), py::arg("scale_shift"));
   m.def("stem_pool_bn_backward", &stem_pool_bn_backward, py::arg("dy"), py::arg("dy2"), py::arg("idx"), py::arg("x"),
         py::arg("scale_shift"), py::arg("mean"), py::arg("coef") = py::none());

@@ -31,7 +31,7 @@ def main():
     y = torch.randint(0, 1000, (256,), device="cuda", generator=g)
     torch.manual_seed(0)
     fused = resnet50(norm_layer=FusedBatchNorm2d).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
-    sd = fused.state_dict()
+    sd = {k: v.detach().clone() for k, v in fused.state_dict().items()}  # (the live tensors get trained)
     curves = {}
 
     ddp = xddp.DDP(fused, device_ids=[0], gradient_as_bucket_view=True)
