@@ -412,38 +412,42 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_kernel(
   }
 }
 
-// dK, dV: one workgroup = 128 keys of one (batch, kv head), 8 waves in two groups of 4. Wave
-// (group G, index wq) owns keys k0 + 32 wq .. +31; the groups split the (query head of the GQA
-// group, 32-row query tile) work items (G takes items G, G + 2, ...), so two waves share each
-// SIMD, and sum their dK^T / dV^T accumulators through LDS at the end. Per item: S = Q·K^T and
+// dK, dV: one workgroup = 32·KW keys of one (batch, kv head), 8 waves in NG = 8 / KW groups of KW.
+// Wave (group G, index wq) owns keys k0 + 32 wq .. +31; the groups split the (query head of the
+// GQA group, 32-row query tile) work items (G takes items G, G + NG, ...), so two waves share each
+// SIMD, and sum their dK^T / dV^T accumulators through LDS at the end. KW = 4 (128-key blocks) is
+// the default; KW = 2 (XDDP_FA_DKDV_KW=2) balances causal work better (twice as many half-size
+// blocks) but re-reads every Q / dO tile per 64 keys: Llama-shape fwd+bwd 1.30 vs 1.16 ms. Per item: S = Q·K^T and
 // dP = dO·V^T with the KEY on the lane (K fragments in registers, the V block in LDS), then
 // dV^T += dO^T·P and dK^T += Q^T·dS with P / dS as the B operands straight from their
 // accumulators. Q / dO / lse / delta tiles go global -> LDS by LDS-DMA (no VGPR staging), two
 // stages per group: item k + 1 is in flight while item k is computed; one barrier per item.
 // Registers: K 32 + dK^T 64 + dV^T 64 + S, dP 32 (D = 128) stay under the 256 of two waves/SIMD.
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int KW>
 __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq, int Sk, int Hq, int Hkv, Strides qs, Strides ks,
     Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale) {
+  constexpr int NG = 8 / KW, BK = 32 * KW;          // groups; keys per workgroup
   constexpr int KS = D / 16, NT = D / 32, QB = 32;  // query rows per work item
   constexpr int TILE = QB * D * 2;                  // bytes of one Q (or dO) tile
   constexpr int STAGE = 2 * TILE + 2 * QB * 4;      // Q, dO, lse, delta
-  constexpr int VBLK = 128 * D * 2;                 // the workgroup's V rows
-  constexpr int RPI = 512 / D, NI = QB / RPI / 4;   // rows per 1-KB DMA instruction; instructions per wave
-  constexpr int RED = 4 * NT * 16 * 64 * 4;         // one accumulator set of group 1
-  static_assert(RED <= VBLK + 4 * STAGE, "group reduction must fit the LDS");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[VBLK + 4 * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wq = w & 3, G = w >> 2, g = lane >> 5;
+  constexpr int VBLK = BK * D * 2;                  // the workgroup's V rows
+  constexpr int RPI = 512 / D, NI = QB / RPI / KW;  // rows per 1-KB DMA instruction; instructions per wave
+  constexpr int ACC = NT * 16 * 64;                 // floats of one wave's dK^T (or dV^T)
+  static_assert(KW >= 2 && KW * NG == 8 && NI * KW * RPI == QB, "wave split");
+  static_assert((NG - 1) * KW * ACC * 4 <= VBLK + 2 * NG * STAGE, "group reduction must fit the LDS");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[VBLK + 2 * NG * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wq = w % KW, G = w / KW, g = lane >> 5;
   const int bhk = blockIdx.y, b = bhk / Hkv, hk = bhk % Hkv, grp = Hq / Hkv;
   // causal: low key blocks see the most query tiles — dispatched first (pairing blocks per
   // workgroup would halve the grid below the CU count at the Llama shape)
   const int kb = (int)blockIdx.x;
-  const int k0 = kb * 128, kw = k0 + 32 * wq, krow = kw + (lane & 31);
+  const int k0 = kb * BK, kw = k0 + 32 * wq, krow = kw + (lane & 31);
   uint8_t* Vblk = smem;
-  {  // V rows [k0, k0 + 128) -> LDS (rows past Sk read row Sk - 1; their P, dS are masked to 0)
-    constexpr int VI = 128 / RPI / 8;
+  {  // V rows [k0, k0 + BK) -> LDS (rows past Sk read row Sk - 1; their P, dS are masked to 0)
+    constexpr int VI = BK / RPI / 8;
     const uint16_t* Vb = V + b * vs.b + hk * vs.h;
 #pragma unroll
     for (int i = 0; i < VI; ++i) {
@@ -466,7 +470,7 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
     for (int i = 0; i < 16; ++i) adk[n][i] = adv[n][i] = 0.f;
   const int qstart = CAUSAL ? (k0 / QB) * QB : 0;
   const int nqt = (Sq - qstart + QB - 1) / QB;
-  const int total = grp * nqt, niter = (total + 1) / 2;
+  const int total = grp * nqt, niter = (total + NG - 1) / NG;
   uint8_t* gsm = smem + VBLK + G * 2 * STAGE;
   auto issue = [&](int it, int st) {  // rows past Sq read row Sq - 1 (masked below)
     const int h = hk * grp + it / nqt, qt0 = qstart + (it % nqt) * QB;
@@ -491,8 +495,8 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
   if (G < total) issue(G, 0);
   for (int k = 0; k < niter; ++k) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const int it = G + 2 * k;
-    if (it + 2 < total) issue(it + 2, (k + 1) & 1);  // into the stage item k - 1 was computed from
+    const int it = G + NG * k;
+    if (it + NG < total) issue(it + NG, (k + 1) & 1);  // into the stage item k - 1 was computed from
     const int qt0 = qstart + (it % nqt) * QB;
     if (it < total && (!CAUSAL || qt0 + QB - 1 >= kw)) {
       const uint8_t* Qt = gsm + (k & 1) * STAGE;
@@ -534,27 +538,34 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
       }
     }
   }
-  // group 1 hands its partial dK^T, then dV^T, to group 0 through the (now idle) LDS
-  float* red = reinterpret_cast<float*>(smem) + wq * (NT * 16 * 64) + lane;
+  // groups 1..NG-1 hand their partial dK^T, then dV^T, to group 0 through the (now idle) LDS
+  float* red = reinterpret_cast<float*>(smem) + lane;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     f32x16* acc = pass == 0 ? adk : adv;
-    if (G == 1) {
+    if (G > 0) {
+      float* r = red + ((G - 1) * KW + wq) * ACC;
 #pragma unroll
       for (int n = 0; n < NT; ++n)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) red[(n * 16 + i) * 64] = acc[n][i];
+        for (int i = 0; i < 16; ++i) r[(n * 16 + i) * 64] = acc[n][i];
     }
     __syncthreads();
     if (G == 0) {
+      const float* r = red + wq * ACC;
 #pragma unroll
       for (int n = 0; n < NT; ++n)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[n][i] += red[(n * 16 + i) * 64];
+        for (int i = 0; i < 16; ++i) {
+          float v = 0.f;
+#pragma unroll
+          for (int gg = 1; gg < NG; ++gg) v += r[(gg - 1) * KW * ACC + (n * 16 + i) * 64];
+          acc[n][i] += v;
+        }
     }
   }
-  if (G == 1 || krow >= Sk) return;
+  if (G != 0 || krow >= Sk) return;
   uint16_t* ok = dK + b * dks.b + hk * dks.h + (int64_t)krow * dks.s;
   uint16_t* ov = dV + b * dvs.b + hk * dvs.h + (int64_t)krow * dvs.s;
 #pragma unroll
@@ -682,7 +693,12 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
 #undef XDDP_FA
   }
   {
-    const int nkb = (int)((Sk + 127) / 128);
+    static const int kw_env = [] {
+      const char* e = std::getenv("XDDP_FA_DKDV_KW");
+      return e ? std::atoi(e) : 4;
+    }();
+    const int kwv = kw_env == 2 ? 2 : 4;
+    const int nkb = (int)((Sk + 32 * kwv - 1) / (32 * kwv));
     const dim3 grid((unsigned)nkb, (unsigned)(B * Hkv));
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, grid, dim3(512), 0, stream, reinterpret_cast<const uint16_t*>(q.data_ptr()),
@@ -693,8 +709,11 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
                          strides_of(k), strides_of(v), strides_of(dout), strides_of(dk), strides_of(dv), sl2, sc);
       XDDP_HIP_CHECK(hipGetLastError());
     };
-    if (D == 128) { if (causal) go(fa_bwd_dkdv_kernel<128, true>); else go(fa_bwd_dkdv_kernel<128, false>); }
-    else { if (causal) go(fa_bwd_dkdv_kernel<64, true>); else go(fa_bwd_dkdv_kernel<64, false>); }
+#define XDDP_FA(D_, C_) \
+  if (kwv == 4) go(fa_bwd_dkdv_kernel<D_, C_, 4>); else go(fa_bwd_dkdv_kernel<D_, C_, 2>)
+    if (D == 128) { if (causal) { XDDP_FA(128, true); } else { XDDP_FA(128, false); } }
+    else { if (causal) { XDDP_FA(64, true); } else { XDDP_FA(64, false); } }
+#undef XDDP_FA
   }
   return {dq, dk, dv};
 }
