@@ -428,7 +428,8 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq, int Sk, int Hq, int Hkv, Strides qs, Strides ks,
-    Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale) {
+    Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale, int nsplit,
+    float* __restrict__ wsk, float* __restrict__ wsv) {
   constexpr int NG = 8 / KW, BK = 32 * KW;          // groups; keys per workgroup
   constexpr int KS = D / 16, NT = D / 32, QB = 32;  // query rows per work item
   constexpr int TILE = QB * D * 2;                  // bytes of one Q (or dO) tile
@@ -440,10 +441,14 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
   static_assert((NG - 1) * KW * ACC * 4 <= VBLK + 2 * NG * STAGE, "group reduction must fit the LDS");
   __shared__ __attribute__((aligned(16))) uint8_t smem[VBLK + 2 * NG * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wq = w % KW, G = w / KW, g = lane >> 5;
-  const int bhk = blockIdx.y, b = bhk / Hkv, hk = bhk % Hkv, grp = Hq / Hkv;
-  // causal: low key blocks see the most query tiles — dispatched first (pairing blocks per
-  // workgroup would halve the grid below the CU count at the Llama shape)
-  const int kb = (int)blockIdx.x;
+  // blockIdx.x = (batch, kv head, head split), blockIdx.y = key block: the dispatcher walks x
+  // first, so every workgroup of key block 0 (the heaviest under a causal mask) starts first.
+  // nsplit > 1 splits the query heads of a GQA group over workgroups (fp32 partial dK/dV summed
+  // by fa_dkdv_sum_kernel): 4x the workgroups, each a quarter of the work, so the heavy-first
+  // dispatch balances the CUs (one workgroup per (key block, kv head) left a 2x work spread).
+  const int split = (int)blockIdx.x % nsplit, bhk = (int)blockIdx.x / nsplit;
+  const int b = bhk / Hkv, hk = bhk % Hkv, grp = Hq / Hkv, hpw = grp / nsplit;
+  const int kb = (int)blockIdx.y;
   const int k0 = kb * BK, kw = k0 + 32 * wq, krow = kw + (lane & 31);
   uint8_t* Vblk = smem;
   {  // V rows [k0, k0 + BK) -> LDS (rows past Sk read row Sk - 1; their P, dS are masked to 0)
@@ -470,10 +475,10 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
     for (int i = 0; i < 16; ++i) adk[n][i] = adv[n][i] = 0.f;
   const int qstart = CAUSAL ? (k0 / QB) * QB : 0;
   const int nqt = (Sq - qstart + QB - 1) / QB;
-  const int total = grp * nqt, niter = (total + NG - 1) / NG;
+  const int total = hpw * nqt, niter = (total + NG - 1) / NG;
   uint8_t* gsm = smem + VBLK + G * 2 * STAGE;
   auto issue = [&](int it, int st) {  // rows past Sq read row Sq - 1 (masked below)
-    const int h = hk * grp + it / nqt, qt0 = qstart + (it % nqt) * QB;
+    const int h = hk * grp + split * hpw + it / nqt, qt0 = qstart + (it % nqt) * QB;
     uint8_t* S = gsm + st * STAGE;
     const uint16_t* Qb = Q + b * qs.b + h * qs.h;
     const uint16_t* Db = dO + b * dos.b + h * dos.h;
@@ -566,6 +571,21 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
     }
   }
   if (G != 0 || krow >= Sk) return;
+  if (nsplit > 1) {  // fp32 partials [split][B][Sk][Hkv][D], summed (and dK scaled) later
+    const int64_t base = ((((int64_t)split * (gridDim.x / nsplit) + bhk) / Hkv * Sk + krow) * Hkv + hk) * D;
+    float* pk = wsk + base;
+    float* pv = wsv + base;
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        *reinterpret_cast<float4*>(pk + 32 * n + 4 * g + 8 * q) =
+            make_float4(adk[n][4 * q], adk[n][4 * q + 1], adk[n][4 * q + 2], adk[n][4 * q + 3]);
+        *reinterpret_cast<float4*>(pv + 32 * n + 4 * g + 8 * q) =
+            make_float4(adv[n][4 * q], adv[n][4 * q + 1], adv[n][4 * q + 2], adv[n][4 * q + 3]);
+      }
+    return;
+  }
   uint16_t* ok = dK + b * dks.b + hk * dks.h + (int64_t)krow * dks.s;
   uint16_t* ov = dV + b * dvs.b + hk * dvs.h + (int64_t)krow * dvs.s;
 #pragma unroll
@@ -580,6 +600,34 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
       *reinterpret_cast<uint2*>(ok + 32 * n + 4 * g + 8 * q) = a;
       *reinterpret_cast<uint2*>(ov + 32 * n + 4 * g + 8 * q) = c;
     }
+}
+
+// dK = scale · sum_s wsk[s], dV = sum_s wsv[s] (fp32 head-split partials, [nsplit][B·Sk·Hkv·D]);
+// 8 elements per thread, output [B, Sk, Hkv, D] contiguous
+__global__ __launch_bounds__(256) void fa_dkdv_sum_kernel(const float* __restrict__ wsk, const float* __restrict__ wsv,
+                                                          uint16_t* __restrict__ dK, uint16_t* __restrict__ dV,
+                                                          int64_t n8, int nsplit, float scale) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  float k[8] = {0, 0, 0, 0, 0, 0, 0, 0}, v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int sp = 0; sp < nsplit; ++sp) {
+    const float4* a = reinterpret_cast<const float4*>(wsk + ((int64_t)sp * n8 + i) * 8);
+    const float4* c = reinterpret_cast<const float4*>(wsv + ((int64_t)sp * n8 + i) * 8);
+    const float4 a0 = a[0], a1 = a[1], c0 = c[0], c1 = c[1];
+    k[0] += a0.x; k[1] += a0.y; k[2] += a0.z; k[3] += a0.w; k[4] += a1.x; k[5] += a1.y; k[6] += a1.z; k[7] += a1.w;
+    v[0] += c0.x; v[1] += c0.y; v[2] += c0.z; v[3] += c0.w; v[4] += c1.x; v[5] += c1.y; v[6] += c1.z; v[7] += c1.w;
+  }
+  uint4 ko, vo;
+  ko.x = dev::pack_bf16x2(k[0] * scale, k[1] * scale);
+  ko.y = dev::pack_bf16x2(k[2] * scale, k[3] * scale);
+  ko.z = dev::pack_bf16x2(k[4] * scale, k[5] * scale);
+  ko.w = dev::pack_bf16x2(k[6] * scale, k[7] * scale);
+  vo.x = dev::pack_bf16x2(v[0], v[1]);
+  vo.y = dev::pack_bf16x2(v[2], v[3]);
+  vo.z = dev::pack_bf16x2(v[4], v[5]);
+  vo.w = dev::pack_bf16x2(v[6], v[7]);
+  reinterpret_cast<uint4*>(dK)[i] = ko;
+  reinterpret_cast<uint4*>(dV)[i] = vo;
 }
 
 Strides strides_of(const at::Tensor& t) { return Strides{t.stride(0), t.stride(1), t.stride(2)}; }
@@ -699,14 +747,30 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
     }();
     const int kwv = kw_env == 2 ? 2 : 4;
     const int nkb = (int)((Sk + 32 * kwv - 1) / (32 * kwv));
-    const dim3 grid((unsigned)nkb, (unsigned)(B * Hkv));
+    // GQA head split for causal attention (balance, see the kernel); XDDP_FA_DKDV_SPLIT overrides
+    static const int split_env = [] {
+      const char* e = std::getenv("XDDP_FA_DKDV_SPLIT");
+      return e ? std::atoi(e) : 0;
+    }();
+    const int grp = (int)(Hq / Hkv);
+    int nsplit = causal ? grp : 1;
+    if (split_env > 0) nsplit = split_env;
+    if (nsplit < 1 || grp % nsplit != 0) nsplit = 1;
+    at::Tensor wsk, wsv;
+    if (nsplit > 1) {
+      wsk = at::empty({nsplit, B, Sk, Hkv, D}, q.options().dtype(at::kFloat));
+      wsv = at::empty({nsplit, B, Sk, Hkv, D}, q.options().dtype(at::kFloat));
+    }
+    const dim3 grid((unsigned)(B * Hkv * nsplit), (unsigned)nkb);
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, grid, dim3(512), 0, stream, reinterpret_cast<const uint16_t*>(q.data_ptr()),
                          reinterpret_cast<const uint16_t*>(k.data_ptr()), reinterpret_cast<const uint16_t*>(v.data_ptr()),
                          reinterpret_cast<const uint16_t*>(dout.data_ptr()), lse.data_ptr<float>(),
                          delta.data_ptr<float>(), reinterpret_cast<uint16_t*>(dk.data_ptr()),
                          reinterpret_cast<uint16_t*>(dv.data_ptr()), (int)Sq, (int)Sk, (int)Hq, (int)Hkv, strides_of(q),
-                         strides_of(k), strides_of(v), strides_of(dout), strides_of(dk), strides_of(dv), sl2, sc);
+                         strides_of(k), strides_of(v), strides_of(dout), strides_of(dk), strides_of(dv), sl2, sc,
+                         nsplit, nsplit > 1 ? wsk.data_ptr<float>() : nullptr,
+                         nsplit > 1 ? wsv.data_ptr<float>() : nullptr);
       XDDP_HIP_CHECK(hipGetLastError());
     };
 #define XDDP_FA(D_, C_) \
@@ -714,6 +778,13 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
     if (D == 128) { if (causal) { XDDP_FA(128, true); } else { XDDP_FA(128, false); } }
     else { if (causal) { XDDP_FA(64, true); } else { XDDP_FA(64, false); } }
 #undef XDDP_FA
+    if (nsplit > 1) {
+      const int64_t n8 = B * Sk * Hkv * D / 8;
+      hipLaunchKernelGGL(fa_dkdv_sum_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, stream,
+                         wsk.data_ptr<float>(), wsv.data_ptr<float>(), reinterpret_cast<uint16_t*>(dk.data_ptr()),
+                         reinterpret_cast<uint16_t*>(dv.data_ptr()), n8, nsplit, sc);
+      XDDP_HIP_CHECK(hipGetLastError());
+    }
   }
   return {dq, dk, dv};
 }
