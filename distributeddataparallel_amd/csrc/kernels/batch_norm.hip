@@ -343,29 +343,63 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
 
 // per channel: dgamma, dbeta; dx = k1*dy_eff + k2*(x-mean) + k3. Same single-wave shape as the
 // stats finalize: lanes stride over row-block partials, then a shuffle butterfly.
+// 16 per-lane sums reduced over a wave in 17 shuffles (halving butterfly: each exchange step
+// trades half of the live values, so lane l ends holding the wave total of value index
+// 8·b5 + 4·b4 + 2·b3 + b2, where b_k is bit k of l; every group of 4 lanes holds the same one).
+__device__ __forceinline__ float wave_reduce16(float (&v)[16], int lane) {
+#pragma unroll
+  for (int step = 0, width = 8; step < 4; ++step, width >>= 1) {
+    const int o = 32 >> step;
+    const bool hi = lane & o;
+#pragma unroll
+    for (int i = 0; i < width; ++i) {
+      const float send = hi ? v[i] : v[i + width];
+      const float recv = __shfl_xor(send, o, 64);
+      v[i] = (hi ? v[i + width] : v[i]) + recv;
+    }
+  }
+  float r = v[0];
+  r += __shfl_xor(r, 2, 64);
+  r += __shfl_xor(r, 1, 64);
+  return r;
+}
+
+// per channel: dgamma, dbeta; dx = k1*dy_eff + k2*(x-mean) + k3. One 256-thread block per
+// 8-channel vector: threads stride over the row-block partials (16 floats each, 4 float4 loads),
+// the 16 sums reduce per wave in 17 shuffles, then across the 4 waves through LDS.
 template <typename W>
-__global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(const float* __restrict__ part, int rblocks, int C,
-                                                             int64_t M, const W* __restrict__ weight,
-                                                             const float* __restrict__ invstd, W* dweight,
-                                                             W* dbias, float* __restrict__ coef,
-                                                             const float* __restrict__ fold_mean) {
-  const int cv = blockIdx.x, lane = threadIdx.x;
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int rblocks, int C,
+                                                              int64_t M, const W* __restrict__ weight,
+                                                              const float* __restrict__ invstd, W* dweight,
+                                                              W* dbias, float* __restrict__ coef,
+                                                              const float* __restrict__ fold_mean) {
+  __shared__ float red[4][16];
+  const int cv = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   float acc[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-  for (int b = lane; b < rblocks; b += 64) {
-    const float* p = part + ((int64_t)b * C + cv * 8) * 2;
+#pragma unroll 2
+  for (int b = tid; b < rblocks; b += 256) {
+    const float4* p = reinterpret_cast<const float4*>(part + ((int64_t)b * C + cv * 8) * 2);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[j] += p[j];
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = p[q];
+      acc[4 * q] += v.x;
+      acc[4 * q + 1] += v.y;
+      acc[4 * q + 2] += v.z;
+      acc[4 * q + 3] += v.w;
+    }
   }
-#pragma unroll
-  for (int j = 0; j < 16; ++j) acc[j] = dev::wave_sum(acc[j]);
-  if (lane >= 8) return;
-  float sd = acc[0], sdx = acc[1];
-#pragma unroll
-  for (int j = 1; j < 8; ++j)
-    if (lane == j) { sd = acc[2 * j]; sdx = acc[2 * j + 1]; }
-  const int c = cv * 8 + lane;
+  const float r = wave_reduce16(acc, lane);
+  if ((lane & 3) == 0) {
+    const int j = ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
+    red[wid][j] = r;
+  }
+  __syncthreads();
+  if (tid >= 8) return;
+  const float sd = (red[0][2 * tid] + red[1][2 * tid]) + (red[2][2 * tid] + red[3][2 * tid]);
+  const float sdx = (red[0][2 * tid + 1] + red[1][2 * tid + 1]) + (red[2][2 * tid + 1] + red[3][2 * tid + 1]);
+  const int c = cv * 8 + tid;
   const float inv = invstd[c];
   const float g = weight ? Elem<W, float>::ld(weight, c) : 1.f;
   if (dweight) Elem<W, float>::st(dweight, c, sdx * inv);
@@ -693,7 +727,7 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
       else { XDDP_BN_RED(0) }
 #undef XDDP_BN_RED
       XDDP_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(64), 0, stream,
+      hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(256), 0, stream,
                          part.data_ptr<float>(), g.rblocks, (int)C, M,
                          has_w ? reinterpret_cast<const W*>(weight->data_ptr()) : nullptr, invstd.data_ptr<float>(),
                          dw.defined() ? reinterpret_cast<W*>(dw.data_ptr()) : nullptr,
@@ -750,7 +784,7 @@ std::vector<at::Tensor> bn_backward_from_partials(const at::Tensor& part, int64_
   at::Tensor db = (has_w && need_dweight) ? at::empty({C}, weight->options()) : at::Tensor();
   dispatch_w(wdt, [&](auto tag_w) {
     using W = decltype(tag_w);
-    hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(64), 0, stream, part.data_ptr<float>(),
+    hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(256), 0, stream, part.data_ptr<float>(),
                        (int)part.size(0), (int)C, M, has_w ? reinterpret_cast<const W*>(weight->data_ptr()) : nullptr,
                        invstd.data_ptr<float>(), dw.defined() ? reinterpret_cast<W*>(dw.data_ptr()) : nullptr,
                        db.defined() ? reinterpret_cast<W*>(db.data_ptr()) : nullptr, coef.data_ptr<float>(),

@@ -452,11 +452,14 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
   }
 }
 
-// Per channel: Chan-merge the groups' (count, mean, M2), then the BN coefficients and the
-// running-stat update (same outputs as the stats finalize of batch_norm.hip). One 256-thread
-// block per channel: threads stride over the groups (element (g, q, c) at g*gs + q*ks + c*cs, so
-// both the [groups][3][C] and the group-minor [3][C][groups] layouts are read), then a shuffle
-// butterfly of pairwise merges per wave and a 4-way merge through LDS.
+// Per channel: merge the groups' (count, mean, M2), then the BN coefficients and the running-stat
+// update (same outputs as the stats finalize of batch_norm.hip). One 256-thread block per
+// channel: threads stride over the groups (element (g, q, c) at g*gs + q*ks + c*cs, so both the
+// [groups][3][C] and the group-minor [3][C][groups] layouts are read). The merge is the shifted
+// form of Chan's: with K = group 0's mean (a sample of this channel's mean, so |mean_g - K| is
+// O(std) and nothing cancels), sum n_g, n_g·(mean_g - K) and M2_g + n_g·(mean_g - K)^2 — plain
+// adds, no division per group, so a thread's loads are independent and issue together (the
+// divide-per-merge chain made this launch latency-bound: 6-12 us at 64-3136 groups).
 template <typename W>
 __global__ __launch_bounds__(256) void bn_partial_finalize_kernel(
     const float* __restrict__ part, int groups, int C, int64_t gs, int64_t ks, int64_t cs, int64_t M,
@@ -466,46 +469,32 @@ __global__ __launch_bounds__(256) void bn_partial_finalize_kernel(
   __shared__ float red[3][4];
   const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float* pc = part + (int64_t)c * cs;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
+  const float K = pc[ks];  // group 0's mean (group 0 always holds rows)
+  float n = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll 4
   for (int gi = tid; gi < groups; gi += 256) {
     const float* q = pc + (int64_t)gi * gs;
-    const float nb = q[0], mb = q[ks], m2b = q[2 * ks];
-    const float nn = n + nb;
-    if (nb > 0.f) {
-      const float d = mb - mean;
-      mean += d * (nb / nn);
-      m2 += m2b + d * d * (n * nb / nn);
-      n = nn;
-    }
+    const float nb = q[0], d = q[ks] - K, m2b = q[2 * ks];
+    n += nb;
+    s1 = fmaf(nb, d, s1);
+    s2 += fmaf(nb * d, d, m2b);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float nb = __shfl_xor(n, o, 64), mb = __shfl_xor(mean, o, 64), m2b = __shfl_xor(m2, o, 64);
-    const float nn = n + nb;
-    if (nn > 0.f) {
-      const float d = mb - mean;
-      mean += d * (nb / nn);
-      m2 += m2b + d * d * (n * nb / nn);
-    }
-    n = nn;
-  }
+  n = dev::wave_sum(n);
+  s1 = dev::wave_sum(s1);
+  s2 = dev::wave_sum(s2);
   if (lane == 0) {
     red[0][wid] = n;
-    red[1][wid] = mean;
-    red[2][wid] = m2;
+    red[1][wid] = s1;
+    red[2][wid] = s2;
   }
   __syncthreads();
   if (tid != 0) return;
-  n = mean = m2 = 0.f;
-  for (int w = 0; w < 4; ++w) {
-    const float nb = red[0][w], nn = n + nb;
-    if (nb > 0.f) {
-      const float d = red[1][w] - mean;
-      mean += d * (nb / nn);
-      m2 += red[2][w] + d * d * (n * nb / nn);
-      n = nn;
-    }
-  }
+  n = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  s1 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  s2 = (red[2][0] + red[2][1]) + (red[2][2] + red[2][3]);
+  const float dm = n > 0.f ? s1 / n : 0.f;
+  const float mean = K + dm;
+  const float m2 = fmaxf(s2 - s1 * dm, 0.f);
   const float var = fmaxf(m2 / (float)M, 0.f);
   const float inv = rsqrtf(var + eps);
   mean_out[c] = mean;
