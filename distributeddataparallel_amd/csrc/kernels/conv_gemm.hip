@@ -687,6 +687,193 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
       }
 }
 
+// Fused backward of a stride-1 1x1 conv whose output gradient dY = k1·G + k2·Y2 + k3 is formed
+// while staging (the BN backward folded in, PRO 2 / 3 as above): the input gradient dX = dY·W
+// and the weight gradient dW = dYᵀ·X computed from ONE staging of the dY tile. The separate
+// dgrad GEMM and wgrad kernel each read G and Y2 (the two largest tensors of the layer): at
+// ResNet-50 layer-1 shapes (M = 802816, N·K = 256·64) both sit at the HBM roofline, so sharing
+// the read removes a third of the layer's backward traffic.
+// One block per CU walks a contiguous pixel range in 64-row steps (two LDS buffers, next step's
+// loads in flight): wgrad as conv1x1_wgrad_kernel with the whole N x K as one tile (fp32 slab
+// per block, summed by wgrad_reduce_kernel); dgrad on the same step, swapped (dXᵀ = Wᵀ·dYᵀ:
+// A = Wᵀ by transposed reads of W [N][K] kept in LDS, B = dY rows), so a lane ends with 4
+// consecutive input channels of one pixel — one 8-B store.
+template <int N, int K, int PRO>
+__global__ __launch_bounds__(256, 1) void conv1x1_bwd_fused_kernel(
+    const uint16_t* __restrict__ G, const uint16_t* __restrict__ Y2, const float* __restrict__ coef,
+    const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wg, uint16_t* __restrict__ dX, float* __restrict__ ws,
+    int M, int mchunk) {
+  constexpr int BM = 64;
+  constexpr int SA = N * 2 + 32, SB = K * 2 + 32, SW = K * 2 + 32;
+  constexpr int ABYTES = BM * SA, BUF = ABYTES + BM * SB;
+  constexpr int CA = N / 8, CB = K / 8;
+  constexpr int LA = BM * CA / 256, LB = BM * CB / 256;
+  constexpr int WTN = N / 2, WTK = K / 2, FN = WTN / 16, FK = WTK / 16;  // wgrad wave tile (2 x 2 waves)
+  constexpr int KW = K / 4, KF = KW / 16;                                // dgrad: k rows per wave
+  static_assert(256 % CA == 0 && LA >= 1 && LB >= 1 && KF >= 1, "fused 1x1 backward tile");
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* Wl = smem + 2 * BUF;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wn = wid >> 1, wk = wid & 1;
+  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
+  const int m_begin = bid * mchunk, m_end = min(M, m_begin + mchunk);
+
+  // W [N][K] -> LDS rows (padded for the transposed reads)
+  for (int q = tid; q < N * CB; q += 256) {
+    const int n = q / CB, c = q % CB;
+    *reinterpret_cast<u32x4*>(Wl + n * SW + c * 16) = *reinterpret_cast<const u32x4*>(Wg + (int64_t)n * K + c * 8);
+  }
+  float pa[8], pb[8], pc[8], pms[8], pmt[8];  // this thread's 8 dY channels (fixed: 256 % CA == 0)
+  {
+    const int c = tid % CA;
+    dev::Vec8<float>::ld(coef + c * 8, pa);
+    dev::Vec8<float>::ld(coef + N + c * 8, pb);
+    dev::Vec8<float>::ld(coef + 2 * N + c * 8, pc);
+    if (PRO == 3) {
+      dev::Vec8<float>::ld(coef + 3 * N + c * 8, pms);
+      dev::Vec8<float>::ld(coef + 4 * N + c * 8, pmt);
+    }
+  }
+  u32x4 sa[LA], sa2[LA], sb[LB];
+  auto load = [&](int m) {
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int q = tid + 256 * i, row = q / CA, c = q - (q / CA) * CA;
+      const int64_t off = (int64_t)min(m + row, M - 1) * N + c * 8;
+      sa[i] = *reinterpret_cast<const u32x4*>(G + off);
+      sa2[i] = *reinterpret_cast<const u32x4*>(Y2 + off);
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int q = tid + 256 * i, row = q / CB, c = q - (q / CB) * CB;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(X + (int64_t)min(m + row, M - 1) * K + c * 8);
+      sb[i] = m + row < m_end ? v : u32x4{0, 0, 0, 0};
+    }
+  };
+  auto store = [&](int buf, int m) {
+    uint8_t* A = smem + buf * BUF;
+    uint8_t* B = A + ABYTES;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int q = tid + 256 * i, row = q / CA, c = q - (q / CA) * CA;
+      u32x4 t;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        float g0 = __uint_as_float(sa[i][h] << 16), g1 = __uint_as_float(sa[i][h] & 0xffff0000u);
+        const float x0 = __uint_as_float(sa2[i][h] << 16), x1 = __uint_as_float(sa2[i][h] & 0xffff0000u);
+        if (PRO == 3) {
+          g0 = fmaf(x0, pms[2 * h], pmt[2 * h]) > 0.f ? g0 : 0.f;
+          g1 = fmaf(x1, pms[2 * h + 1], pmt[2 * h + 1]) > 0.f ? g1 : 0.f;
+        }
+        t[h] = dev::pack_bf16x2(fmaf(pa[2 * h], g0, fmaf(pb[2 * h], x0, pc[2 * h])),
+                                fmaf(pa[2 * h + 1], g1, fmaf(pb[2 * h + 1], x1, pc[2 * h + 1])));
+      }
+      *reinterpret_cast<u32x4*>(A + row * SA + c * 16) = m + row < m_end ? t : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int q = tid + 256 * i, row = q / CB, c = q - (q / CB) * CB;
+      *reinterpret_cast<u32x4*>(B + row * SB + c * 16) = sb[i];
+    }
+  };
+
+  f32x4 acc[FN][FK];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  if (m_begin < m_end) {
+    load(m_begin);
+    store(0, m_begin);
+    lds_barrier();
+    int cur = 0;
+    for (int m = m_begin; m < m_end; m += BM) {
+      const bool more = m + BM < m_end;
+      if (more) load(m + BM);  // in flight during the MFMAs below
+      const uint8_t* A = smem + cur * BUF;
+      const uint8_t* B = A + ABYTES;
+      // ---- wgrad: acc[n][k] += dYᵀ·X over this step's 64 pixel rows
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int r0 = s2 * 32 + 8 * g + q4;
+        bf16x8 a[FN], b[FK];
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const int col = wn * WTN + i * 16 + 4 * p4;
+          const v4s v8[2] = {lds_tr16(A + r0 * SA + col * 2), lds_tr16(A + (r0 + 4) * SA + col * 2)};
+          a[i] = __builtin_bit_cast(bf16x8, v8);
+        }
+#pragma unroll
+        for (int j = 0; j < FK; ++j) {
+          const int col = wk * WTK + j * 16 + 4 * p4;
+          const v4s v8[2] = {lds_tr16(B + r0 * SB + col * 2), lds_tr16(B + (r0 + 4) * SB + col * 2)};
+          b[j] = __builtin_bit_cast(bf16x8, v8);
+        }
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+      // ---- dgrad: dXᵀ[k][m] = Σ_n W[n][k]·dY[m][n] for this step's rows; wave owns k rows wid·KW..
+      {
+        f32x4 d[KF][4];
+#pragma unroll
+        for (int kf = 0; kf < KF; ++kf)
+#pragma unroll
+          for (int mf = 0; mf < 4; ++mf) d[kf][mf] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+        for (int ns = 0; ns < N / 32; ++ns) {
+          const int r0 = ns * 32 + 8 * g + q4;
+          bf16x8 a[KF], b[4];
+#pragma unroll
+          for (int kf = 0; kf < KF; ++kf) {
+            const int col = wid * KW + kf * 16 + 4 * p4;
+            const v4s v8[2] = {lds_tr16(Wl + r0 * SW + col * 2), lds_tr16(Wl + (r0 + 4) * SW + col * 2)};
+            a[kf] = __builtin_bit_cast(bf16x8, v8);
+          }
+#pragma unroll
+          for (int mf = 0; mf < 4; ++mf)
+            b[mf] = *reinterpret_cast<const bf16x8*>(A + (mf * 16 + (lane & 15)) * SA + (ns * 32 + 8 * g) * 2);
+#pragma unroll
+          for (int kf = 0; kf < KF; ++kf)
+#pragma unroll
+            for (int mf = 0; mf < 4; ++mf) d[kf][mf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kf], b[mf], d[kf][mf], 0, 0, 0);
+        }
+        // lane: k = wid·KW + kf·16 + 4g + r (r = 0..3), pixel m + mf·16 + (lane & 15)
+#pragma unroll
+        for (int mf = 0; mf < 4; ++mf) {
+          const int mm = m + mf * 16 + (lane & 15);
+          if (mm < m_end) {
+#pragma unroll
+            for (int kf = 0; kf < KF; ++kf) {
+              uint2 pk;
+              pk.x = dev::pack_bf16x2(d[kf][mf][0], d[kf][mf][1]);
+              pk.y = dev::pack_bf16x2(d[kf][mf][2], d[kf][mf][3]);
+              *reinterpret_cast<uint2*>(dX + (int64_t)mm * K + wid * KW + kf * 16 + 4 * g) = pk;
+            }
+          }
+        }
+      }
+      if (more) store(cur ^ 1, m + BM);
+      lds_barrier();
+      cur ^= 1;
+    }
+  }
+  float* out = ws + (int64_t)bid * N * K;
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = wn * WTN + i * 16 + (lane >> 4) * 4 + r;
+        const int k = wk * WTK + j * 16 + (lane & 15);
+        out[(int64_t)n * K + k] = acc[i][j][r];
+      }
+}
+
 // dW = sum over the S slabs, cast to the weight dtype; 4 elements per lane.
 template <typename W>
 __global__ __launch_bounds__(512) void wgrad_reduce_kernel(const float* __restrict__ ws, int S, int64_t nk,
@@ -937,6 +1124,59 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stri
     default: TORCH_CHECK(false, "conv1x1_wgrad: unsupported weight dtype");
   }
   return dw;
+}
+
+// Fused stride-1 1x1 backward (see conv1x1_bwd_fused_kernel): g, y2 [B, N, H, W], coef [3|5, N]
+// (dY = k1·g + k2·y2 + k3', with the ReLU mask recomputed from y2 for 5 rows), x [B, K, H, W],
+// w [N, K, 1, 1] -> (dx [B, K, H, W], dw like w). (N, K) in {(256, 64), (64, 256)}.
+bool conv1x1_bwd_fused_supported(int64_t N, int64_t K) { return (N == 256 && K == 64) || (N == 64 && K == 256); }
+
+std::vector<at::Tensor> conv1x1_bwd_fused(const at::Tensor& g, const at::Tensor& y2, const at::Tensor& coef,
+                                          const at::Tensor& x, const at::Tensor& w) {
+  TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kBFloat16 && g.dim() == 4 &&
+                  g.is_contiguous(at::MemoryFormat::ChannelsLast) && y2.sizes() == g.sizes() &&
+                  y2.scalar_type() == at::kBFloat16 && y2.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv1x1_bwd_fused: g, y2 must be matching bf16 channels_last tensors");
+  const int64_t B = x.size(0), K = x.size(1), H = x.size(2), Wd = x.size(3), N = g.size(1);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  g.size(0) == B && g.size(2) == H && g.size(3) == Wd,
+              "conv1x1_bwd_fused: x must be bf16 channels_last with g's batch and spatial size (stride 1)");
+  TORCH_CHECK(conv1x1_bwd_fused_supported(N, K), "conv1x1_bwd_fused: unsupported (N, K)");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.numel() == N * K && w.size(0) == N && w.is_contiguous(),
+              "conv1x1_bwd_fused: w must be contiguous bf16 [N, K, 1, 1]");
+  const int pro = coef.numel() == 5 * N ? 3 : 2;
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.is_contiguous() && (coef.numel() == 3 * N || pro == 3),
+              "conv1x1_bwd_fused: coef must be float [3|5, N]");
+  const int64_t M = B * H * Wd;
+  TORCH_CHECK(M > 0 && M < (int64_t(1) << 31), "conv1x1_bwd_fused: bad M");
+  const int64_t steps = (M + 63) / 64;
+  int S = (int)std::max<int64_t>(1, std::min<int64_t>(steps, (int64_t)num_cus()));
+  const int64_t mchunk = ((steps + S - 1) / S) * 64;
+  S = (int)((M + mchunk - 1) / mchunk);
+  auto dx = at::empty({B, K, H, Wd}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto ws = at::empty({S, N, K}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({N, K, 1, 1}, w.options().memory_format(at::MemoryFormat::Contiguous));
+  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  const size_t lds = 2 * (size_t)64 * ((N * 2 + 32) + (K * 2 + 32)) + (size_t)N * (K * 2 + 32);
+  auto go = [&](auto kern) {
+    static size_t lds_set = 0;
+    if (lds > 65536 && lds > lds_set) {
+      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      lds_set = lds;
+    }
+    hipLaunchKernelGGL(kern, dim3(S), dim3(256), lds, stream, reinterpret_cast<const uint16_t*>(g.data_ptr()),
+                       reinterpret_cast<const uint16_t*>(y2.data_ptr()), coef.data_ptr<float>(),
+                       reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                       reinterpret_cast<uint16_t*>(dx.data_ptr()), ws.data_ptr<float>(), (int)M, (int)mchunk);
+    XDDP_HIP_CHECK(hipGetLastError());
+  };
+  if (N == 256) { if (pro == 3) go(conv1x1_bwd_fused_kernel<256, 64, 3>); else go(conv1x1_bwd_fused_kernel<256, 64, 2>); }
+  else { if (pro == 3) go(conv1x1_bwd_fused_kernel<64, 256, 3>); else go(conv1x1_bwd_fused_kernel<64, 256, 2>); }
+  const int64_t nk = N * K;
+  hipLaunchKernelGGL((wgrad_reduce_kernel<dev::bf16_t>), dim3((unsigned)((nk / 4 + 63) / 64)), dim3(512), 0, stream,
+                     ws.data_ptr<float>(), S, nk, reinterpret_cast<dev::bf16_t*>(dw.data_ptr()));
+  XDDP_HIP_CHECK(hipGetLastError());
+  return {dx, dw};
 }
 
 // 3x3 (pad 1, stride 1/2) weight gradient: dy [B, N, OH, OW], x [B, C, IH, IW] (bf16

@@ -49,6 +49,10 @@ at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_
                                int64_t splits = -1);
 at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,
                          const c10::optional<at::Tensor>& prologue_y, const c10::optional<at::Tensor>& coef);
+// stride-1 1x1 input + weight gradient from one staging of dY = k1·g + k2·y2 + k3' (conv_gemm.hip)
+bool conv1x1_bwd_fused_supported(int64_t N, int64_t K);
+std::vector<at::Tensor> conv1x1_bwd_fused(const at::Tensor& g, const at::Tensor& y2, const at::Tensor& coef,
+                                          const at::Tensor& x, const at::Tensor& w);
 std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M,
                                                const c10::optional<at::Tensor>& weight,
                                                const c10::optional<at::Tensor>& bias,

@@ -30,6 +30,9 @@ void bind_norm_kernels(py::module_& m) {
   m.def("conv3x3_wgrad", &conv3x3_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"));
   m.def("conv3x3_wgrad_patch", &conv3x3_wgrad_patch, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"),
         py::arg("splits") = -1);
+  m.def("conv1x1_bwd_fused_supported", &conv1x1_bwd_fused_supported, py::arg("N"), py::arg("K"));
+  m.def("conv1x1_bwd_fused", &conv1x1_bwd_fused, py::arg("g"), py::arg("y2"), py::arg("coef"), py::arg("x"),
+        py::arg("w"));
   m.def("conv1x1_wgrad", &conv1x1_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"),
         py::arg("prologue_y") = py::none(), py::arg("coef") = py::none());
   m.def("bn_stats_from_partials", &bn_stats_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),

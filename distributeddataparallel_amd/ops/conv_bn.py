@@ -128,9 +128,11 @@ class _Conv1x1BN(torch.autograd.Function):
             g = dout
             dres = g if need_dres else None
             dx = dw = None
-            if s == 1 and need_x and _dgrad_gemm():
+            if s == 1 and need_x and need_w and _bwd_fused_ok(ctx, C, w):
+                dx, dw = C.conv1x1_bwd_fused(g, y, coef, x, w)
+            if s == 1 and need_x and dx is None and _dgrad_gemm():
                 dx = _dgrad_in(ctx, C, g, w, coef, y)
-            if need_w and s == 1 and _wgrad_gemm():
+            if need_w and dw is None and s == 1 and _wgrad_gemm():
                 dw = C.conv1x1_wgrad(g, x, 1, w, y, coef)
             if (need_x and dx is None) or (need_w and dw is None):
                 v = lambda i: coef[i].view(1, -1, 1, 1)  # noqa: E731
@@ -151,8 +153,11 @@ class _Conv1x1BN(torch.autograd.Function):
             coef, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu, need_dres,
                                                      need_bn_w, dout2, bits, True)
             g = dres if need_dres else dout.contiguous(memory_format=torch.channels_last)
-            dx = _dgrad_in(ctx, C, g, w, coef, y)
-            dw = C.conv1x1_wgrad(g, x, 1, w, y, coef)
+            if _bwd_fused_ok(ctx, C, w):
+                dx, dw = C.conv1x1_bwd_fused(g, y, coef, x, w)
+            else:
+                dx = _dgrad_in(ctx, C, g, w, coef, y)
+                dw = C.conv1x1_wgrad(g, x, 1, w, y, coef)
             return _grads(ctx, dx, dw, dw_bn, db_bn, dres)
         dy, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu, need_dres,
                                                need_bn_w, dout2, bits)
@@ -189,6 +194,19 @@ def _grads(ctx, dx, dw, dw_bn, db_bn, dres):
     return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
             None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None, None, None, None,
             None)
+
+
+def _bwd_fused_ok(ctx, C, w) -> bool:
+    """Input and weight gradient of a stride-1 1x1 conv from one staging of its BN-backward dY
+    (``conv1x1_bwd_fused``): the ResNet-50 layer-1 shapes (N, K) = (256, 64), (64, 256), where
+    both gradient kernels sit at the HBM roofline reading the same two tensors.
+    XDDP_CONV_BWD_FUSED=0 keeps the two separate kernels (A/B switch)."""
+    if os.environ.get("XDDP_CONV_BWD_FUSED", "1") == "0":
+        return False
+    if ctx.link_in is not None and _epi() and os.environ.get("XDDP_CONV_EPI2", "0") == "1":
+        return False  # the dgrad epilogue has extra work to do there
+    return (w.dtype == torch.bfloat16 and w.is_contiguous() and w.shape[2] == 1 and w.shape[3] == 1
+            and C.conv1x1_bwd_fused_supported(w.shape[0], w.shape[1]))
 
 
 def _dgrad_in(ctx, C, g, w, coef, y):

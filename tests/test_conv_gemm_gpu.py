@@ -319,3 +319,42 @@ def test_bottleneck_bn2_fold_matches_separate_pass(monkeypatch):
     assert abs(l1 - l0) < 1e-6 * max(1.0, abs(l0))
     assert ((g1 - g0).norm() / g0.norm()).item() < 2e-2
     assert F.cosine_similarity(g1, g0, dim=0).item() > 0.999
+
+
+@pytest.mark.parametrize("N,K,pro", [(256, 64, 2), (256, 64, 3), (64, 256, 2), (64, 256, 3)])
+def test_conv1x1_bwd_fused_matches_separate_kernels(N, K, pro):
+    """conv1x1_bwd_fused (dgrad + wgrad from one staging of dY = k1·g + k2·y2 + k3') equals the
+    separate dgrad GEMM + wgrad kernel on the same prologue, and the fp32 math of dY."""
+    from distributeddataparallel_amd._native import load
+
+    C = load()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    B, H, W = 3, 55, 57  # M = 9405: a partial last 64-row step
+    cl = torch.channels_last
+    gr = torch.randn(B, N, H, W, device="cuda", generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    y2 = torch.randn(B, N, H, W, device="cuda", generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    x = torch.randn(B, K, H, W, device="cuda", generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (torch.randn(N, K, 1, 1, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    rows = 5 if pro == 3 else 3
+    coef = torch.randn(rows, N, device="cuda", generator=g) * 0.5
+    if pro == 3:
+        coef[3].abs_().add_(0.1)  # a positive BN scale for the mask recompute
+    coef = coef.contiguous()
+    dx_f, dw_f = C.conv1x1_bwd_fused(gr, y2, coef, x, w)
+    dx_s = C.conv1x1_gemm(gr, w, 1, coef, False, y2, True)[0]
+    dw_s = C.conv1x1_wgrad(gr, x, 1, w, y2, coef)
+
+    def rel(a, b):
+        return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+    assert rel(dx_f, dx_s) < 5e-3, rel(dx_f, dx_s)
+    assert rel(dw_f.view(N, K), dw_s.view(N, K)) < 5e-3, rel(dw_f.view(N, K), dw_s.view(N, K))
+    # fp32 reference of the same math
+    gf, yf = gr.float(), y2.float()
+    if pro == 3:
+        gf = torch.where(yf * coef[3].view(1, -1, 1, 1) + coef[4].view(1, -1, 1, 1) > 0, gf, torch.zeros_like(gf))
+    dy = (coef[0].view(1, -1, 1, 1) * gf + coef[1].view(1, -1, 1, 1) * yf + coef[2].view(1, -1, 1, 1)).to(
+        torch.bfloat16).float()
+    dx_r = torch.einsum("bnhw,nk->bkhw", dy, w.float().view(N, K))
+    dw_r = torch.einsum("bnhw,bkhw->nk", dy, x.float())
+    assert rel(dx_f, dx_r) < 1e-2 and rel(dw_f.view(N, K), dw_r) < 1e-2
