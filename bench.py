@@ -203,6 +203,8 @@ def _install_tunableop(args):
         return None
     dst = os.path.join(tempfile.mkdtemp(prefix=f"xddp_tunableop_{os.environ.get('LOCAL_RANK', '0')}_"), name)
     shutil.copy(src, dst)
+    # (torch may insert the device ordinal before the extension when it opens the file)
+    shutil.copy(src, dst[:-4] + os.environ.get("LOCAL_RANK", "0") + ".csv")
     os.environ["PYTORCH_TUNABLEOP_TUNING"] = "0"
     os.environ["PYTORCH_TUNABLEOP_FILENAME"] = dst
     return "use"

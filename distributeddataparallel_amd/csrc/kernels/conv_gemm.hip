@@ -130,8 +130,6 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
   u32x4 st_k = {0, 0, 0, 0};  // the shift, kept as the 8 packed bf16 values it came from
 #pragma unroll
   for (int e = 0; e < 8; ++e) st_s[e] = st_ss[e] = 0.f;
-  float ep_mu[8];  // EPI: the previous BN's mean of this thread's 8 channels (st_s / st_ss hold its sums)
-  if (EPI) dev::Vec8<float>::ld(epi.mean + n0 + cc * 8, ep_mu);
 
   const uint16_t* wrow[BR];
   constexpr int BCH = BN / 8;  // BT: 16-B chunks per staged k row (64 * BCH == NT * BR)
@@ -152,13 +150,18 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
   float* pro_lds = reinterpret_cast<float*>(smem + 2 * BUF);
   // EPI mask-recompute form: this N tile's (scale, shift) of the masked BN, after the coefficients
   float* epi_ss_lds = pro_lds + (PRO == 3 ? 5 : PRO == 2 ? 3 : PRO == 1 ? 2 : 0) * K;
+  // EPI: and this N tile's mean of the previous BN (the shift of the st_ss products; LDS, not VGPRs)
+  float* epi_mu_lds = epi_ss_lds + 2 * BN;
   if (EPI && epi.ss) {
     for (int i = tid; i < 2 * BN; i += NT) epi_ss_lds[i] = epi.ss[(i >= BN ? N - BN : 0) + n0 + i];
+  }
+  if (EPI) {
+    for (int i = tid; i < BN; i += NT) epi_mu_lds[i] = epi.mean[n0 + i];
   }
   if (PRO) {
     for (int i = tid; i < (PRO == 3 ? 5 : PRO == 2 ? 3 : 2) * K; i += NT) pro_lds[i] = pro_ss[i];
   }
-  if (PRO || (EPI && epi.ss)) lds_barrier();
+  if (PRO || EPI) lds_barrier();
   const uint16_t* arow[AR];
   const int64_t dx2 = PRO >= 2 ? X2 - X : 0;  // the second A source at the same element offsets
   // Rows past M load row M-1 (clamped, branch-free: a per-row "load or zero" select makes hipcc
@@ -313,19 +316,39 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
           *reinterpret_cast<uint16_t*>(Cs + row * CST + col * 2) =
               (uint16_t)(__float_as_uint(acc[i][j][r]) >> 16);  // exact: already bf16-rounded
         }
+    // EPI: every readout row's y / add / mask loads are issued here, before the barrier that publishes
+    // the C tile (rows past M clamped, not used): one round of latency per tile, not RIT
+    constexpr int RIT = BM * CPR / NT;  // readout rows per thread
+    static_assert(BM * CPR % NT == 0, "readout rows must divide evenly over the threads");
+    u32x4 e_y[EPI ? RIT : 1], e_ad[EPI ? RIT : 1];
+    uint32_t e_mb[EPI ? RIT : 1];
+    if (EPI) {
+      const bool form1 = epi.bits != nullptr;  // uniform per launch
+#pragma unroll
+      for (int it = 0; it < RIT; ++it) {
+        const int row = min((tid + NT * it) / CPR, rows_valid - 1);
+        const int64_t e0 = (m0 + row) * N + n0 + cc * 8;
+        e_y[it] = *reinterpret_cast<const u32x4*>(epi.y + e0);
+        if (form1) {
+          e_ad[it] = *reinterpret_cast<const u32x4*>(epi.add + e0);
+          e_mb[it] = epi.bits[e0 >> 3];
+        } else {
+          e_ad[it] = u32x4{0, 0, 0, 0};
+          e_mb[it] = 0u;
+        }
+      }
+    }
     lds_barrier();
     if (STATS && mt == g) st_k = *reinterpret_cast<const u32x4*>(Cs + cc * 16);  // row 0: always valid
 #pragma unroll
-    for (int q = tid; q < BM * CPR; q += NT) {
-      const int row = q / CPR;
+    for (int it = 0; it < RIT; ++it) {
+      const int row = (tid + NT * it) / CPR;
       if (row < rows_valid) {
         u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
         if (EPI) {
-          const int64_t e0 = (m0 + row) * N + n0 + cc * 8;
-          const u32x4 yv = *reinterpret_cast<const u32x4*>(epi.y + e0);
-          const bool form1 = epi.bits != nullptr;  // uniform per launch
-          const u32x4 ad = form1 ? *reinterpret_cast<const u32x4*>(epi.add + e0) : u32x4{0, 0, 0, 0};
-          const uint32_t mb = form1 ? epi.bits[e0 >> 3] : 0u;
+          const u32x4 yv = e_y[EPI ? it : 0], ad = e_ad[EPI ? it : 0];
+          const uint32_t mb = e_mb[EPI ? it : 0];
+          const bool form1 = epi.bits != nullptr;
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
             float g0 = __uint_as_float(v[h] << 16) + __uint_as_float(ad[h] << 16);
@@ -344,8 +367,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
             g1 = __uint_as_float(v[h] & 0xffff0000u);
             st_s[2 * h] += g0;
             st_s[2 * h + 1] += g1;
-            st_ss[2 * h] = fmaf(g0, __uint_as_float(yv[h] << 16) - ep_mu[2 * h], st_ss[2 * h]);
-            st_ss[2 * h + 1] = fmaf(g1, __uint_as_float(yv[h] & 0xffff0000u) - ep_mu[2 * h + 1], st_ss[2 * h + 1]);
+            const float2 mu = *reinterpret_cast<const float2*>(epi_mu_lds + cc * 8 + 2 * h);
+            st_ss[2 * h] = fmaf(g0, __uint_as_float(yv[h] << 16) - mu.x, st_ss[2 * h]);
+            st_ss[2 * h + 1] = fmaf(g1, __uint_as_float(yv[h] & 0xffff0000u) - mu.y, st_ss[2 * h + 1]);
           }
         }
         if (NTSTORE) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + (m0 + row) * N + n0 + cc * 8));
@@ -1018,7 +1042,12 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
     const char* e = std::getenv("XDDP_GEMM_OCC");
     return e && std::atoi(e) == 2 ? 2 : 4;
   }();
-  const int target = num_cus() * (occ == 2 ? 1 : blocks_per_cu);
+  static const int epi_occ = [] {  // the BN-reduce epilogue variant's own choice (XDDP_GEMM_EPI_OCC)
+    const char* e = std::getenv("XDDP_GEMM_EPI_OCC");
+    return e ? (std::atoi(e) == 2 ? 2 : 4) : occ;
+  }();
+  const int kocc = epi_on ? epi_occ : occ;
+  const int target = num_cus() * (kocc == 2 ? 1 : blocks_per_cu);
   int groups = std::max(1, std::min(mtiles, (target + ntiles - 1) / ntiles));
   at::Tensor part = stats ? at::empty({groups, 3, N}, x.options().dtype(at::kFloat))
                           : (epi_on ? at::empty({groups, N, 2}, x.options().dtype(at::kFloat)) : at::Tensor());
@@ -1033,7 +1062,7 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   const dim3 grid(groups * ntiles);
   const size_t bbytes = w_t ? (size_t)64 * (BN * 2 + 32) : (size_t)BN * 128;
   const size_t lds = 2 * ((size_t)BM * 128 + bbytes) + (pro ? ncoef * K * sizeof(float) : 0) +
-                     (epi_form2 ? 2 * (size_t)BN * sizeof(float) : 0);
+                     (epi_on ? 3 * (size_t)BN * sizeof(float) : 0);
   const auto* x2p = pro >= 2 ? reinterpret_cast<const uint16_t*>(prologue_y->data_ptr()) : nullptr;
   const auto* xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
   const auto* wp = reinterpret_cast<const uint16_t*>(wc.data_ptr());
@@ -1043,8 +1072,8 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
 #define XDDP_LG(BN_, WM_, WN_, OCC_)                                                                            \
   launch_gemm<128, BN_, WM_, WN_, OCC_>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, \
                                         mtiles, ntiles, groups, x2p, epi)
-  if (BN == 128) { if (occ == 2) XDDP_LG(128, 4, 2, 2); else XDDP_LG(128, 4, 2, 4); }
-  else { if (occ == 2) XDDP_LG(64, 8, 1, 2); else XDDP_LG(64, 8, 1, 4); }
+  if (BN == 128) { if (kocc == 2) XDDP_LG(128, 4, 2, 2); else XDDP_LG(128, 4, 2, 4); }
+  else { if (kocc == 2) XDDP_LG(64, 8, 1, 2); else XDDP_LG(64, 8, 1, 4); }
 #undef XDDP_LG
   return {y, part};
 }

@@ -686,7 +686,9 @@ std::vector<at::Tensor> flash_attn_forward(const at::Tensor& q, const at::Tensor
 // -> (dq, dk, dv) in the layouts of q, k, v ([B, S, H, D] contiguous)
 std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
                                             const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse,
-                                            bool causal, double scale) {
+                                            bool causal, double scale, const c10::optional<at::Tensor>& dq_out,
+                                            const c10::optional<at::Tensor>& dk_out,
+                                            const c10::optional<at::Tensor>& dv_out) {
   const int64_t D = q.size(3);
   TORCH_CHECK(D == 64 || D == 128, "flash_attn: head dim 64 or 128");
   check_bshd(q, "q", D);
@@ -698,9 +700,19 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
   TORCH_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && lse.is_contiguous() &&
                   lse.numel() == B * Hq * Sq && lse.scalar_type() == at::kFloat,
               "flash_attn backward: shape mismatch");
-  auto dq = at::empty({B, Sq, Hq, D}, q.options());
-  auto dk = at::empty({B, Sk, Hkv, D}, k.options());
-  auto dv = at::empty({B, Sk, Hkv, D}, v.options());
+  // optional caller-provided outputs (e.g. strided views of one packed [B, S, 3, H, D] gradient, so
+  // a fused qkv projection gets its gradient without a gather)
+  auto out_or = [&](const c10::optional<at::Tensor>& o_, const at::Tensor& like, int64_t S_, int64_t H_) {
+    if (o_.has_value() && o_->defined()) {
+      check_bshd(*o_, "dq/dk/dv out", D);
+      TORCH_CHECK(o_->sizes() == like.sizes(), "flash_attn backward: output shape mismatch");
+      return *o_;
+    }
+    return at::empty({B, S_, H_, D}, like.options());
+  };
+  auto dq = out_or(dq_out, q, Sq, Hq);
+  auto dk = out_or(dk_out, k, Sk, Hkv);
+  auto dv = out_or(dv_out, v, Sk, Hkv);
   auto delta = at::empty({B, Hq, Sq}, q.options().dtype(at::kFloat));
   auto stream = c10::hip::getCurrentHIPStream(q.device().index()).stream();
   const int64_t rows = B * Hq * Sq;
@@ -778,12 +790,16 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
     if (D == 128) { if (causal) { XDDP_FA(128, true); } else { XDDP_FA(128, false); } }
     else { if (causal) { XDDP_FA(64, true); } else { XDDP_FA(64, false); } }
 #undef XDDP_FA
-    if (nsplit > 1) {
+    if (nsplit > 1) {  // the split-sum writes dense [B, Sk, Hkv, D]: strided outputs get a copy
       const int64_t n8 = B * Sk * Hkv * D / 8;
+      auto dkc = dk.is_contiguous() ? dk : at::empty({B, Sk, Hkv, D}, k.options());
+      auto dvc = dv.is_contiguous() ? dv : at::empty({B, Sk, Hkv, D}, v.options());
       hipLaunchKernelGGL(fa_dkdv_sum_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, stream,
-                         wsk.data_ptr<float>(), wsv.data_ptr<float>(), reinterpret_cast<uint16_t*>(dk.data_ptr()),
-                         reinterpret_cast<uint16_t*>(dv.data_ptr()), n8, nsplit, sc);
+                         wsk.data_ptr<float>(), wsv.data_ptr<float>(), reinterpret_cast<uint16_t*>(dkc.data_ptr()),
+                         reinterpret_cast<uint16_t*>(dvc.data_ptr()), n8, nsplit, sc);
       XDDP_HIP_CHECK(hipGetLastError());
+      if (!dk.is_same(dkc)) dk.copy_(dkc);
+      if (!dv.is_same(dvc)) dv.copy_(dvc);
     }
   }
   return {dq, dk, dv};

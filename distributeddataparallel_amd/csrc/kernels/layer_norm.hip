@@ -26,11 +26,14 @@ namespace {
 constexpr int kRowsPerBlock = 4;
 constexpr int kMaxVec = 16;  // 16 vectors × 8 × 64 lanes = D up to 8192
 
+// addb / xb (optional): xb = x + addb, the residual stream with the NEXT linear's bias folded in
+// (the transformer block then adds its projection onto xb with a beta = 1 GEMM: no add pass)
 template <typename T, typename W, int NV, bool RMS>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const W* __restrict__ gamma,
                                                      const W* __restrict__ beta, T* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     int64_t rows, int D, float eps) {
+                                                     int64_t rows, int D, float eps, const W* __restrict__ addb,
+                                                     T* __restrict__ xb) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -79,23 +82,40 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = fmaf((v[k][j] - mean) * rstd, g[j], b[j]);
       Vec8<T>::st(yr + c, o);
+      if (addb) {  // uniform per launch
+        Vec8<W>::ld(addb + c, b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = v[k][j] + b[j];
+        Vec8<T>::st(xb + row * D + c, o);
+      }
     }
   }
 }
 
-// dx per row + register-resident dγ/dβ column partials; part = [gridDim.x][2][D]
-template <typename T, typename W, int NV, bool RMS>
+// dx per row + register-resident dγ/dβ column partials; part = [gridDim.x][NP][D].
+// RES: dx += res (the residual-stream gradient that bypasses this norm, so the caller's add pass
+// disappears), and two more column partials: Σ res and Σ dx — the bias gradients of the linear
+// layers whose outputs fed the residual sums after and before this norm. NP = RES ? 4 : 2.
+template <typename T, typename W, int NV, bool RMS, bool RES>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const W* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, T* __restrict__ dx,
-                                                     float* __restrict__ part, int64_t rows, int D) {
-  __shared__ float red[kRowsPerBlock][64 * 8 * 2];  // one-vector-at-a-time fold buffer
+                                                     float* __restrict__ part, int64_t rows, int D,
+                                                     const T* __restrict__ res) {
+  constexpr int NP = RES ? 4 : 2;
+  __shared__ float red[kRowsPerBlock][64 * 8 * 2];  // one-vector-at-a-time fold buffer (two sums)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float dg[NV][8], db[NV][8];
+  float dg[NV][8], db[NV][8], sr[RES ? NV : 1][8], so[RES ? NV : 1][8];
 #pragma unroll
   for (int k = 0; k < NV; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) dg[k][j] = db[k][j] = 0.f;
+  if (RES) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sr[k][j] = so[k][j] = 0.f;
+  }
   const float invD = 1.f / (float)D;
   for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w; row < rows; row += (int64_t)gridDim.x * kRowsPerBlock) {
     const float mean = RMS ? 0.f : mean_in[row];
@@ -135,23 +155,32 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
           dg[k][j] = fmaf(d[j], xh, dg[k][j]);
           db[k][j] += d[j];
         }
+        if (RES) {
+          float r[8];
+          Vec8<T>::ld(res + row * D + c, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            o[j] += r[j];
+            sr[RES ? k : 0][j] += r[j];
+            so[RES ? k : 0][j] += o[j];
+          }
+        }
         Vec8<T>::st(dx + row * D + c, o);
       }
     }
   }
   if (!part) return;
-  // fold the 4 waves' column partials, one vector slot at a time
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
+  // fold the 4 waves' column partials, one vector slot (two sums) at a time
+  auto fold = [&](float (&pa)[NV][8], float (&pb)[NV][8], int k, int p0) {
     const int c = (k * 64 + lane) * 8;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      red[w][lane * 16 + j] = dg[k][j];
-      red[w][lane * 16 + 8 + j] = db[k][j];
+      red[w][lane * 16 + j] = pa[k][j];
+      red[w][lane * 16 + 8 + j] = pb[k][j];
     }
     __syncthreads();
     if (w == 0 && c < D) {
-      float* pg = part + (int64_t)blockIdx.x * 2 * D;
+      float* pg = part + ((int64_t)blockIdx.x * NP + p0) * D;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float a = 0.f, b = 0.f;
@@ -165,52 +194,53 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
       }
     }
     __syncthreads();
+  };
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    fold(dg, db, k, 0);
+    if constexpr (RES) fold(sr, so, k, 2);
   }
 }
 
-// dγ/dβ = column sums of the [nblk][2][D] partials. One 1024-thread block per 64 columns: 16
-// waves each sum nblk/16 partial rows (one coalesced 256-B row segment per load, 8 loads in
-// flight per lane), then fold through LDS. A thread-per-column loop over all nblk rows was
-// latency-bound (~255 us for ViT-L's D=1024, 1024 partial rows); this is ~10 us.
+// Column sums of the [nblk][NP][D] partials: blockIdx.y = which of the NP sums (out.p[y], skipped
+// when null). One 1024-thread block per 64 columns: 16 waves each sum nblk/16 partial rows (one
+// coalesced 256-B row segment per load, 8 loads in flight per lane), then fold through LDS. A
+// thread-per-column loop over all nblk rows was latency-bound (~255 us for ViT-L's D=1024, 1024
+// partial rows); this is ~10 us.
 template <typename W>
-__global__ __launch_bounds__(1024) void ln_param_grad_kernel(const float* __restrict__ part, int nblk, int D,
-                                                             W* __restrict__ dgamma, W* __restrict__ dbeta) {
-  __shared__ float red[2][16][64];
+struct ColOuts {
+  W* p[4];
+};
+
+template <typename W>
+__global__ __launch_bounds__(1024) void ln_param_grad_kernel(const float* __restrict__ part, int nblk, int NP, int D,
+                                                             ColOuts<W> out) {
+  __shared__ float red[16][64];
+  W* dst = out.p[blockIdx.y];
+  if (!dst) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  float a = 0.f, b = 0.f;
+  const int64_t rs = (int64_t)NP * D;
+  const float* src = part + (int64_t)blockIdx.y * D + c;
+  float a = 0.f;
   if (c < D) {
     int i = w;
     for (; i + 16 * 7 < nblk; i += 16 * 8) {
-      float ga[8], gb[8];
+      float ga[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        ga[u] = part[(int64_t)(i + 16 * u) * 2 * D + c];
-        gb[u] = part[(int64_t)(i + 16 * u) * 2 * D + D + c];
-      }
+      for (int u = 0; u < 8; ++u) ga[u] = src[(int64_t)(i + 16 * u) * rs];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        a += ga[u];
-        b += gb[u];
-      }
+      for (int u = 0; u < 8; ++u) a += ga[u];
     }
-    for (; i < nblk; i += 16) {
-      a += part[(int64_t)i * 2 * D + c];
-      b += part[(int64_t)i * 2 * D + D + c];
-    }
+    for (; i < nblk; i += 16) a += src[(int64_t)i * rs];
   }
-  red[0][w][lane] = a;
-  red[1][w][lane] = b;
+  red[w][lane] = a;
   __syncthreads();
   if (w == 0 && c < D) {
-    float sa = 0.f, sb = 0.f;
+    float sa = 0.f;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      sa += red[0][q][lane];
-      sb += red[1][q][lane];
-    }
-    if (dgamma) Elem<W, float>::st(dgamma, c, sa);
-    if (dbeta) Elem<W, float>::st(dbeta, c, sb);
+    for (int q = 0; q < 16; ++q) sa += red[q][lane];
+    Elem<W, float>::st(dst, c, sa);
   }
 }
 
@@ -238,7 +268,8 @@ void nv_dispatch(int nv, F&& f) {
 
 // returns (y, mean (empty for RMS), rstd)
 std::vector<at::Tensor> ln_forward(const at::Tensor& x_in, const c10::optional<at::Tensor>& gamma,
-                                   const c10::optional<at::Tensor>& beta, double eps, bool rms) {
+                                   const c10::optional<at::Tensor>& beta, double eps, bool rms,
+                                   const c10::optional<at::Tensor>& add_bias) {
   auto x = x_in.contiguous();
   TORCH_CHECK(x.is_cuda(), "xddp layer_norm: device tensor expected");
   const int D = (int)x.size(-1);
@@ -250,10 +281,15 @@ std::vector<at::Tensor> ln_forward(const at::Tensor& x_in, const c10::optional<a
   auto mean = rms ? at::Tensor() : at::empty({rows}, fopt);
   const bool hg = gamma.has_value() && gamma->defined(), hb = beta.has_value() && beta->defined();
   const auto wdt = hg ? gamma->scalar_type() : x.scalar_type();
+  const bool ha = add_bias.has_value() && add_bias->defined();
+  if (ha)
+    TORCH_CHECK(add_bias->is_contiguous() && add_bias->numel() == D && add_bias->scalar_type() == wdt,
+                "xddp layer_norm: add_bias must be [D] in the weight dtype");
+  auto xb = ha ? at::empty_like(x) : at::Tensor();
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
   const int nv = (D / 8 + 63) / 64;
   const int grid = (int)((rows + kRowsPerBlock - 1) / kRowsPerBlock);
-  if (rows == 0) return {y, mean, rstd};
+  if (rows == 0) return {y, mean, rstd, xb};
   dispatch_t(x.scalar_type(), [&](auto tt) {
     using T = decltype(tt);
     dispatch_t(wdt, [&](auto tw) {
@@ -265,58 +301,90 @@ std::vector<at::Tensor> ln_forward(const at::Tensor& x_in, const c10::optional<a
                            hg ? reinterpret_cast<const W*>(gamma->data_ptr()) : nullptr,
                            hb ? reinterpret_cast<const W*>(beta->data_ptr()) : nullptr,
                            reinterpret_cast<T*>(y.data_ptr()), rms ? nullptr : mean.data_ptr<float>(),
-                           rstd.data_ptr<float>(), rows, D, (float)eps);
+                           rstd.data_ptr<float>(), rows, D, (float)eps,
+                           ha ? reinterpret_cast<const W*>(add_bias->data_ptr()) : nullptr,
+                           ha ? reinterpret_cast<T*>(xb.data_ptr()) : nullptr);
         XDDP_HIP_CHECK(hipGetLastError());
       });
     });
   });
-  return {y, mean, rstd};
+  return {y, mean, rstd, xb};
 }
 
-// returns (dx, dgamma, dbeta)
+// returns (dx, dgamma, dbeta, Σ res, Σ dx); with res: dx = LN backward + res (the last two only then)
 std::vector<at::Tensor> ln_backward(const at::Tensor& dy_in, const at::Tensor& x_in,
                                     const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& mean,
-                                    const at::Tensor& rstd, bool rms, bool need_dgamma, bool need_dbeta) {
+                                    const at::Tensor& rstd, bool rms, bool need_dgamma, bool need_dbeta,
+                                    const c10::optional<at::Tensor>& res_in) {
   auto x = x_in.contiguous();
   auto dy = dy_in.contiguous();
   const int D = (int)x.size(-1);
   const int64_t rows = x.numel() / D;
   auto dx = at::empty_like(x);
   const bool hg = gamma.has_value() && gamma->defined();
+  const bool hr = res_in.has_value() && res_in->defined();
+  TORCH_CHECK(!hr || !rms, "xddp layer_norm backward: the residual form is LayerNorm-only");
+  at::Tensor res;
+  if (hr) {
+    res = res_in->contiguous();
+    TORCH_CHECK(res.sizes() == x.sizes() && res.scalar_type() == x.scalar_type(),
+                "xddp layer_norm backward: res must match x");
+  }
   const auto wdt = hg ? gamma->scalar_type() : x.scalar_type();
-  at::Tensor dgamma = (hg && need_dgamma) ? at::empty({D}, gamma->options()) : at::Tensor();
-  at::Tensor dbeta = (need_dbeta && !rms) ? at::empty({D}, hg ? gamma->options() : x.options()) : at::Tensor();
+  auto wopt = hg ? gamma->options() : x.options();
+  at::Tensor dgamma = (hg && need_dgamma) ? at::empty({D}, wopt) : at::Tensor();
+  at::Tensor dbeta = (need_dbeta && !rms) ? at::empty({D}, wopt) : at::Tensor();
+  at::Tensor sres = hr ? at::empty({D}, wopt) : at::Tensor(), sout = hr ? at::empty({D}, wopt) : at::Tensor();
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
   const int nv = (D / 8 + 63) / 64;
-  const bool need_part = dgamma.defined() || dbeta.defined();
+  const bool need_part = dgamma.defined() || dbeta.defined() || hr;
+  const int NP = hr ? 4 : 2;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + kRowsPerBlock - 1) / kRowsPerBlock, 1024));
-  auto part = need_part ? at::empty({grid, 2, D}, x.options().dtype(at::kFloat)) : at::Tensor();
-  if (rows == 0) return {dx, dgamma, dbeta};
+  auto part = need_part ? at::empty({grid, NP, D}, x.options().dtype(at::kFloat)) : at::Tensor();
+  if (rows == 0) return {dx, dgamma, dbeta, sres, sout};
   dispatch_t(x.scalar_type(), [&](auto tt) {
     using T = decltype(tt);
     dispatch_t(wdt, [&](auto tw) {
       using W = decltype(tw);
       nv_dispatch<1>(nv, [&](auto nvc) {
         constexpr int NV = decltype(nvc)::value;
-        auto k = rms ? ln_bwd_kernel<T, W, NV, true> : ln_bwd_kernel<T, W, NV, false>;
+        auto k = rms ? ln_bwd_kernel<T, W, NV, true, false>
+                     : (hr ? ln_bwd_kernel<T, W, NV, false, true> : ln_bwd_kernel<T, W, NV, false, false>);
         hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, stream, reinterpret_cast<const T*>(dy.data_ptr()),
                            reinterpret_cast<const T*>(x.data_ptr()),
                            hg ? reinterpret_cast<const W*>(gamma->data_ptr()) : nullptr,
                            (!rms && mean.has_value()) ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(),
                            reinterpret_cast<T*>(dx.data_ptr()), need_part ? part.data_ptr<float>() : nullptr, rows,
-                           D);
+                           D, hr ? reinterpret_cast<const T*>(res.data_ptr()) : nullptr);
         XDDP_HIP_CHECK(hipGetLastError());
       });
       if (need_part) {
-        hipLaunchKernelGGL((ln_param_grad_kernel<W>), dim3((D + 63) / 64), dim3(1024), 0, stream,
-                           part.data_ptr<float>(), grid, D,
-                           dgamma.defined() ? reinterpret_cast<W*>(dgamma.data_ptr()) : nullptr,
-                           dbeta.defined() ? reinterpret_cast<W*>(dbeta.data_ptr()) : nullptr);
+        auto ptr = [](at::Tensor& t) { return t.defined() ? reinterpret_cast<W*>(t.data_ptr()) : nullptr; };
+        ColOuts<W> outs{{ptr(dgamma), ptr(dbeta), ptr(sres), ptr(sout)}};
+        hipLaunchKernelGGL((ln_param_grad_kernel<W>), dim3((D + 63) / 64, NP), dim3(1024), 0, stream,
+                           part.data_ptr<float>(), grid, NP, D, outs);
         XDDP_HIP_CHECK(hipGetLastError());
       }
     });
   });
-  return {dx, dgamma, dbeta};
+  return {dx, dgamma, dbeta, sres, sout};
+}
+
+// Column sums of [P][N] fp32 partial rows into out [N] (dtype of out): the second stage of the
+// bias-gradient reductions in transformer.hip.
+void colsum_partials(const at::Tensor& part, at::Tensor& out) {
+  TORCH_CHECK(part.is_contiguous() && part.scalar_type() == at::kFloat && part.dim() == 2 &&
+                  out.numel() == part.size(1) && out.is_contiguous(),
+              "colsum_partials: part [P, N] fp32, out [N]");
+  const int P = (int)part.size(0), N = (int)part.size(1);
+  auto stream = c10::hip::getCurrentHIPStream(part.device().index()).stream();
+  dispatch_t(out.scalar_type(), [&](auto tw) {
+    using W = decltype(tw);
+    ColOuts<W> outs{{reinterpret_cast<W*>(out.data_ptr()), nullptr, nullptr, nullptr}};
+    hipLaunchKernelGGL((ln_param_grad_kernel<W>), dim3((N + 63) / 64, 1), dim3(1024), 0, stream,
+                       part.data_ptr<float>(), P, 1, N, outs);
+    XDDP_HIP_CHECK(hipGetLastError());
+  });
 }
 
 }  // namespace kernels

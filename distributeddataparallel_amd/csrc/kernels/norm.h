@@ -61,10 +61,12 @@ std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M
                                                const c10::optional<at::Tensor>& num_batches_tracked, double momentum,
                                                bool cumulative, double eps, bool group_minor);
 std::vector<at::Tensor> ln_forward(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
-                                   const c10::optional<at::Tensor>& beta, double eps, bool rms);
+                                   const c10::optional<at::Tensor>& beta, double eps, bool rms,
+                                   const c10::optional<at::Tensor>& add_bias);
 std::vector<at::Tensor> ln_backward(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
                                     const c10::optional<at::Tensor>& mean, const at::Tensor& rstd, bool rms,
-                                    bool need_dgamma, bool need_dbeta);
+                                    bool need_dgamma, bool need_dbeta, const c10::optional<at::Tensor>& res);
+void colsum_partials(const at::Tensor& part, at::Tensor& out);
 
 std::vector<at::Tensor> maxpool_forward(const at::Tensor& x, int64_t k, int64_t stride, int64_t pad);
 // ResNet stem 7x7/s2 conv (3 -> 64) with BN-statistics partials, and its weight gradient
@@ -86,13 +88,18 @@ at::Tensor maxpool_backward(const at::Tensor& dy, const at::Tensor& idx, const a
 at::Tensor rope(const at::Tensor& x, const at::Tensor& cosv, const at::Tensor& sinv, bool backward);
 at::Tensor swiglu_forward(const at::Tensor& a, const at::Tensor& b);
 std::vector<at::Tensor> swiglu_backward(const at::Tensor& g, const at::Tensor& a, const at::Tensor& b);
+at::Tensor gelu_forward(const at::Tensor& h);
+std::vector<at::Tensor> bias_grad(const at::Tensor& g, const c10::optional<at::Tensor>& gelu_input,
+                                  const at::Tensor& bias_like);
 
 // flash attention, [B, S, H, D] bf16 (csrc/kernels/flash_attn.hip)
 std::vector<at::Tensor> flash_attn_forward(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, bool causal,
                                            double scale);
 std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
                                             const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse,
-                                            bool causal, double scale);
+                                            bool causal, double scale, const c10::optional<at::Tensor>& dq_out,
+                                            const c10::optional<at::Tensor>& dk_out,
+                                            const c10::optional<at::Tensor>& dv_out);
 
 void bind_norm_kernels(pybind11::module_& m);
 

@@ -41,7 +41,8 @@ void bind_norm_kernels(py::module_& m) {
   m.def("flash_attn_forward", &flash_attn_forward, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
         py::arg("scale"));
   m.def("flash_attn_backward", &flash_attn_backward, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
-        py::arg("o"), py::arg("lse"), py::arg("causal"), py::arg("scale"));
+        py::arg("o"), py::arg("lse"), py::arg("causal"), py::arg("scale"), py::arg("dq_out") = py::none(),
+        py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none());
   m.def("rope", &rope, py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("backward") = false);
   m.def("swiglu_forward", &swiglu_forward, py::arg("a"), py::arg("b"));
   m.def("swiglu_backward", &swiglu_backward, py::arg("grad"), py::arg("a"), py::arg("b"));
@@ -55,9 +56,12 @@ void bind_norm_kernels(py::module_& m) {
   m.def("maxpool_forward", &maxpool_forward, py::arg("x"), py::arg("kernel"), py::arg("stride"), py::arg("pad"));
   m.def("maxpool_backward", &maxpool_backward, py::arg("dy"), py::arg("idx"), py::arg("x_like"), py::arg("kernel"),
         py::arg("stride"), py::arg("pad"), py::arg("dy2") = py::none());
-  m.def("ln_forward", &ln_forward, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("rms"));
+  m.def("ln_forward", &ln_forward, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("rms"),
+        py::arg("add_bias") = py::none());
   m.def("ln_backward", &ln_backward, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
-        py::arg("rms"), py::arg("need_dgamma"), py::arg("need_dbeta"));
+        py::arg("rms"), py::arg("need_dgamma"), py::arg("need_dbeta"), py::arg("res") = py::none());
+  m.def("gelu_forward", &gelu_forward, py::arg("h"));
+  m.def("bias_grad", &bias_grad, py::arg("grad"), py::arg("gelu_input") = py::none(), py::arg("bias_like"));
 }
 
 }  // namespace kernels

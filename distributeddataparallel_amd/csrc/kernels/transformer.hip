@@ -12,6 +12,7 @@
 
 #include "common.h"
 #include "kernels/dev_utils.h"
+#include "kernels/norm.h"
 
 namespace xddp {
 namespace kernels {
@@ -91,6 +92,58 @@ __global__ __launch_bounds__(kBlock) void swiglu_bwd_kernel(const T* __restrict_
     Vec8<T>::st(da + v * 8, oa);
     Vec8<T>::st(db + v * 8, ob);
   }
+}
+
+// GELU (exact, erf form): gelu(x) = x Φ(x), Φ(x) = (1 + erf(x / √2)) / 2;
+// gelu'(x) = Φ(x) + x φ(x), φ(x) = exp(-x² / 2) / √(2π).
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void gelu_fwd_kernel(const T* __restrict__ h, T* __restrict__ a, int64_t nvec) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
+    float x[8];
+    Vec8<T>::ld(h + v * 8, x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = gelu_f(x[j]);
+    Vec8<T>::st(a + v * 8, x);
+  }
+}
+
+// Bias gradient of a linear layer = column sums of its output gradient g [rows, N]; with GELU the
+// layer feeds a GELU and g is the gradient after it: dh = g · gelu'(h) is written and summed in
+// the same pass. Each thread owns one 8-column chunk (fixed, so its 8 sums stay in registers) and
+// every rgroups-th row; part [rgroups][N] fp32 is summed by colsum_partials (layer_norm.hip).
+template <typename T, bool GELU>
+__global__ __launch_bounds__(kBlock) void bias_grad_kernel(const T* __restrict__ g, const T* __restrict__ h,
+                                                           T* __restrict__ dh, float* __restrict__ part, int64_t rows,
+                                                           int N, int rgroups) {
+  const int cpr = N / 8;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)rgroups * cpr) return;
+  const int c = (int)(t % cpr) * 8, r0 = (int)(t / cpr);
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+#pragma unroll 4
+  for (int64_t r = r0; r < rows; r += rgroups) {
+    float d[8];
+    Vec8<T>::ld(g + r * N + c, d);
+    if (GELU) {
+      float x[8];
+      Vec8<T>::ld(h + r * N + c, x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] *= gelu_grad(x[j]);
+      Vec8<T>::st(dh + r * N + c, d);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += d[j];
+  }
+  float* p = part + (int64_t)r0 * N + c;
+  *reinterpret_cast<dev::f32x4*>(p) = dev::f32x4{s[0], s[1], s[2], s[3]};
+  *reinterpret_cast<dev::f32x4*>(p + 4) = dev::f32x4{s[4], s[5], s[6], s[7]};
 }
 
 template <typename F>
@@ -176,6 +229,61 @@ std::vector<at::Tensor> swiglu_backward(const at::Tensor& g, const at::Tensor& a
     XDDP_HIP_CHECK(hipGetLastError());
   });
   return {da, db};
+}
+
+at::Tensor gelu_forward(const at::Tensor& h) {
+  check_vec(h, "gelu_forward");
+  auto a = at::empty_like(h);
+  const int64_t nvec = h.numel() / 8;
+  if (nvec == 0) return a;
+  auto stream = c10::hip::getCurrentHIPStream(h.device().index()).stream();
+  dispatch16(h.scalar_type(), [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL((gelu_fwd_kernel<T>), dim3(grid_for(nvec)), dim3(kBlock), 0, stream,
+                       reinterpret_cast<const T*>(h.data_ptr()), reinterpret_cast<T*>(a.data_ptr()), nvec);
+    XDDP_HIP_CHECK(hipGetLastError());
+  });
+  return a;
+}
+
+// g: [..., N] output gradient of a linear layer; gelu_input (optional): the pre-activation h of a
+// GELU applied to that output, g then being the gradient after the GELU. Returns (bias gradient
+// [N] in bias_like's dtype, dh = g · gelu'(h) or an undefined tensor).
+std::vector<at::Tensor> bias_grad(const at::Tensor& g, const c10::optional<at::Tensor>& gelu_input,
+                                  const at::Tensor& bias_like) {
+  check_vec(g, "bias_grad");
+  const int64_t N = g.size(-1), rows = g.numel() / N;
+  TORCH_CHECK(N % 8 == 0 && bias_like.numel() == N, "bias_grad: N % 8 == 0 and a bias of N elements required");
+  const bool gelu = gelu_input.has_value() && gelu_input->defined();
+  if (gelu) {
+    check_vec(*gelu_input, "bias_grad");
+    TORCH_CHECK(gelu_input->sizes() == g.sizes() && gelu_input->scalar_type() == g.scalar_type(),
+                "bias_grad: gelu_input must match grad");
+  }
+  auto dh = gelu ? at::empty_like(g) : at::Tensor();
+  auto db = at::empty({N}, bias_like.options().memory_format(at::MemoryFormat::Contiguous));
+  const int cpr = (int)(N / 8);
+  // ~128K threads: each sums rows / rgroups rows of its column chunk
+  const int rgroups = (int)std::max<int64_t>(1, std::min<int64_t>(rows, (131072 + cpr - 1) / cpr));
+  auto part = at::empty({rgroups, N}, g.options().dtype(at::kFloat));
+  if (rows == 0) {
+    db.zero_();
+    return {db, dh};
+  }
+  auto stream = c10::hip::getCurrentHIPStream(g.device().index()).stream();
+  const int64_t threads = (int64_t)rgroups * cpr;
+  dispatch16(g.scalar_type(), [&](auto tag) {
+    using T = decltype(tag);
+    auto k = gelu ? bias_grad_kernel<T, true> : bias_grad_kernel<T, false>;
+    hipLaunchKernelGGL(k, dim3((unsigned)((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                       reinterpret_cast<const T*>(g.data_ptr()),
+                       gelu ? reinterpret_cast<const T*>(gelu_input->data_ptr()) : nullptr,
+                       gelu ? reinterpret_cast<T*>(dh.data_ptr()) : nullptr, part.data_ptr<float>(), rows, (int)N,
+                       rgroups);
+    XDDP_HIP_CHECK(hipGetLastError());
+  });
+  colsum_partials(part, db);
+  return {db, dh};
 }
 
 }  // namespace kernels

@@ -1,7 +1,8 @@
 """Vision Transformer (ViT-B/16, ViT-L/16, ...) — BASELINE.json config 4 (ViT-L/16 bf16 DDP).
 
 Pre-norm encoder blocks with xddp's fused LayerNorm kernel, attention on xddp's gfx950 flash
-attention kernels (``ops/attention.py``; SDPA fallback), GELU MLP, patch embedding as one GEMM. Random init; the
+attention kernels (``ops/attention.py``; SDPA fallback), GELU MLP, patch embedding as one GEMM.
+On bf16 GPU tensors each block runs as one fused autograd node (``ops/encoder_block.py``). Random init; the
 structure/parameter count matches torchvision's ``vit_l_16`` (304,326,632 params at 1000
 classes).
 """
@@ -12,6 +13,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.attention import flash_attention
+from ..ops.encoder_block import encoder_block, encoder_block_supported
 from ..ops.layer_norm import FusedLayerNorm
 
 __all__ = ["VisionTransformer", "vit_b_16", "vit_l_16", "vit_tiny"]
@@ -42,6 +44,9 @@ class EncoderBlock(nn.Module):
         self.mlp = nn.Sequential(nn.Linear(dim, mlp_dim), nn.GELU(), nn.Linear(mlp_dim, dim))
 
     def forward(self, x):
+        # bf16 on the GPU: the whole block is one fused autograd node (ops/encoder_block.py)
+        if isinstance(self.mlp[1], nn.GELU) and self.mlp[1].approximate == "none" and encoder_block_supported(x, self):
+            return encoder_block(x, self)
         x = x + self.self_attention(self.ln_1(x))
         return x + self.mlp(self.ln_2(x))
 

@@ -21,7 +21,7 @@ class _LN(torch.autograd.Function):
         C = load()
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
-        y, mean, rstd = C.ln_forward(x2, weight, bias, eps, rms)
+        y, mean, rstd, _ = C.ln_forward(x2, weight, bias, eps, rms)
         ctx.rms = rms
         ctx.save_for_backward(x2, weight, mean if not rms else None, rstd)
         ctx.shape = shape
@@ -31,7 +31,7 @@ class _LN(torch.autograd.Function):
     def backward(ctx, dy):
         C = load()
         x2, weight, mean, rstd = ctx.saved_tensors
-        dx, dg, db = C.ln_backward(dy.reshape(x2.shape), x2, weight, mean, rstd, ctx.rms,
+        dx, dg, db, _, _ = C.ln_backward(dy.reshape(x2.shape), x2, weight, mean, rstd, ctx.rms,
                                    ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         return dx.view(ctx.shape), dg, (db if not ctx.rms else None), None, None
 
