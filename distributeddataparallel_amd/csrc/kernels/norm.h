@@ -41,6 +41,8 @@ std::vector<at::Tensor> bn_backward_from_partials(const at::Tensor& part, int64_
 // pass on an already-masked gradient g
 at::Tensor bn_backward_elem(const at::Tensor& g, const at::Tensor& x, const at::Tensor& mean, const at::Tensor& coef);
 // 3x3 pad-1 conv (stride 1/2) as an implicit MFMA GEMM (csrc/kernels/conv3x3.hip)
+std::vector<at::Tensor> conv1x1_dma_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats,
+                                            int64_t tile);
 std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats);
 at::Tensor conv3x3_rot_weight(const at::Tensor& w);
 at::Tensor conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like);

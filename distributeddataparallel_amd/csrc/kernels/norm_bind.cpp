@@ -38,6 +38,8 @@ void bind_norm_kernels(py::module_& m) {
   m.def("bn_stats_from_partials", &bn_stats_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"),
         py::arg("momentum"), py::arg("cumulative"), py::arg("eps"), py::arg("group_minor") = false);
+  m.def("conv1x1_dma_forward", &conv1x1_dma_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"),
+        py::arg("tile") = -1);
   m.def("flash_attn_forward", &flash_attn_forward, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
         py::arg("scale"));
   m.def("flash_attn_backward", &flash_attn_backward, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),

@@ -67,6 +67,17 @@ class BNReLULink:
         self.part = self.g = None
 
 
+def _c1_dma(x, w) -> bool:
+    """1x1 forward on the LDS-DMA pipeline? XDDP_C1_DMA = 0 (never, default) | 1 (always) | min Cin.
+
+    Measured on ResNet-50 bs256 (profiles/r2_c1dma_ab.txt): no threshold beats the register-staged
+    GEMM (11,662 img/s off, 11,625 at Cin >= 1024, 11,508 for every 1x1), so it stays opt-in."""
+    v = os.environ.get("XDDP_C1_DMA", "0")
+    if v == "0":
+        return False
+    return x.size(1) >= (1 if v == "1" else int(v))
+
+
 def _same_tensor(a, b) -> bool:
     return a is not None and b is not None and a.data_ptr() == b.data_ptr() and a.shape == b.shape and \
         a.stride() == b.stride()
@@ -78,10 +89,14 @@ class _Conv1x1BN(torch.autograd.Function):
                 stride, link_out, link_x, link_res, link_in):
         C = load()
         ctx.set_materialize_grads(False)
-        y, part = C.conv1x1_gemm(x, w, stride, None, True)
+        dma = _c1_dma(x, w)
+        if dma:  # deep-K / few-tile shapes: the 3-stage LDS-DMA pipeline (csrc/kernels/conv3x3.hip TAPS=1)
+            y, part = C.conv1x1_dma_forward(x, w, stride, True)
+        else:
+            y, part = C.conv1x1_gemm(x, w, stride, None, True)
         M = y.numel() // y.size(1)
         mean, invstd, ss = C.bn_stats_from_partials(part, M, weight, bias, running_mean, running_var, nbt, momentum,
-                                                    cma, eps)
+                                                    cma, eps, dma)
         keep_mask = relu and residual is not None
         out, bits = C.bn_apply(y, ss, residual, relu, keep_mask, nbt)
         ctx.relu, ctx.has_res, ctx.stride = relu, residual is not None, stride

@@ -59,6 +59,32 @@ def test_conv1x1_wgrad_matches_fp32(b, cin, h, w, cout, s, wdt):
     torch.testing.assert_close(dw.float(), ref, rtol=tol, atol=tol * ref.abs().max().item())
 
 
+@pytest.mark.parametrize("b,cin,h,w,cout,s,tile", [
+    (1, 1024, 14, 14, 256, 1, 4),   # layer3 conv1 shape class, 128x64 tiles, partial last M-tile
+    (2, 2048, 7, 7, 512, 1, 0),     # layer4 conv1 class (32 K-steps), 256x128 tiles
+    (2, 512, 15, 15, 1024, 2, 4),   # strided (downsample) rows, odd input size
+    (1, 64, 9, 7, 128, 1, 0),       # a single K-step
+])
+def test_conv1x1_dma_forward_matches_fp32(b, cin, h, w, cout, s, tile):
+    """The 1x1 conv on the 3-stage LDS-DMA pipeline (conv3x3.hip TAPS=1): output vs fp32 torch,
+    statistics partials (group-minor) vs torch's mean/var of the stored bf16 output."""
+    torch.manual_seed(5)
+    x = _x(b, cin, h, w, offset=3.0)
+    wt = (torch.randn(cout, cin, 1, 1, device="cuda") / cin ** 0.5).to(torch.bfloat16)
+    y, part = C.conv1x1_dma_forward(x, wt, s, True, int(tile))
+    ref = F.conv2d(x.float(), wt.float(), stride=s)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+    y2, _ = C.conv1x1_gemm(x, wt, s, None, True)
+    assert (y.float() - y2.float()).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, cout)
+    rm, rv = torch.zeros(cout, device="cuda"), torch.ones(cout, device="cuda")
+    nbt = torch.zeros((), dtype=torch.long, device="cuda")
+    mean, invstd, _ = C.bn_stats_from_partials(part, yf.shape[0], None, None, rm, rv, nbt, 0.1, False, 1e-5, True)
+    torch.testing.assert_close(mean, yf.mean(0), rtol=1e-5, atol=1e-4 * yf.std(0).max().item())
+    torch.testing.assert_close(1.0 / invstd ** 2 - 1e-5, yf.var(0, unbiased=False), rtol=2e-3, atol=1e-6)
+
+
 @pytest.mark.parametrize("offset", [0.0, 300.0])
 def test_epilogue_stats_match_torch(offset):
     """Epilogue partials -> mean/var equal torch's over the stored bf16 output, also when
@@ -106,11 +132,13 @@ def test_bn_backward_prologue_in_gemms(b, cin, h, w, cout, masked):
     torch.testing.assert_close(dw, refw, rtol=2e-2, atol=2e-2 * refw.abs().max().item())
 
 
-@pytest.mark.parametrize("residual,relu,stride", [(False, True, 1), (True, True, 1), (False, False, 2),
-                                                  (False, False, 1)])
-def test_conv1x1_bn_act_forward_backward(residual, relu, stride):
+@pytest.mark.parametrize("residual,relu,stride,dma", [(False, True, 1, "0"), (True, True, 1, "0"),
+                                                      (False, False, 2, "0"), (False, False, 1, "0"),
+                                                      (True, True, 1, "1"), (False, False, 2, "1")])
+def test_conv1x1_bn_act_forward_backward(residual, relu, stride, dma, monkeypatch):
     from distributeddataparallel_amd.ops import FusedBatchNorm2d, conv1x1_bn_act
 
+    monkeypatch.setenv("XDDP_C1_DMA", dma)  # "1": forward on the LDS-DMA kernel (group-minor partials)
     torch.manual_seed(2)
     conv = torch.nn.Conv2d(128, 256, 1, stride=stride, bias=False).cuda().to(torch.bfloat16)
     bn = FusedBatchNorm2d(256).cuda().to(torch.bfloat16)
