@@ -27,7 +27,9 @@ resnet = [("r50 l1 64>256", 802816, 64, 256), ("r50 l1 256>64", 802816, 256, 64)
           ("r50 l2 512>128", 200704, 512, 128), ("r50 l3 256>1024", 50176, 256, 1024),
           ("r50 l3 1024>256", 50176, 1024, 256), ("r50 l4 512>2048", 12544, 512, 2048),
           ("r50 l4 2048>512", 12544, 2048, 512), ("r50 l2.0 256>128", 802816, 256, 128)]
-shapes = resnet if os.environ.get("GEMM_SET") == "resnet" else [("vit qkv", 12608, 1024, 3072), ("vit proj", 12608, 1024, 1024), ("vit fc1", 12608, 1024, 4096),
+vit256 = [("vit256 qkv", 50432, 1024, 3072), ("vit256 proj", 50432, 1024, 1024), ("vit256 fc1", 50432, 1024, 4096),
+          ("vit256 fc2", 50432, 4096, 1024)]
+shapes = resnet if os.environ.get("GEMM_SET") == "resnet" else vit256 if os.environ.get("GEMM_SET") == "vit256" else [("vit qkv", 12608, 1024, 3072), ("vit proj", 12608, 1024, 1024), ("vit fc1", 12608, 1024, 4096),
           ("vit fc2", 12608, 4096, 1024), ("llama qkv", 4096, 4096, 6144), ("llama o", 4096, 4096, 4096),
           ("llama gate+up", 4096, 4096, 28672), ("llama down", 4096, 14336, 4096)]
 for name, M, K, N in shapes:
@@ -45,6 +47,12 @@ for name, M, K, N in shapes:
         own = f"own {t_own:.3f} ms ({fl / t_own / 1e9:.0f} TF/s, maxerr {err:.3f})"
     except Exception as e:  # noqa: BLE001
         own = f"own: {str(e)[:80]}"
+    for tile in (0, 4):  # the 3-stage LDS-DMA pipeline (conv3x3.hip TAPS=1): 256x128 / 128x64 tiles
+        try:
+            t_d = timeit(lambda: C.conv1x1_dma_forward(x4, w4, 1, False, tile))
+            own += f" | dma{tile} {t_d:.3f} ms ({fl / t_d / 1e9:.0f} TF/s)"
+        except Exception as e:  # noqa: BLE001
+            own += f" | dma{tile}: {str(e)[:60]}"
     gb = 2.0 * (M * K + N * K + M * N) / 1e9
     print(f"{name:14s} M{M} K{K} N{N}: hipBLASLt {t_mm:.3f} ms ({fl / t_mm / 1e9:.0f} TF/s, {gb / t_mm:.1f} TB/s) | "
           f"{own} [{gb / t_own if 'own ' in own else 0:.1f} TB/s]", flush=True)
