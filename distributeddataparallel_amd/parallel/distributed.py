@@ -167,6 +167,20 @@ class _DDPJoinHook(JoinHook):
         self.ddp._sync_final_model(is_last_joiner)
 
 
+def _python_reducer_mode() -> bool:
+    """XDDP_PYTHON_REDUCER=1, or torch._dynamo's ``optimize_ddp`` set to "python_reducer" (only
+    consulted when dynamo is already imported: importing it costs seconds)."""
+    if os.environ.get("XDDP_PYTHON_REDUCER", "0") == "1":
+        return True
+    dyn = sys.modules.get("torch._dynamo")
+    if dyn is None:
+        return False
+    try:
+        return dyn.utils.get_optimize_ddp_mode() == "python_reducer"
+    except Exception:  # older/newer dynamo without the helper
+        return False
+
+
 class DistributedDataParallel(nn.Module, Joinable):
     def __init__(
         self,
@@ -190,6 +204,7 @@ class DistributedDataParallel(nn.Module, Joinable):
         comm_dtype: Optional[torch.dtype] = None,
         first_bucket_cap_mb: Optional[float] = None,
         bucket_policy: Optional[str] = None,
+        python_reducer: Optional[bool] = None,
     ):
         super().__init__()
         Joinable.__init__(self)
@@ -268,6 +283,7 @@ class DistributedDataParallel(nn.Module, Joinable):
 
         self._buffers_list = [b for n, b in module.named_buffers() if n not in self._params_and_buffers_to_ignore]
         self._comm_hooks = []
+        self._use_python_reducer, self._accum_grad_hooks = False, []
         self._logging_sample_rate = 100
         self._delay_grad_buffer = None
         self._delay_grad_views: List[torch.Tensor] = []
@@ -283,6 +299,42 @@ class DistributedDataParallel(nn.Module, Joinable):
         self._build_reducer()
         if static_graph:
             self._set_static_graph()
+        self._use_python_reducer = _python_reducer_mode() if python_reducer is None else bool(python_reducer)
+        self._accum_grad_hooks = []
+        if self._use_python_reducer:
+            self._register_accum_grad_hook()
+
+    # ----------------------------------------------------------------------------- python reducer
+    def _register_accum_grad_hook(self):
+        """T6k, the compiled-autograd "python reducer" (``pt:nn/parallel/distributed.py:954-986``):
+        no bucketing Reducer; each parameter's post-accumulate-grad hook reduces its own gradient
+        (AVG) or hands ``(grad, param)`` to the registered comm hooks. The all-reduces are launched
+        asynchronously on the communicator's stream as the gradients arrive, and one end-of-backward
+        callback makes the compute stream wait for all of them (torch's version blocks per
+        parameter through a functional all-reduce + copy)."""
+        ref = weakref.ref(self)
+        pending = []
+
+        def finish():
+            works = list(pending)
+            pending.clear()
+            for w in works:
+                w.wait()
+
+        def hook(param):
+            ddp = ref()
+            if ddp is None or not ddp.require_backward_grad_sync or param.grad is None:
+                return
+            if ddp._comm_hooks:
+                for state, h in ddp._comm_hooks:
+                    h(state, (param.grad, param))
+                return
+            if not pending:
+                torch.autograd.Variable._execution_engine.queue_callback(finish)
+            pending.append(ddp.process_group.allreduce(param.grad, xdist.ReduceOp.AVG))
+
+        for p in self._module_parameters:
+            self._accum_grad_hooks.append(p.register_post_accumulate_grad_hook(hook))
 
     # ----------------------------------------------------------------------------- delayed all-reduce
     def _register_delay_all_reduce_hook(self, param_to_hook_all_reduce):
@@ -479,7 +531,7 @@ class DistributedDataParallel(nn.Module, Joinable):
     def _pre_forward(self, *inputs, **kwargs):
         self._forward_count = getattr(self, "_forward_count", 0) + 1
         _fault.maybe_fail(self.process_group.rank(), self._forward_count)
-        if self._delay_all_reduce_all_params:
+        if self._delay_all_reduce_all_params or getattr(self, "_use_python_reducer", False):
             if self.device_ids:
                 inputs = _to_device(inputs, self.device_ids[0])
                 kwargs = _to_device(kwargs, self.device_ids[0])
@@ -513,7 +565,7 @@ class DistributedDataParallel(nn.Module, Joinable):
 
     def _post_forward(self, output):
         self._clear_grad_buffer()
-        if self._delay_all_reduce_all_params:
+        if self._delay_all_reduce_all_params or getattr(self, "_use_python_reducer", False):
             return output
         if self._check_sync_bufs_post_fwd():
             self._sync_buffers()
@@ -632,7 +684,8 @@ class DistributedDataParallel(nn.Module, Joinable):
         if not callable(hook):
             raise TypeError("comm hook must be callable")
         self._comm_hooks.append((state, hook))
-        self.reducer.register_comm_hook(state, hook)
+        if not getattr(self, "_use_python_reducer", False):  # python reducer: hook(state, (grad, param))
+            self.reducer.register_comm_hook(state, hook)
 
     def _register_builtin_comm_hook(self, comm_hook_type):
         """Native builtin hooks: ALLREDUCE (default) or FP16/BF16 compression (fused casts)."""
@@ -685,6 +738,9 @@ class DistributedDataParallel(nn.Module, Joinable):
 
     def _remove_autograd_hooks(self):
         self.reducer.remove_autograd_hooks()
+        for h in self._accum_grad_hooks:
+            h.remove()
+        self._accum_grad_hooks = []
 
     def _check_reducer_finalized(self):
         self.reducer.check_finalized()
@@ -700,6 +756,7 @@ class DistributedDataParallel(nn.Module, Joinable):
         del attrs["process_group"]
         del attrs["reducer"]
         attrs["_comm_hooks"] = []
+        attrs["_accum_grad_hooks"] = []
         return attrs
 
     def __setstate__(self, state):
@@ -711,6 +768,8 @@ class DistributedDataParallel(nn.Module, Joinable):
         if self.static_graph:
             self.static_graph = False
             self._set_static_graph()
+        if self.__dict__.get("_use_python_reducer", False):
+            self._register_accum_grad_hook()
 
     def _check_default_group(self):
         if xdist.is_initialized() and self.process_group is not xdist.get_default_group():

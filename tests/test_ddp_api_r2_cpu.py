@@ -367,3 +367,45 @@ def _w_monitored_barrier(rank, world):
 
 def test_monitored_barrier_generations_and_missing_ranks():
     run_ranks(_w_monitored_barrier, world=2)
+
+
+# --------------------------------------------------------------------------------------------
+def _w_python_reducer(rank, world):
+    import distributeddataparallel_amd as xddp
+
+    tdist = _torch_pg(rank, world)
+    m1, m2, m3 = _mlp(), _mlp(), _mlp()
+    ddp = xddp.DDP(m1, python_reducer=True)
+    assert ddp._use_python_reducer and len(ddp._accum_grad_hooks) == len(list(m1.parameters()))
+    tddp = torch.nn.parallel.DistributedDataParallel(m2)
+    seen = []
+
+    def hook(state, grad_and_param):  # the compiled-mode comm-hook protocol: (grad, param)
+        g, p = grad_and_param
+        seen.append(p.shape)
+        w = state.allreduce(g, xddp.distributed.ReduceOp.AVG)
+        w.wait()
+
+    ddp_h = xddp.DDP(m3, python_reducer=True)
+    ddp_h.register_comm_hook(ddp_h.process_group, hook)
+    opts = [torch.optim.SGD(m.parameters(), lr=0.1) for m in (m1, m2, m3)]
+    for x, y in _batches(1, 3, per_rank=4, seed=80 + rank):
+        for model, opt in zip((ddp, tddp, ddp_h), opts):
+            opt.zero_grad()
+            F.cross_entropy(model(x), y).backward()
+            opt.step()
+        with ddp.no_sync():  # no_sync: local accumulation only
+            F.cross_entropy(ddp(x), y).backward()
+        g_local = [p.grad.clone() for p in m1.parameters()]
+        opts[0].zero_grad()
+        for p, g in zip(m1.parameters(), g_local):
+            assert g.abs().sum() > 0
+    _assert_params_equal(m1, m2)
+    _assert_params_equal(m3, m2)
+    assert len(seen) == 3 * len(list(m3.parameters()))
+
+
+def test_python_reducer_matches_torch_ddp():
+    """T6k: the compiled-autograd "python reducer" mode (per-parameter post-accumulate-grad
+    all-reduce) trains identically to torch DDP; comm hooks get (grad, param)."""
+    run_ranks(_w_python_reducer, world=2)
