@@ -44,14 +44,28 @@ struct Geo3 {
   int IH, IW, OH, OW, stride;
 };
 
+// DG2 (stride-2 input gradient, pad 1): dX pixel (2p + a, 2q + b) only receives the taps whose
+// forward window put it under dY pixel (p + di, q + dj): a = 0 -> tap row 1 (di = 0); a = 1 -> tap
+// rows 0 (di = 1) and 2 (di = 0); columns alike. So dX splits into four phase grids, each an
+// implicit GEMM over dY with 1, 2, 2 or 4 taps of the rotated weights (4 of 9 MACs a pixel, no zero
+// insertion), its rows scattered to the strided output pixels. All four phases share one launch,
+// heaviest first: block tiles [start[k], start[k+1]) belong to phase k = (a, b) in order
+// (1,1), (1,0), (0,1), (0,0).
+struct Dg2Geo {
+  int B, H, W;       // dX batch and spatial size (geo.IH / IW are dY's)
+  int start[4];      // first block tile of each phase
+};
+
 // TAPS = 9: the 3x3 conv (pad 1). TAPS = 1: a 1x1 conv (pad 0, stride 1 or 2) through the same
 // 3-stage LDS-DMA pipeline — the K loop of the register-staged 1x1 GEMM (conv_gemm.hip) waits a
 // full memory latency per 64-deep step, which dominates the deep-K / few-tile layers (ResNet-50
 // layer3/4: K = 1024..2048 with 400-800 output tiles).
-template <int BM, int BN, int WM, int WN, bool STATS, int TAPS = 9>
+template <int BM, int BN, int WM, int WN, bool STATS, int TAPS = 9, bool DG2 = false>
 __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_fwd_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y,
-    const uint16_t* __restrict__ zeros, int M, int N, int C, Geo3 geo, float* __restrict__ part, int ntiles) {
+    const uint16_t* __restrict__ zeros, int M, int N, int C, Geo3 geo, float* __restrict__ part, int ntiles,
+    Dg2Geo dg) {
+  static_assert(!DG2 || (TAPS == 9 && !STATS), "the stride-2 input gradient is a 3x3 tap walk without stats");
   constexpr int NT = 64 * WM * WN, NW = NT / 64;
   constexpr int AI = BM / 8 / NW, BI = BN / 8 / NW;  // DMA wave-instructions per stage (8 rows each)
   static_assert(AI * NW * 8 == BM && BI * NW * 8 == BN, "tile rows must split evenly over the waves");
@@ -61,11 +75,22 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_fwd_kernel(
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
-  const int wg = dev::xcd_remap(blockIdx.x, gridDim.x);
+  int wg = dev::xcd_remap(blockIdx.x, gridDim.x);
+  int pa = 0, pb = 0, PH = geo.OH, PW = geo.OW, Mk = M;  // DG2: this block's phase and its grid
+  if (DG2) {
+    const int k = (wg >= dg.start[1]) + (wg >= dg.start[2]) + (wg >= dg.start[3]);
+    wg -= dg.start[k];
+    pa = k < 2;
+    pb = !(k & 1);
+    PH = (dg.H - pa + 1) >> 1;
+    PW = (dg.W - pb + 1) >> 1;
+    Mk = dg.B * PH * PW;
+  }
   const int nt = wg % ntiles, mt = wg / ntiles;
   const int n0 = nt * BN, m0 = mt * BM;
-  constexpr int PAD = TAPS == 9 ? 1 : 0;
-  const int cb_n = C >> 6, nk = TAPS * cb_n;
+  constexpr int PAD = TAPS == 9 && !DG2 ? 1 : 0;
+  const int ntaps = DG2 ? (1 + pa) * (1 + pb) : TAPS;
+  const int cb_n = C >> 6, nk = ntaps * cb_n;
   const int pos = lane & 7;  // 16-B slot this lane fills in its 128-B LDS row
 
   // A rows: output pixel -> top-left input pixel of its 3x3 window (may be outside the image)
@@ -75,10 +100,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_fwd_kernel(
   for (int i = 0; i < AI; ++i) {
     const int row = (wid * AI + i) * 8 + (lane >> 3);
     const int m = m0 + row;
-    const int hw = geo.OH * geo.OW;
-    const int b = m / hw, rem = m - b * hw, oh = rem / geo.OW, ow = rem - oh * geo.OW;
-    ih0[i] = m < M ? oh * geo.stride - PAD : -4;  // rows past M: every tap out of bounds -> zeros
-    iw0[i] = ow * geo.stride - PAD;
+    const int hw = PH * PW;
+    const int b = m / hw, rem = m - b * hw, oh = rem / PW, ow = rem - oh * PW;
+    const int st = DG2 ? 1 : geo.stride;  // DG2: phase pixel (p, q) reads dY from (p, q) on
+    ih0[i] = m < Mk ? oh * st - PAD : -4;  // rows past M: every tap out of bounds -> zeros
+    iw0[i] = ow * st - PAD;
     aoff[i] = (((int64_t)b * geo.IH + ih0[i]) * geo.IW + iw0[i]) * C + 8 * (pos ^ ((row >> 1) & 7));
   }
   int64_t boff[BI];
@@ -89,7 +115,16 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_fwd_kernel(
   }
 
   auto issue = [&](int kt, int buf) {
-    const int t = TAPS == 1 ? 0 : kt / cb_n, cb = kt - t * cb_n, r = t / 3, s = t - 3 * r;
+    int t = TAPS == 1 ? 0 : kt / cb_n;
+    const int cb = kt - t * cb_n;
+    int r = t / 3, s = t - 3 * r;  // A-operand offset of the tap (rows, columns)
+    if (DG2) {  // t-th tap of the phase: forward tap (fr, fs), rotated-weight index 8 - (3 fr + fs)
+      const int rr = pb ? t >> 1 : t, sr = pb ? t & 1 : 0;
+      const int fr = pa ? 2 * rr : 1, fs = pb ? 2 * sr : 1;  // a = 1: rows 0 and 2; a = 0: row 1
+      r = fr == 0;
+      s = fs == 0;
+      t = 8 - (3 * fr + fs);
+    }
     uint8_t* A = smem + buf * STAGE;
     const int64_t tap = ((int64_t)r * geo.IW + s) * C + cb * 64;
 #pragma unroll
@@ -163,7 +198,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_fwd_kernel(
   constexpr int CPR = BN / 8;
   static_assert(NT % CPR == 0, "readout mapping needs a fixed chunk column per thread");
   const int cc = tid % CPR;
-  const int rows_valid = min(BM, M - m0);
+  const int rows_valid = min(BM, Mk - m0);
   float st_n = 0.f, st_s[8], st_ss[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) st_s[e] = st_ss[e] = 0.f;
@@ -173,7 +208,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_fwd_kernel(
     const int row = q / CPR;
     if (row < rows_valid) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + (int64_t)(m0 + row) * N + n0 + cc * 8));
+      int64_t yrow = m0 + row;
+      if (DG2) {  // phase pixel -> dX pixel (2p + a, 2q + b)
+        const int hw = PH * PW, m = m0 + row, b = m / hw, rem = m - b * hw, p = rem / PW, q = rem - p * PW;
+        yrow = ((int64_t)b * dg.H + 2 * p + pa) * dg.W + 2 * q + pb;
+      }
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + yrow * N + n0 + cc * 8));
       if (STATS) {
         st_n += 1.f;
 #pragma unroll
@@ -302,7 +342,7 @@ std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w
     hipLaunchKernelGGL(kern, dim3(mtiles * ntiles), dim3(nt), lds, stream,
                        reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()), zeros, (int)M, (int)N, (int)C, geo,
-                       stats ? part.data_ptr<float>() : nullptr, ntiles);
+                       stats ? part.data_ptr<float>() : nullptr, ntiles, Dg2Geo{});
     XDDP_HIP_CHECK(hipGetLastError());
   };
 #define XDDP_C3(BM_, BN_, WM_, WN_)                                                                             \
@@ -367,7 +407,7 @@ std::vector<at::Tensor> conv1x1_dma_forward(const at::Tensor& x, const at::Tenso
     hipLaunchKernelGGL(kern, dim3(mtiles * ntiles), dim3(nt), lds, stream,
                        reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(wc.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()), zeros, (int)M, (int)N, (int)C, geo,
-                       stats ? part.data_ptr<float>() : nullptr, ntiles);
+                       stats ? part.data_ptr<float>() : nullptr, ntiles, Dg2Geo{});
     XDDP_HIP_CHECK(hipGetLastError());
   };
 #define XDDP_C1(BM_, BN_, WM_, WN_)                                                                             \
@@ -380,6 +420,69 @@ std::vector<at::Tensor> conv1x1_dma_forward(const at::Tensor& x, const at::Tenso
   else XDDP_C1(128, 64, 2, 2);
 #undef XDDP_C1
   return {y, part};
+}
+
+// Stride-2 input gradient of conv3x3_forward(x, w, 2): dy [B, N, OH, OW] bf16 channels_last,
+// w_rot = conv3x3_rot_weight(w) ([C, N, 3, 3]); returns dx [B, C, H, W] channels_last (every pixel
+// written: each phase covers its pixels, taps past dY read the zero line).
+at::Tensor conv3x3_dgrad_s2(const at::Tensor& dy, const at::Tensor& w_rot, int64_t H, int64_t W) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_dgrad_s2: dy must be a bf16 channels_last CUDA tensor");
+  TORCH_CHECK(w_rot.scalar_type() == at::kBFloat16 && w_rot.dim() == 4 && w_rot.size(2) == 3 && w_rot.size(3) == 3 &&
+                  w_rot.is_contiguous(at::MemoryFormat::ChannelsLast) && w_rot.size(1) == dy.size(1),
+              "conv3x3_dgrad_s2: w_rot must be bf16 [C, N, 3, 3] channels_last (conv3x3_rot_weight)");
+  const int64_t B = dy.size(0), N = dy.size(1), OH = dy.size(2), OW = dy.size(3), C = w_rot.size(0);
+  TORCH_CHECK(H >= 1 && W >= 1 && (H - 1) / 2 + 1 == OH && (W - 1) / 2 + 1 == OW,
+              "conv3x3_dgrad_s2: (H, W) must be a stride-2 pad-1 input of dy's size");
+  TORCH_CHECK(C % 64 == 0 && N % 64 == 0, "conv3x3_dgrad_s2: channel counts must be multiples of 64");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16) == 0 &&
+                  (reinterpret_cast<uintptr_t>(w_rot.data_ptr()) % 16) == 0,
+              "conv3x3_dgrad_s2: 16-B aligned operands required");
+  TORCH_CHECK(B * H * W < (int64_t(1) << 31) && dy.numel() < (int64_t(1) << 40), "conv3x3_dgrad_s2: bad size");
+  auto dx = at::empty({B, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  int cfg = tile_choice((int)C);
+  if (const char* e = std::getenv("XDDP_DG2_TILE")) {  // A/B: the phase grids' tile on its own
+    cfg = std::atoi(e);
+    if (C % 128 != 0 && cfg < 2) cfg += 2;
+  }
+  const int BM = cfg == 1 || cfg == 3 || cfg == 4 ? 128 : 256, BN = cfg <= 1 ? 128 : 64;
+  const int ntiles = (int)(C / BN);
+  Dg2Geo dg{(int)B, (int)H, (int)W, {0, 0, 0, 0}};
+  int total = 0;
+  for (int k = 0; k < 4; ++k) {  // (a, b) = (1,1), (1,0), (0,1), (0,0)
+    const int a = k < 2, b = !(k & 1);
+    const int64_t mk = B * ((H - a + 1) / 2) * ((W - b + 1) / 2);
+    dg.start[k] = total;
+    total += (int)((mk + BM - 1) / BM) * ntiles;
+  }
+  auto stream = c10::hip::getCurrentHIPStream(dy.device().index()).stream();
+  Geo3 geo{(int)OH, (int)OW, (int)OH, (int)OW, 1};
+  const uint16_t* zeros = zero_line(dy);
+  auto go = [&](auto kern, int nt, size_t lds) {
+    static size_t lds_set = 0;
+    if (lds > 65536 && lds > lds_set) {
+      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      lds_set = lds;
+    }
+    hipLaunchKernelGGL(kern, dim3(total), dim3(nt), lds, stream, reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                       reinterpret_cast<const uint16_t*>(w_rot.data_ptr()), reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                       zeros, 0, (int)C, (int)N, geo, nullptr, ntiles, dg);
+    XDDP_HIP_CHECK(hipGetLastError());
+  };
+#define XDDP_D2(BM_, BN_, WM_, WN_) \
+  go(conv3x3_fwd_kernel<BM_, BN_, WM_, WN_, false, 9, true>, 64 * WM_ * WN_, (size_t)kStages * (BM_ + BN_) * 128)
+  switch (cfg) {
+    case 0: XDDP_D2(256, 128, 4, 2); break;
+    case 1: XDDP_D2(128, 128, 2, 2); break;
+    case 2: XDDP_D2(256, 64, 4, 1); break;
+    case 3: XDDP_D2(128, 64, 2, 1); break;
+    case 4: XDDP_D2(128, 64, 2, 2); break;
+    case 5: XDDP_D2(256, 64, 4, 2); break;
+    default: TORCH_CHECK(false, "conv3x3_dgrad_s2: XDDP_C3_TILE must be 0..5");
+  }
+#undef XDDP_D2
+  return dx;
 }
 
 // w [N, C, 3, 3] channels_last -> [C, N, 3, 3] channels_last rotated by 180 degrees, so that

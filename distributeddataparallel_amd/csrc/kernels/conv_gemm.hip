@@ -66,6 +66,10 @@ __device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
 // whose input is relu(bn2(y2)) with a single consumer: g = dX masked by relu(y2·s + t) > 0 (the
 // mask recomputed from the BN input and its scale/shift), reduced into bn2's backward partials —
 // bn2's separate BN-backward reduce pass over (dX, y2) is gone.
+// add_h / add_w > 0 (first form): add is the compact input gradient of a stride-2 1x1 conv
+// (the downsample branch) over the same tensor — [B][ceil(H/2)][ceil(W/2)][C] — and only the
+// even-(h, w) pixels of the H x W output receive it. MIOpen's strided dgrad wrote that gradient
+// at full resolution, three quarters of it zeros (plus a separate zero-fill pass).
 struct EpiBN {
   const uint16_t* add;
   const uint16_t* y;
@@ -73,6 +77,7 @@ struct EpiBN {
   const float* mean;
   float* part;
   const float* ss;  // [2][C] scale, shift (mask recompute form)
+  int add_h, add_w;
 };
 
 struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every stride-th pixel)
@@ -330,7 +335,19 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
         const int64_t e0 = (m0 + row) * N + n0 + cc * 8;
         e_y[it] = *reinterpret_cast<const u32x4*>(epi.y + e0);
         if (form1) {
-          e_ad[it] = *reinterpret_cast<const u32x4*>(epi.add + e0);
+          int64_t ea = e0;
+          bool have = true;
+          if (epi.add_w) {  // compact stride-2 addend: pixel (b, h, w) -> (b, h/2, w/2) when h, w even
+            const int hw = epi.add_h * epi.add_w;
+            const int64_t m = m0 + row;
+            const int64_t b = m / hw;
+            const int r = (int)(m - b * hw), h = r / epi.add_w, w = r - h * epi.add_w;
+            have = ((h | w) & 1) == 0;
+            const int ah = (epi.add_h + 1) >> 1, aw = (epi.add_w + 1) >> 1;
+            ea = have ? ((b * ah + (h >> 1)) * aw + (w >> 1)) * N + n0 + cc * 8 : 0;
+          }
+          const u32x4 av = *reinterpret_cast<const u32x4*>(epi.add + ea);
+          e_ad[it] = have ? av : u32x4{0, 0, 0, 0};
           e_mb[it] = epi.bits[e0 >> 3];
         } else {
           e_ad[it] = u32x4{0, 0, 0, 0};
@@ -982,7 +999,7 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
                                      const c10::optional<at::Tensor>& prologue_y, bool w_t,
                                      const c10::optional<at::Tensor>& epi_add, const c10::optional<at::Tensor>& epi_y,
                                      const c10::optional<at::Tensor>& epi_bits, const c10::optional<at::Tensor>& epi_mean,
-                                     const c10::optional<at::Tensor>& epi_ss) {
+                                     const c10::optional<at::Tensor>& epi_ss, int64_t epi_add_stride) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16, "conv1x1_gemm: x must be 4-D bf16 on GPU");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv1x1_gemm: x must be channels_last");
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 1 && w.size(3) == 1 && w.scalar_type() == at::kBFloat16,
@@ -1022,7 +1039,10 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
                     epi_mean->scalar_type() == at::kFloat && epi_mean->numel() == N && epi_mean->is_contiguous(),
                 "conv1x1_gemm: epilogue y / mean must match the output (bf16 channels_last, float mean)");
     if (epi_form1) {
-      TORCH_CHECK(epi_add->sizes() == y.sizes() && epi_add->scalar_type() == at::kBFloat16 &&
+      TORCH_CHECK(epi_add_stride == 1 || epi_add_stride == 2, "conv1x1_gemm: epi_add_stride must be 1 or 2");
+      const std::vector<int64_t> asz = epi_add_stride == 1 ? y.sizes().vec()
+                                                           : std::vector<int64_t>{B, N, (OH + 1) / 2, (OW + 1) / 2};
+      TORCH_CHECK(epi_add->sizes() == at::IntArrayRef(asz) && epi_add->scalar_type() == at::kBFloat16 &&
                       epi_add->is_contiguous(at::MemoryFormat::ChannelsLast) && epi_bits.has_value() &&
                       epi_bits->scalar_type() == at::kByte && epi_bits->numel() * 8 == y.numel(),
                   "conv1x1_gemm: epilogue add / bits must match the output (bf16 channels_last, uint8 bits)");
@@ -1051,13 +1071,14 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   int groups = std::max(1, std::min(mtiles, (target + ntiles - 1) / ntiles));
   at::Tensor part = stats ? at::empty({groups, 3, N}, x.options().dtype(at::kFloat))
                           : (epi_on ? at::empty({groups, N, 2}, x.options().dtype(at::kFloat)) : at::Tensor());
-  EpiBN epi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  EpiBN epi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
   if (epi_form1)
     epi = EpiBN{reinterpret_cast<const uint16_t*>(epi_add->data_ptr()), reinterpret_cast<const uint16_t*>(epi_y->data_ptr()),
-                epi_bits->data_ptr<uint8_t>(), epi_mean->data_ptr<float>(), part.data_ptr<float>(), nullptr};
+                epi_bits->data_ptr<uint8_t>(), epi_mean->data_ptr<float>(), part.data_ptr<float>(), nullptr,
+                epi_add_stride == 2 ? (int)OH : 0, epi_add_stride == 2 ? (int)OW : 0};
   else if (epi_form2)
     epi = EpiBN{nullptr, reinterpret_cast<const uint16_t*>(epi_y->data_ptr()), nullptr, epi_mean->data_ptr<float>(),
-                part.data_ptr<float>(), epi_ss->data_ptr<float>()};
+                part.data_ptr<float>(), epi_ss->data_ptr<float>(), 0, 0};
   RowMap rm{(int)OH, (int)OW, (int)IH, (int)IW, (int)stride};
   const dim3 grid(groups * ntiles);
   const size_t bbytes = w_t ? (size_t)64 * (BN * 2 + 32) : (size_t)BN * 128;

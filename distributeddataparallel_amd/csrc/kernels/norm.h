@@ -31,7 +31,7 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
                                      const c10::optional<at::Tensor>& prologue_y, bool w_t,
                                      const c10::optional<at::Tensor>& epi_add, const c10::optional<at::Tensor>& epi_y,
                                      const c10::optional<at::Tensor>& epi_bits, const c10::optional<at::Tensor>& epi_mean,
-                                     const c10::optional<at::Tensor>& epi_ss);
+                                     const c10::optional<at::Tensor>& epi_ss, int64_t epi_add_stride);
 // BN backward from external (sum g, sum g·(x - mean)) partials [groups, C, 2]: (coef [3, C] with the
 // mean folded in, dweight, dbias)
 std::vector<at::Tensor> bn_backward_from_partials(const at::Tensor& part, int64_t M,
@@ -45,6 +45,7 @@ std::vector<at::Tensor> conv1x1_dma_forward(const at::Tensor& x, const at::Tenso
                                             int64_t tile);
 std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats);
 at::Tensor conv3x3_rot_weight(const at::Tensor& w);
+at::Tensor conv3x3_dgrad_s2(const at::Tensor& dy, const at::Tensor& w_rot, int64_t H, int64_t W);
 at::Tensor conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like);
 // 3x3 weight gradient over 8x8 output patches with a shared X halo (csrc/kernels/conv3x3_wgrad.hip)
 at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,

@@ -19,7 +19,7 @@ void bind_norm_kernels(py::module_& m) {
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("prologue_ss"),
         py::arg("stats"), py::arg("prologue_y") = py::none(), py::arg("w_t") = false, py::arg("epi_add") = py::none(),
         py::arg("epi_y") = py::none(), py::arg("epi_bits") = py::none(), py::arg("epi_mean") = py::none(),
-        py::arg("epi_ss") = py::none());
+        py::arg("epi_ss") = py::none(), py::arg("epi_add_stride") = 1);
   m.def("bn_backward_from_partials", &bn_backward_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),
         py::arg("mean"), py::arg("invstd"), py::arg("need_dweight"), py::arg("fold_mean") = true);
   m.def("bn_backward_elem", &bn_backward_elem, py::arg("g"), py::arg("x"), py::arg("mean"), py::arg("coef"));
@@ -27,6 +27,7 @@ void bind_norm_kernels(py::module_& m) {
   m.def("bn_grad_partials", &bn_grad_partials, py::arg("dy"), py::arg("x"), py::arg("mean"));
   m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"));
   m.def("conv3x3_rot_weight", &conv3x3_rot_weight, py::arg("w"));
+  m.def("conv3x3_dgrad_s2", &conv3x3_dgrad_s2, py::arg("dy"), py::arg("w_rot"), py::arg("H"), py::arg("W"));
   m.def("conv3x3_wgrad", &conv3x3_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"));
   m.def("conv3x3_wgrad_patch", &conv3x3_wgrad_patch, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"),
         py::arg("splits") = -1);

@@ -40,6 +40,14 @@ def _stem_fusion() -> bool:
     return os.environ.get("XDDP_STEM_FUSION", "1") != "0"
 
 
+def _ds_link() -> bool:
+    """XDDP_CONV_EPI_DS=0 keeps the stride-2 downsample's input gradient out of the next conv1's
+    epilogue (scattered to full resolution and reduced by the producer instead; A/B switch)."""
+    import os
+
+    return os.environ.get("XDDP_CONV_EPI_DS", "1") != "0"
+
+
 def _bn_relu(norm_layer, c):
     """Return (bn, act). A fused norm layer (``fuses_relu``) absorbs the ReLU."""
     bn = norm_layer(c)
@@ -102,14 +110,23 @@ class Bottleneck(nn.Module):
             # 1x1 convs with the BN statistics in the conv's MFMA epilogue (ops/conv_bn.py)
             from ..ops.conv_bn import conv1x1_bn_act, conv3x3_bn_relu
 
-            identity = xr if self.downsample is None else conv1x1_bn_act(xr, self.downsample[0], self.downsample[1])
-            # previous block's output consumed by conv1 and the identity: their backward hands the
-            # identity gradient to conv1's input-gradient GEMM epilogue (ops/conv_bn.py:EpiLink)
-            link = getattr(x, "_xddp_epi", None) if self.downsample is None else None
+            # previous block's output consumed by conv1 and the identity (or the stride-2
+            # downsample): their backward hands that gradient to conv1's input-gradient GEMM
+            # epilogue (ops/conv_bn.py:EpiLink)
+            link = getattr(x, "_xddp_epi", None)
+            ds = self.downsample
+            if ds is not None and not (ds[0].stride[0] == 2 and _ds_link()):
+                link = None
+            if ds is not None and link is None:
+                identity = conv1x1_bn_act(xr, ds[0], ds[1])
             out = conv1x1_bn_act(x, self.conv1, self.bn1, relu=True, link_x=link)
             out = self.act2(conv3x3_bn_relu(out, self.conv2, self.bn2))
+            if ds is None:
+                identity = xr
+            elif link is not None:  # issued after conv2: its backward runs before conv1's
+                identity = conv1x1_bn_act(xr, ds[0], ds[1], link_ds=link)
             return conv1x1_bn_act(out, self.conv3, self.bn3, residual=identity, relu=True, dual_output=True,
-                                  link_res=link)
+                                  link_res=link if ds is None else None)
         identity = xr if self.downsample is None else self.downsample(xr)
         out = self.act1(self.bn1(self.conv1(x)))
         out = self.act2(self.bn2(self.conv2(out)))

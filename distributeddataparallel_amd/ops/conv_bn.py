@@ -7,13 +7,14 @@ output also reduces it per channel, so the stats pass disappears; the apply pass
 residual, ReLU, ReLU bit mask) and the BN backward reuse the fused-BN kernels. The conv input
 gradient of stride-1 convs is the same MFMA GEMM on (dY, Wᵀ); the weight gradient is an MFMA
 GEMM over the pixel dimension (``conv1x1_wgrad``: dYᵀ·X with transposed LDS reads, fp32 slabs
-split over pixels and summed by a second kernel). Only strided input gradients go to MIOpen
-through ``aten::convolution_backward``.
+split over pixels and summed by a second kernel). The stride-2 input gradient is the stride-1
+GEMM over the strided pixels (compact), handed to the next consumer's epilogue or scattered.
 
 The ResNet bottleneck's 3x3 conv + BN + ReLU (``conv3x3_bn_relu``) runs on the implicit-GEMM
 kernel of ``csrc/kernels/conv3x3.hip`` with the same statistics epilogue; its stride-1 input
-gradient is that kernel on (dY, rot180(W)ᵀ), its weight gradient (and strided input gradient)
-stay on MIOpen.
+gradient is that kernel on (dY, rot180(W)ᵀ) and its stride-2 input gradient the same kernel over
+four phase grids of dX; the stride-1 weight gradient is ``conv3x3_wgrad.hip``, the stride-2 one
+stays on MIOpen.
 
 Parameters and buffers stay in the original ``nn.Conv2d`` / ``FusedBatchNorm2d`` modules, so
 state_dict layout and DDP bucketing are unchanged.
@@ -43,12 +44,28 @@ class EpiLink:
     ``g`` is the exact tensor conv1's backward returned. If the gradient reaching the producer is
     any other tensor (a third consumer of the block output — a feature hook, an auxiliary loss —
     had its gradient summed in), the partials do not describe it and the producer falls back to
-    its own masked reduce over the sum (exact: g is already masked, and masking is idempotent)."""
+    its own masked reduce over the sum (exact: g is already masked, and masking is idempotent).
 
-    __slots__ = ("y", "bits", "mean", "add", "part", "g")
+    Downsample blocks (``add_s2``): the second consumer is the stride-2 1x1 downsample conv. Its
+    backward (which runs before conv1's: the downsample is issued after conv2 in the forward, so
+    the autograd engine's sequence-number order takes it first) leaves its *compact* input
+    gradient dY·W at the strided pixels here; conv1's epilogue adds it at the even (h, w) pixels.
+    MIOpen's strided dgrad (zero-fill + full-resolution write, three quarters zeros) and the
+    producer's separate reduce pass are both gone. ``c1_done`` marks that conv1's backward already
+    ran (any order surprise): the downsample then returns its gradient to autograd instead."""
+
+    __slots__ = ("y", "bits", "mean", "add", "part", "g", "add_s2", "c1_done")
 
     def __init__(self):
         self.y = self.bits = self.mean = self.add = self.part = self.g = None
+        self.add_s2 = self.c1_done = False
+
+
+def _expand_s2(add, like):
+    """Full-resolution gradient of a stride-2 1x1 conv's input from its compact form."""
+    full = torch.zeros_like(like, memory_format=torch.channels_last)
+    full[:, :, ::2, ::2] = add
+    return full
 
 
 class BNReLULink:
@@ -86,7 +103,7 @@ def _same_tensor(a, b) -> bool:
 class _Conv1x1BN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, residual, relu, dual,
-                stride, link_out, link_x, link_res, link_in):
+                stride, link_out, link_x, link_res, link_in, link_ds):
         C = load()
         ctx.set_materialize_grads(False)
         dma = _c1_dma(x, w)
@@ -102,6 +119,7 @@ class _Conv1x1BN(torch.autograd.Function):
         ctx.relu, ctx.has_res, ctx.stride = relu, residual is not None, stride
         ctx.save_for_backward(x, w, y, bits if keep_mask else None, weight, mean, invstd, ss)
         ctx.link_out, ctx.link_x, ctx.link_res, ctx.link_in = link_out, link_x, link_res, link_in
+        ctx.link_ds = link_ds
         if link_out is not None:
             if keep_mask and dual:
                 link_out.y, link_out.bits, link_out.mean = y, bits, mean
@@ -113,6 +131,14 @@ class _Conv1x1BN(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, dout2=None):
+        try:
+            return _Conv1x1BN._backward(ctx, dout, dout2)
+        finally:
+            if ctx.link_x is not None:
+                ctx.link_x.c1_done = True
+
+    @staticmethod
+    def _backward(ctx, dout, dout2):
         C = load()
         x, w, y, bits, weight, mean, invstd, ss = ctx.saved_tensors
         lo = ctx.link_out
@@ -124,13 +150,15 @@ class _Conv1x1BN(torch.autograd.Function):
                 elif dout2 is not None:  # an extra consumer of the residual alias
                     dout = dout2 if dout is None else dout + dout2
                 dout2 = None  # (the identity-path gradient is inside g already)
-            elif lo.add is not None:
-                dout2 = lo.add if dout2 is None else dout2 + lo.add
+            elif lo.add is not None:  # left unconsumed: back to a plain second gradient
+                add = _expand_s2(lo.add, y) if lo.add_s2 else lo.add
+                dout2 = add if dout2 is None else dout2 + add
             lo.y = lo.bits = lo.mean = lo.add = lo.part = lo.g = None
+            lo.add_s2 = False
         if dout is None:
             dout, dout2 = dout2, None
         if dout is None:
-            return (None,) * 18
+            return (None,) * 19
         need_bn_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         s = ctx.stride
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
@@ -182,12 +210,25 @@ class _Conv1x1BN(torch.autograd.Function):
             # MIOpen's 1x1 dgrad over the ResNet-50 shapes (scripts/dgrad_bench.py)
             lx = ctx.link_x
             if lx is not None and lx.add is not None and lx.y is not None and _epi():
-                # the previous block's output gradient: dX + identity-path gradient, masked by its
-                # ReLU and reduced into its BN-backward partials in this GEMM's epilogue
-                dx, lx.part = C.conv1x1_gemm(dy, w, 1, None, False, None, True, lx.add, lx.y, lx.bits, lx.mean)
-                lx.add, lx.g = None, dx
+                # the previous block's output gradient: dX + identity-path gradient (or the
+                # downsample's compact one at the even pixels), masked by its ReLU and reduced into
+                # its BN-backward partials in this GEMM's epilogue
+                dx, lx.part = C.conv1x1_gemm(dy, w, 1, None, False, None, True, lx.add, lx.y, lx.bits, lx.mean, None,
+                                             2 if lx.add_s2 else 1)
+                lx.add, lx.g, lx.add_s2 = None, dx, False
             else:
                 dx = _dgrad_in(ctx, C, dy, w, None, None)
+            need_x = False
+        elif need_x and s == 2 and _dgrad_gemm():
+            # strided 1x1 input gradient: only the stride-2 pixels receive dY·W. The compact product
+            # is one stride-1 GEMM; linked (downsample of a bottleneck whose input is the previous
+            # block's output) it goes to conv1's epilogue, else it is scattered into zeros
+            dxe = _dgrad(C, dy, w, None, None)
+            ld = ctx.link_ds
+            if ld is not None and ld.y is not None and ld.add is None and not ld.c1_done and _epi():
+                ld.add, ld.add_s2 = dxe, True
+            else:
+                dx = _expand_s2(dxe, x)
             need_x = False
         if need_w and _wgrad_gemm():
             # dW[N, K] = dYᵀ[N, M] · X[M, K] (strided pixel rows for the downsample): 14 % less
@@ -203,12 +244,12 @@ class _Conv1x1BN(torch.autograd.Function):
 
 
 def _grads(ctx, dx, dw, dw_bn, db_bn, dres):
-    """The 18 input gradients of _Conv1x1BN; a linked residual gradient goes to the consumer link."""
+    """The 19 input gradients of _Conv1x1BN; a linked residual gradient goes to the consumer link."""
     if dres is not None and ctx.link_res is not None:
         ctx.link_res.add, dres = dres, None
     return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
             None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None, None, None, None,
-            None)
+            None, None)
 
 
 def _bwd_fused_ok(ctx, C, w) -> bool:
@@ -283,6 +324,10 @@ class _Conv3x3BNReLU(torch.autograd.Function):
         if need_x and s == 1:
             dx = C.conv3x3_forward(dy, C.conv3x3_rot_weight(w), 1, False)[0]
             need_x = False
+        elif need_x and s == 2 and _dgrad3_s2():
+            # four phase grids of the strided dX, 1/2/2/4 taps each, one launch (conv3x3.hip DG2)
+            dx = C.conv3x3_dgrad_s2(dy, C.conv3x3_rot_weight(w), x.size(2), x.size(3))
+            need_x = False
         if need_w and _wgrad3() and (s == 1 or os.environ.get("XDDP_CONV3X3_WGRAD_S2", "0") == "1"):
             # 8x8 output patches sharing one staged X halo across the 9 taps (conv3x3_wgrad.hip):
             # 96-98 us vs MIOpen's 120-182 us per stride-1 ResNet-50 shape (bs256); the stride-2
@@ -312,6 +357,11 @@ def _dgrad(C, g, w, coef, y):
 def _conv3x3() -> bool:
     """XDDP_CONV3X3=0 sends the bottleneck 3x3 conv back to MIOpen + separate BN (A/B switch)."""
     return os.environ.get("XDDP_CONV3X3", "1") != "0"
+
+
+def _dgrad3_s2() -> bool:
+    """XDDP_CONV3X3_DGRAD_S2=0 sends the stride-2 3x3 input gradient back to MIOpen (A/B switch)."""
+    return os.environ.get("XDDP_CONV3X3_DGRAD_S2", "1") != "0"
 
 
 def _epi() -> bool:
@@ -379,12 +429,13 @@ def conv3x3_bn_relu(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module):
 
 def conv1x1_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, residual: Optional[torch.Tensor] = None,
                    relu: bool = False, dual_output: bool = False, link_x: Optional[EpiLink] = None,
-                   link_res: Optional[EpiLink] = None):
+                   link_res: Optional[EpiLink] = None, link_ds: Optional[EpiLink] = None):
     """``relu(bn(conv(x)) [+ residual])`` with BN statistics from the conv epilogue when supported.
 
     link_x / link_res: the :class:`EpiLink` of the block output that is this conv's input /
     this op's residual (``x._xddp_epi`` of a dual output); with dual_output and residual + ReLU
-    the returned output carries a fresh link for the next block."""
+    the returned output carries a fresh link for the next block. link_ds: this stride-2 conv is
+    the downsample sharing its input with a linked conv1 (compact input gradient to the link)."""
     if conv.kernel_size != (1, 1) or not conv_bn_supported(x, conv, bn) or (residual is not None and not (
             residual.shape[0] == x.shape[0] and residual.dtype == x.dtype
             and residual.is_contiguous(memory_format=torch.channels_last))):
@@ -393,7 +444,8 @@ def conv1x1_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, residual: Op
     link_in = getattr(x, "_xddp_bnr", None) if conv.stride[0] == 1 else None
     out = _Conv1x1BN.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                            bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), residual, relu,
-                           dual_output, int(conv.stride[0]), link_out, link_x, link_res, link_in)
+                           dual_output, int(conv.stride[0]), link_out, link_x, link_res, link_in,
+                           link_ds if conv.stride[0] == 2 else None)
     if link_out is not None:
         out[0]._xddp_epi = link_out
     return out

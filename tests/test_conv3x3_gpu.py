@@ -53,6 +53,26 @@ def test_conv3x3_rotated_weight_gives_input_gradient():
     torch.testing.assert_close(dx.float(), xr.grad, rtol=1e-2, atol=1e-2 * xr.grad.abs().max().item())
 
 
+@pytest.mark.parametrize("b,cin,h,w,cout", [
+    (2, 128, 10, 11, 64),    # odd width: phase grids of unequal size
+    (3, 64, 15, 15, 128),    # odd input: the last dY row/column feeds the even phase only
+    (2, 128, 28, 28, 128),   # ResNet-50 layer2 entry shape (reduced batch), 256x128 tiles
+    (1, 512, 14, 14, 512),   # layer4 entry shape, long reduction
+])
+def test_conv3x3_dgrad_s2_matches_conv2d(b, cin, h, w, cout):
+    """Stride-2 input gradient over the four phase grids (conv3x3.hip DG2) vs fp32 autograd."""
+    torch.manual_seed(3)
+    x = torch.randn(b, cin, h, w, device="cuda")
+    wt = torch.randn(cout, cin, 3, 3, device="cuda") / (9 * cin) ** 0.5
+    oh, ow = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    dy = _cl(torch.randn(b, cout, oh, ow, device="cuda"))
+    dx = C.conv3x3_dgrad_s2(dy, C.conv3x3_rot_weight(_cl(wt)), h, w)
+    xr = x.requires_grad_()
+    F.conv2d(xr, _cl(wt).float(), stride=2, padding=1).backward(dy.float())
+    assert dx.shape == xr.shape and dx.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(dx.float(), xr.grad, rtol=1e-2, atol=1e-2 * xr.grad.abs().max().item())
+
+
 @pytest.mark.parametrize("stride", [1, 2])
 def test_conv3x3_bn_relu_forward_backward(stride):
     from distributeddataparallel_amd.ops import FusedBatchNorm2d, conv3x3_bn_relu

@@ -250,6 +250,60 @@ def test_dgrad_bn_reduce_epilogue(b, cin, h, w, cout):
     torch.testing.assert_close(coef, torch.stack([k1, k2, k3]), rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("b,cin,h,w,cout", [(2, 64, 14, 14, 256), (2, 128, 7, 9, 128)])
+def test_dgrad_bn_reduce_epilogue_stride2_add(b, cin, h, w, cout):
+    """EPI epilogue with the compact stride-2 addend (a downsample's input gradient, only at the
+    even (h, w) pixels), against fp32 PyTorch of the same math."""
+    torch.manual_seed(7)
+    dy = _x(b, cin, h, w)
+    wf = (torch.randn(cin, cout, 1, 1, device="cuda") / cin ** 0.5).to(torch.bfloat16)
+    add = _x(b, cout, (h + 1) // 2, (w + 1) // 2)
+    yb = _x(b, cout, h, w, offset=0.3)
+    keep = torch.rand(b, cout, h, w, device="cuda") > 0.4
+    flat = keep.permute(0, 2, 3, 1).reshape(-1, 8).to(torch.int32)
+    bits = (flat << torch.arange(8, device="cuda", dtype=torch.int32)).sum(1).to(torch.uint8)
+    mean = yb.float().mean((0, 2, 3))
+    g, part = C.conv1x1_gemm(dy, wf, 1, None, False, None, True, add, yb, bits, mean, None, 2)
+    full = torch.zeros(b, cout, h, w, device="cuda")
+    full[:, :, ::2, ::2] = add.float()
+    ref = torch.where(keep, F.conv_transpose2d(dy.float(), wf.float()) + full, 0.0)
+    torch.testing.assert_close(g.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+    sd, sdx = part.sum(0).unbind(1)
+    gq = g.float()
+    torch.testing.assert_close(sd, gq.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(sdx, (gq * (yb.float() - mean.view(1, -1, 1, 1))).sum((0, 2, 3)), rtol=1e-3,
+                               atol=1e-2)
+
+
+def test_downsample_epilogue_handoff_matches_separate_pass(monkeypatch):
+    """Stride-2 downsample blocks fed by a linked block output: the downsample's compact input
+    gradient folded into conv1's epilogue (XDDP_CONV_EPI_DS=1) gives the same gradients as the
+    scattered full-resolution gradient + the producer's own reduce pass (=0)."""
+    from distributeddataparallel_amd.models.resnet import Bottleneck, ResNet
+    from distributeddataparallel_amd.ops import FusedBatchNorm2d
+
+    torch.manual_seed(8)
+    m = ResNet(Bottleneck, [1, 1, 2, 1], norm_layer=FusedBatchNorm2d).cuda().to(torch.bfloat16)
+    m = m.to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 96, 96, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (4,), device="cuda")
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+
+    def run(flag):
+        monkeypatch.setenv("XDDP_CONV_EPI_DS", flag)
+        m.load_state_dict(sd)
+        m.zero_grad()
+        loss = F.cross_entropy(m(x).float(), y)
+        loss.backward()
+        return loss.item(), torch.cat([p.grad.float().flatten() for p in m.parameters()])
+
+    l1, g1 = run("1")
+    l0, g0 = run("0")
+    assert abs(l1 - l0) < 1e-6 * max(1.0, abs(l0))
+    assert ((g1 - g0).norm() / g0.norm()).item() < 2e-2
+    assert F.cosine_similarity(g1, g0, dim=0).item() > 0.999
+
+
 def test_bottleneck_epilogue_handoff_matches_separate_pass(monkeypatch):
     """ResNet with two bottlenecks in a stage (so one block output feeds a non-downsample block):
     the conv1-epilogue hand-off of the previous block's BN backward (XDDP_CONV_EPI=1) gives the
