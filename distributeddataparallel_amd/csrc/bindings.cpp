@@ -6,6 +6,7 @@
 #include <torch/extension.h>
 
 #include "comm/comm.h"
+#include "comm/peer.h"
 #include "kernels/multi_tensor.h"
 #include "kernels/norm.h"
 #include "reducer/reducer.h"
@@ -204,6 +205,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                               std::chrono::milliseconds(static_cast<int64_t>(timeout_s * 1000)), high_priority);
       }, py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("timeout_s") = 600.0,
       py::arg("high_priority") = true, py::call_guard<py::gil_scoped_release>());
+  py::class_<PeerAllReduce, std::shared_ptr<PeerAllReduce>>(m, "PeerAllReduce",
+      "One-shot small-message all-reduce / broadcast over IPC-mapped peer buffers (xGMI)")
+      .def(py::init<std::shared_ptr<Store>, int, int, int, int64_t>(), py::arg("store"), py::arg("rank"),
+           py::arg("size"), py::arg("device"), py::arg("capacity") = 1 << 20, py::call_guard<py::gil_scoped_release>())
+      .def("supports", [](PeerAllReduce& p, const at::Tensor& t, int op, bool bcast) {
+             return p.supports(t, static_cast<RedOp>(op), bcast);
+           }, py::arg("t"), py::arg("op") = 0, py::arg("bcast") = false)
+      .def("allreduce", [](PeerAllReduce& p, at::Tensor t, int op) {
+             p.allreduce(t, static_cast<RedOp>(op), c10::hip::getCurrentHIPStream(t.device().index()).stream());
+           }, py::arg("t"), py::arg("op") = 0)
+      .def("broadcast", [](PeerAllReduce& p, at::Tensor t, int root) {
+             p.broadcast(t, root, c10::hip::getCurrentHIPStream(t.device().index()).stream());
+           }, py::arg("t"), py::arg("root") = 0)
+      .def("status", &PeerAllReduce::status)
+      .def("close", &PeerAllReduce::close)
+      .def_property_readonly("capacity", &PeerAllReduce::capacity);
   m.def("make_fake_comm", &make_fake_comm, py::arg("rank"), py::arg("size"),
         "Communicator whose collectives complete locally without peers (testing at any world size)");
   m.def("install_crash_handler", &install_crash_handler,

@@ -29,6 +29,7 @@
 #include <thread>
 
 #include "comm/comm.h"
+#include "comm/peer.h"
 
 #define XDDP_NCCL_CHECK(expr)                                                                  \
   do {                                                                                         \
@@ -166,6 +167,7 @@ class RcclComm : public Comm {
     // launch path (comm-stream ordering, events, allocator stream records) runs on a 1-GPU box
     const char* fl = std::getenv("XDDP_RCCL_FORCE_LAUNCH");
     force_launch_ = fl && std::string(fl) == "1";
+    init_peer(store);
     heartbeat_ = now_ns();
     watchdog_ = std::thread([this] { watchdog_loop(); });
     const char* hb = std::getenv("XDDP_HEARTBEAT_TIMEOUT_SEC");
@@ -184,6 +186,8 @@ class RcclComm : public Comm {
   std::shared_ptr<Work> allreduce(at::Tensor t, RedOp op, double premul) override {
     check_tensor(t);
     if (size_ == 1 && !force_launch_ && op != RedOp::PREMUL_SUM) return local_noop("allreduce", t);  // identity
+    if (use_peer(t, op, false))
+      return launch("allreduce_peer", t, {t}, [&](hipStream_t s) { peer_->allreduce(t, op, s); });
     return launch("allreduce", t, {t}, [&](hipStream_t s) {
       if (op == RedOp::PREMUL_SUM) {
         TORCH_CHECK(at::isFloatingType(t.scalar_type()), "PREMUL_SUM needs a floating-point tensor");
@@ -208,6 +212,8 @@ class RcclComm : public Comm {
   std::shared_ptr<Work> broadcast(at::Tensor t, int root) override {
     check_tensor(t);
     if (size_ == 1 && !force_launch_) return local_noop("broadcast", t);
+    if (use_peer(t, RedOp::SUM, true))
+      return launch("broadcast_peer", t, {t}, [&](hipStream_t s) { peer_->broadcast(t, root, s); });
     return launch("broadcast", t, {t}, [&](hipStream_t s) {
       XDDP_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, s));
     });
@@ -296,6 +302,36 @@ class RcclComm : public Comm {
       ncclCommDestroy(comm_);
       destroyed_ = true;
     }
+    if (peer_) peer_->close();
+  }
+
+  // XDDP_PEER_ALLREDUCE=1 (node-local groups of 2..8 ranks): messages up to
+  // XDDP_PEER_ALLREDUCE_BYTES (default 256 KiB) take the one-shot peer-memory kernel
+  // (comm/peer_allreduce.hip) instead of an RCCL ring — the latency-bound per-forward buffer
+  // broadcast, find-unused bitmap and small first bucket. Every rank must agree: each posts
+  // whether its IPC mapping worked and the path is used only if all did.
+  void init_peer(const std::shared_ptr<Store>& store) {
+    const char* e = std::getenv("XDDP_PEER_ALLREDUCE");
+    if (!e || std::string(e) != "1" || size_ < 2 || size_ > kPeerMaxRanks) return;
+    const char* b = std::getenv("XDDP_PEER_ALLREDUCE_BYTES");
+    peer_bytes_ = b ? std::atoll(b) : (256 << 10);
+    const int64_t cap = std::max<int64_t>(4096, (peer_bytes_ + 4095) / 4096 * 4096);
+    std::string ok = "1";
+    try {
+      peer_ = std::make_unique<PeerAllReduce>(store, rank_, size_, device_, cap);
+    } catch (const std::exception& ex) {
+      ok = "0";
+      peer_.reset();
+      fprintf(stderr, "[xddp rccl] rank %d: peer all-reduce unavailable (%s)\n", rank_, ex.what());
+    }
+    store->set("peer/use/" + std::to_string(rank_), ok);
+    bool all = true;
+    for (int r = 0; r < size_; ++r) all = all && store->get("peer/use/" + std::to_string(r)) == "1";
+    if (!all) peer_.reset();
+  }
+
+  bool use_peer(const at::Tensor& t, RedOp op, bool bcast) const {
+    return peer_ && in_group_ == 0 && (int64_t)t.nbytes() <= peer_bytes_ && peer_->supports(t, op, bcast);
   }
 
   hipStream_t stream() const { return stream_.stream(); }
@@ -463,6 +499,8 @@ class RcclComm : public Comm {
   std::mutex comm_mu_;
   bool aborted_ = false;
   bool destroyed_ = false;
+  std::unique_ptr<PeerAllReduce> peer_;
+  int64_t peer_bytes_ = 0;
   bool force_launch_ = false;
   int in_group_ = 0;
   bool capturing_ = false;

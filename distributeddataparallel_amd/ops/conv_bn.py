@@ -12,9 +12,9 @@ GEMM over the strided pixels (compact), handed to the next consumer's epilogue o
 
 The ResNet bottleneck's 3x3 conv + BN + ReLU (``conv3x3_bn_relu``) runs on the implicit-GEMM
 kernel of ``csrc/kernels/conv3x3.hip`` with the same statistics epilogue; its stride-1 input
-gradient is that kernel on (dY, rot180(W)ᵀ) and its stride-2 input gradient the same kernel over
-four phase grids of dX; the stride-1 weight gradient is ``conv3x3_wgrad.hip``, the stride-2 one
-stays on MIOpen.
+gradient is that kernel on (dY, rot180(W)ᵀ) (the stride-2 one: the same kernel over four phase
+grids of dX, opt-in, MIOpen is faster there); the stride-1 weight gradient is
+``conv3x3_wgrad.hip``, the stride-2 one stays on MIOpen.
 
 Parameters and buffers stay in the original ``nn.Conv2d`` / ``FusedBatchNorm2d`` modules, so
 state_dict layout and DDP bucketing are unchanged.
@@ -360,8 +360,12 @@ def _conv3x3() -> bool:
 
 
 def _dgrad3_s2() -> bool:
-    """XDDP_CONV3X3_DGRAD_S2=0 sends the stride-2 3x3 input gradient back to MIOpen (A/B switch)."""
-    return os.environ.get("XDDP_CONV3X3_DGRAD_S2", "1") != "0"
+    """XDDP_CONV3X3_DGRAD_S2=1 runs the stride-2 3x3 input gradient on the phase-grid kernel
+    (conv3x3.hip DG2). Off by default: MIOpen is faster on all three ResNet-50 shapes, zero-fill
+    included (177/149/139 vs 185/168/169 us at bs256, scripts/dg2_bench.py,
+    profiles/r2_dg2_vs_miopen.txt) — the 1- and 2-tap phases are too short to fill the 3-stage
+    pipeline of a one-block-per-CU tile."""
+    return os.environ.get("XDDP_CONV3X3_DGRAD_S2", "0") == "1"
 
 
 def _epi() -> bool:
