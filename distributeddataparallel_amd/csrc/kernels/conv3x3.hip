@@ -175,10 +175,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_fwd_kernel(
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h][i], b[h][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[h][j], a[h][i], acc[i][j], 0, 0, 0);
   }
 
   // ---- epilogue: bf16 C tile through LDS (rows padded 16 B), 16-B row stores ----
+  // (the MFMA above computes the transposed tile: a lane's 4 accumulators are 4 consecutive
+  // output channels of one pixel, stored as one 8-B LDS write)
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave is done reading the stages
   constexpr int CST = BN * 2 + 16;
   static_assert(BM * CST <= kStages * STAGE, "C tile must fit in the stage buffers");
@@ -186,13 +188,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_fwd_kernel(
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-        const int col = wn * WTN + j * 16 + (lane & 15);
-        *reinterpret_cast<uint16_t*>(Cs + row * CST + col * 2) = (uint16_t)(dev::pack_bf16x2(acc[i][j][r], 0.f));
-      }
+    for (int j = 0; j < TN; ++j) {
+      const int row = wm * WTM + i * 16 + (lane & 15);
+      const int col = wn * WTN + j * 16 + (lane >> 4) * 4;
+      uint2 pk;
+      pk.x = dev::pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+      pk.y = dev::pack_bf16x2(acc[i][j][2], acc[i][j][3]);
+      *reinterpret_cast<uint2*>(Cs + row * CST + col * 2) = pk;
+    }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   constexpr int CPR = BN / 8;

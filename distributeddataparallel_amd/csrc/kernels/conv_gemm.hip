@@ -292,7 +292,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
       }
       if (kt + 1 < nk) store(cur ^ 1, kt + 1);
       lds_barrier();
@@ -308,19 +308,22 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
         for (int r = 0; r < 4; ++r) acc[i][j][r] = bf16_round(acc[i][j][r]);
 
     // ---- store Y through LDS: C tile [BM][BN] bf16, rows padded 16 B, then 16-B global stores ----
+    // The MFMA computes the transposed tile (W rows as the first operand), so a lane's 4
+    // accumulator values are 4 consecutive channels of one pixel row: one 8-B LDS store each
+    // instead of four 2-B stores.
     constexpr int CST = BN * 2 + 16;
     uint8_t* Cs = smem;  // the K loop ended with a barrier: the operand buffers are free
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-          const int col = wn * WTN + j * 16 + (lane & 15);
-          *reinterpret_cast<uint16_t*>(Cs + row * CST + col * 2) =
-              (uint16_t)(__float_as_uint(acc[i][j][r]) >> 16);  // exact: already bf16-rounded
-        }
+      for (int j = 0; j < TN; ++j) {
+        const int row = wm * WTM + i * 16 + (lane & 15);
+        const int col = wn * WTN + j * 16 + (lane >> 4) * 4;
+        uint2 pk;  // exact: already bf16-rounded
+        pk.x = (__float_as_uint(acc[i][j][0]) >> 16) | (__float_as_uint(acc[i][j][1]) & 0xffff0000u);
+        pk.y = (__float_as_uint(acc[i][j][2]) >> 16) | (__float_as_uint(acc[i][j][3]) & 0xffff0000u);
+        *reinterpret_cast<uint2*>(Cs + row * CST + col * 2) = pk;
+      }
     // EPI: every readout row's y / add / mask loads are issued here, before the barrier that publishes
     // the C tile (rows past M clamped, not used): one round of latency per tile, not RIT
     constexpr int RIT = BM * CPR / NT;  // readout rows per thread

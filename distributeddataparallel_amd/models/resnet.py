@@ -219,8 +219,12 @@ class ResNet(nn.Module):
         x = self.layer4(x)
         if isinstance(x, tuple):  # fused blocks hand (output, alias) to the next block
             x = x[0]
-        x = self.avgpool(x)
-        x = torch.flatten(x, 1)
+        if fused and isinstance(self.avgpool, nn.AdaptiveAvgPool2d) and self.avgpool.output_size in (1, (1, 1)):
+            from ..ops.pool import global_avg_pool
+
+            x = global_avg_pool(x)  # channels_last gradient without a transpose copy
+        else:
+            x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 
 

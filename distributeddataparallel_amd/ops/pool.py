@@ -7,7 +7,7 @@ import torch.nn.functional as F
 
 from .._native import load
 
-__all__ = ["FusedMaxPool2d", "stem_bn_relu_maxpool"]
+__all__ = ["FusedMaxPool2d", "stem_bn_relu_maxpool", "global_avg_pool"]
 
 
 class _MaxPool(torch.autograd.Function):
@@ -102,3 +102,29 @@ class FusedMaxPool2d(nn.MaxPool2d):
             y = super().forward(x)
             return (y, y) if self.dual_output else y
         return _MaxPool.apply(x, k, s, p, self.dual_output)
+
+
+class _GlobalAvgPool(torch.autograd.Function):
+    """[B, C, H, W] channels_last -> [B, C] spatial mean. The backward writes the broadcast
+    gradient g / HW straight into a channels_last tensor (one write pass). ``nn.AdaptiveAvgPool2d``
+    backward produces an NCHW gradient that autograd then converts to channels_last with a strided
+    transpose copy: 102 us per ResNet-50 bs256 step (rocprof), against ~15 us here."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape, ctx.dtype = x.shape, x.dtype
+        return x.mean((2, 3))
+
+    @staticmethod
+    def backward(ctx, g):
+        B, C, H, W = ctx.shape
+        out = torch.empty((B, C, H, W), dtype=ctx.dtype, device=g.device, memory_format=torch.channels_last)
+        out.copy_((g / (H * W)).to(ctx.dtype)[:, :, None, None].expand(B, C, H, W))
+        return out
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """``flatten(AdaptiveAvgPool2d(1)(x), 1)`` with a channels_last backward."""
+    if x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and torch.is_grad_enabled():
+        return _GlobalAvgPool.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -69,3 +69,20 @@ def _w_transformer(rank, world, which):
 @pytest.mark.parametrize("which", ["llama", "vit"])
 def test_ddp_transformers(which):
     run_ranks(_w_transformer, world=2, args=(which,))
+
+
+def test_global_avg_pool_matches_adaptive_avg_pool():
+    """ops.pool.global_avg_pool: same values and gradient as flatten(AdaptiveAvgPool2d(1)), with a
+    channels_last gradient (no NCHW -> NHWC transpose copy in backward)."""
+    from distributeddataparallel_amd.ops.pool import global_avg_pool
+
+    torch.manual_seed(0)
+    x = torch.randn(3, 16, 7, 5).contiguous(memory_format=torch.channels_last).requires_grad_()
+    x2 = x.detach().clone().requires_grad_()
+    y, y2 = global_avg_pool(x), torch.flatten(torch.nn.functional.adaptive_avg_pool2d(x2, 1), 1)
+    g = torch.randn_like(y)
+    y.backward(g)
+    y2.backward(g)
+    torch.testing.assert_close(y, y2)
+    torch.testing.assert_close(x.grad, x2.grad)
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
