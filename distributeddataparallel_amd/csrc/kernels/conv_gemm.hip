@@ -250,6 +250,41 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
   for (int mt = g; mt < mtiles; mt += groups) {
     const int64_t m0 = (int64_t)mt * BM;
     const int next = mt + groups;
+    const int rows_valid = (int)min<int64_t>(BM, M - m0);
+    // EPI: every readout row's y / add / mask loads are issued at the start of the tile, so they
+    // are in flight during the K loop (rows past M clamped, not used)
+    constexpr int RIT = BM * CPR / NT;  // readout rows per thread
+    static_assert(BM * CPR % NT == 0, "readout rows must divide evenly over the threads");
+    u32x4 e_y[EPI ? RIT : 1], e_ad[EPI ? RIT : 1];
+    uint32_t e_mb[EPI ? RIT : 1];
+    if (EPI) {
+      const bool form1 = epi.bits != nullptr;  // uniform per launch
+#pragma unroll
+      for (int it = 0; it < RIT; ++it) {
+        const int row = min((tid + NT * it) / CPR, rows_valid - 1);
+        const int64_t e0 = (m0 + row) * N + n0 + cc * 8;
+        e_y[it] = *reinterpret_cast<const u32x4*>(epi.y + e0);
+        if (form1) {
+          int64_t ea = e0;
+          bool have = true;
+          if (epi.add_w) {  // compact stride-2 addend: pixel (b, h, w) -> (b, h/2, w/2) when h, w even
+            const int hw = epi.add_h * epi.add_w;
+            const int64_t m = m0 + row;
+            const int64_t b = m / hw;
+            const int r = (int)(m - b * hw), h = r / epi.add_w, w = r - h * epi.add_w;
+            have = ((h | w) & 1) == 0;
+            const int ah = (epi.add_h + 1) >> 1, aw = (epi.add_w + 1) >> 1;
+            ea = have ? ((b * ah + (h >> 1)) * aw + (w >> 1)) * N + n0 + cc * 8 : 0;
+          }
+          const u32x4 av = *reinterpret_cast<const u32x4*>(epi.add + ea);
+          e_ad[it] = have ? av : u32x4{0, 0, 0, 0};
+          e_mb[it] = epi.bits[e0 >> 3];
+        } else {
+          e_ad[it] = u32x4{0, 0, 0, 0};
+          e_mb[it] = 0u;
+        }
+      }
+    }
     store(0, 0);
     lds_barrier();
 
@@ -299,7 +334,6 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
     }
 
     // ---- epilogue: round to bf16 (the stored values are what BN normalizes) ----
-    const int rows_valid = (int)min<int64_t>(BM, M - m0);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -324,40 +358,6 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
         pk.y = (__float_as_uint(acc[i][j][2]) >> 16) | (__float_as_uint(acc[i][j][3]) & 0xffff0000u);
         *reinterpret_cast<uint2*>(Cs + row * CST + col * 2) = pk;
       }
-    // EPI: every readout row's y / add / mask loads are issued here, before the barrier that publishes
-    // the C tile (rows past M clamped, not used): one round of latency per tile, not RIT
-    constexpr int RIT = BM * CPR / NT;  // readout rows per thread
-    static_assert(BM * CPR % NT == 0, "readout rows must divide evenly over the threads");
-    u32x4 e_y[EPI ? RIT : 1], e_ad[EPI ? RIT : 1];
-    uint32_t e_mb[EPI ? RIT : 1];
-    if (EPI) {
-      const bool form1 = epi.bits != nullptr;  // uniform per launch
-#pragma unroll
-      for (int it = 0; it < RIT; ++it) {
-        const int row = min((tid + NT * it) / CPR, rows_valid - 1);
-        const int64_t e0 = (m0 + row) * N + n0 + cc * 8;
-        e_y[it] = *reinterpret_cast<const u32x4*>(epi.y + e0);
-        if (form1) {
-          int64_t ea = e0;
-          bool have = true;
-          if (epi.add_w) {  // compact stride-2 addend: pixel (b, h, w) -> (b, h/2, w/2) when h, w even
-            const int hw = epi.add_h * epi.add_w;
-            const int64_t m = m0 + row;
-            const int64_t b = m / hw;
-            const int r = (int)(m - b * hw), h = r / epi.add_w, w = r - h * epi.add_w;
-            have = ((h | w) & 1) == 0;
-            const int ah = (epi.add_h + 1) >> 1, aw = (epi.add_w + 1) >> 1;
-            ea = have ? ((b * ah + (h >> 1)) * aw + (w >> 1)) * N + n0 + cc * 8 : 0;
-          }
-          const u32x4 av = *reinterpret_cast<const u32x4*>(epi.add + ea);
-          e_ad[it] = have ? av : u32x4{0, 0, 0, 0};
-          e_mb[it] = epi.bits[e0 >> 3];
-        } else {
-          e_ad[it] = u32x4{0, 0, 0, 0};
-          e_mb[it] = 0u;
-        }
-      }
-    }
     lds_barrier();
     if (STATS && mt == g) st_k = *reinterpret_cast<const u32x4*>(Cs + cc * 16);  // row 0: always valid
 #pragma unroll
@@ -1066,8 +1066,12 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
     return e && std::atoi(e) == 2 ? 2 : 4;
   }();
   static const int epi_occ = [] {  // the BN-reduce epilogue variant's own choice (XDDP_GEMM_EPI_OCC)
+    // default 2 (one block per CU, 190 VGPRs, no spills): its epilogue loads are issued at the
+    // tile start and stay live across the K loop, which spills 76 registers within the 128 of
+    // occupancy 4 (331/189/105/78 vs 614/334/200/96 us on the ResNet-50 stage shapes,
+    // profiles/r2_epi_dgrad_shapes.txt; 11,969 vs 10,915 img/s)
     const char* e = std::getenv("XDDP_GEMM_EPI_OCC");
-    return e ? (std::atoi(e) == 2 ? 2 : 4) : occ;
+    return e ? (std::atoi(e) == 4 ? 4 : 2) : 2;
   }();
   const int kocc = epi_on ? epi_occ : occ;
   const int target = num_cus() * (kocc == 2 ? 1 : blocks_per_cu);
