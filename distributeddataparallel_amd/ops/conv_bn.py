@@ -95,6 +95,13 @@ def _c1_dma(x, w) -> bool:
     return x.size(1) >= (1 if v == "1" else int(v))
 
 
+def _c1_blas_min_k() -> int:
+    """Stride-1 1x1 forwards with Cin >= XDDP_C1_BLAS_MIN_K (default 1024; 0 = never) run the GEMM
+    on hipBLASLt + a statistics pass instead of the fused-statistics GEMM."""
+    v = int(os.environ.get("XDDP_C1_BLAS_MIN_K", "1024"))
+    return v if v > 0 else 1 << 30
+
+
 def _same_tensor(a, b) -> bool:
     return a is not None and b is not None and a.data_ptr() == b.data_ptr() and a.shape == b.shape and \
         a.stride() == b.stride()
@@ -109,6 +116,15 @@ class _Conv1x1BN(torch.autograd.Function):
         dma = _c1_dma(x, w)
         if dma:  # deep-K / few-tile shapes: the 3-stage LDS-DMA pipeline (csrc/kernels/conv3x3.hip TAPS=1)
             y, part = C.conv1x1_dma_forward(x, w, stride, True)
+        elif stride == 1 and x.size(1) >= _c1_blas_min_k():
+            # deep-K, few-tile layers (ResNet-50 layer3/4 conv1: K = 1024 / 2048, 400-800 output
+            # tiles): the register-staged GEMM waits a memory latency per 64-deep K step there and
+            # hipBLASLt's is 30-35 % faster (profiles/r2_gemm_resnet_shapes_vs_hipblaslt.txt); the
+            # outputs are small (26 / 13 MB), so a separate statistics pass costs ~5 us
+            B, K, H, W = x.shape
+            y = torch.mm(x.permute(0, 2, 3, 1).reshape(-1, K), w.view(w.size(0), K).t())
+            y = y.view(B, H, W, -1).permute(0, 3, 1, 2)
+            part = C.bn_moments(y).view(1, 3, -1)
         else:
             y, part = C.conv1x1_gemm(x, w, stride, None, True)
         M = y.numel() // y.size(1)
