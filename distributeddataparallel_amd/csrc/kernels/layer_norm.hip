@@ -117,55 +117,138 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
       for (int j = 0; j < 8; ++j) sr[k][j] = so[k][j] = 0.f;
   }
   const float invD = 1.f / (float)D;
-  for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w; row < rows; row += (int64_t)gridDim.x * kRowsPerBlock) {
-    const float mean = RMS ? 0.f : mean_in[row];
-    const float rstd = rstd_in[row];
-    // pass 1: row reductions (x, dy re-read in pass 2 hit L1/L2; keeps VGPRs for the partials)
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
+  if constexpr (NV <= 2) {
+    float gm[NV][8];  // gamma: loaded once
+  #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 8;
-      if (c < D) {
-        float a[8], d[8], g[8];
-        Vec8<T>::ld(x + row * D + c, a);
-        Vec8<T>::ld(dy + row * D + c, d);
-        if (gamma) Vec8<W>::ld(gamma + c, g); else for (int j = 0; j < 8; ++j) g[j] = 1.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float gy = d[j] * g[j];
-          s1 += gy;
-          s2 = fmaf(gy, (a[j] - mean) * rstd, s2);
+      if (gamma && c < D) Vec8<W>::ld(gamma + c, gm[k]);
+      else for (int j = 0; j < 8; ++j) gm[k][j] = 1.f;
+    }
+    // Software-pipelined over this wave's rows: the next row's x / dy (and mean, rstd) are loaded
+    // while the current row is reduced and written, and each row is read once (both passes run
+    // from registers) — the one-row-at-a-time version waited a full memory latency per pass.
+    const int64_t step = (int64_t)gridDim.x * kRowsPerBlock;
+    auto load_row = [&](int64_t r, float (&a)[NV][8], float (&d)[NV][8], float& mu, float& rs) {
+      mu = RMS ? 0.f : mean_in[r];
+      rs = rstd_in[r];
+  #pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = (k * 64 + lane) * 8;
+        if (c < D) {
+          Vec8<T>::ld(x + r * D + c, a[k]);
+          Vec8<T>::ld(dy + r * D + c, d[k]);
         }
       }
-    }
-    const float m1 = RMS ? 0.f : dev::wave_sum(s1) * invD;
-    const float m2 = dev::wave_sum(s2) * invD;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int c = (k * 64 + lane) * 8;
-      if (c < D) {
-        float a[8], d[8], g[8], o[8];
-        Vec8<T>::ld(x + row * D + c, a);
-        Vec8<T>::ld(dy + row * D + c, d);
-        if (gamma) Vec8<W>::ld(gamma + c, g); else for (int j = 0; j < 8; ++j) g[j] = 1.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float xh = (a[j] - mean) * rstd;
-          o[j] = rstd * (d[j] * g[j] - m1 - xh * m2);
-          dg[k][j] = fmaf(d[j], xh, dg[k][j]);
-          db[k][j] += d[j];
-        }
-        if (RES) {
-          float r[8];
-          Vec8<T>::ld(res + row * D + c, r);
-#pragma unroll
+    };
+    int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w;
+    float a[NV][8], d[NV][8], mean = 0.f, rstd = 0.f;
+    if (row < rows) load_row(row, a, d, mean, rstd);
+    for (; row < rows; row += step) {
+      float na[NV][8], nd[NV][8], nmean = 0.f, nrstd = 0.f;
+      if (row + step < rows) load_row(row + step, na, nd, nmean, nrstd);
+      // pass 1: row reductions
+      float s1 = 0.f, s2 = 0.f;
+  #pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = (k * 64 + lane) * 8;
+        if (c < D) {
+  #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            o[j] += r[j];
-            sr[RES ? k : 0][j] += r[j];
-            so[RES ? k : 0][j] += o[j];
+            const float gy = d[k][j] * gm[k][j];
+            s1 += gy;
+            s2 = fmaf(gy, (a[k][j] - mean) * rstd, s2);
           }
         }
-        Vec8<T>::st(dx + row * D + c, o);
+      }
+      const float m1 = RMS ? 0.f : dev::wave_sum(s1) * invD;
+      const float m2 = dev::wave_sum(s2) * invD;
+  #pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = (k * 64 + lane) * 8;
+        if (c < D) {
+          float o[8];
+          float r[8];
+          if (RES) Vec8<T>::ld(res + row * D + c, r);
+  #pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xh = (a[k][j] - mean) * rstd;
+            o[j] = rstd * (d[k][j] * gm[k][j] - m1 - xh * m2);
+            dg[k][j] = fmaf(d[k][j], xh, dg[k][j]);
+            db[k][j] += d[k][j];
+          }
+          if (RES) {
+  #pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              o[j] += r[j];
+              sr[RES ? k : 0][j] += r[j];
+              so[RES ? k : 0][j] += o[j];
+            }
+          }
+          Vec8<T>::st(dx + row * D + c, o);
+        }
+      }
+  #pragma unroll
+      for (int k = 0; k < NV; ++k)
+  #pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a[k][j] = na[k][j];
+          d[k][j] = nd[k][j];
+        }
+      mean = nmean;
+      rstd = nrstd;
+    }
+  } else {  // wide rows (D > 1024): the register-lean one-row-at-a-time loop (no spills)
+    for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w; row < rows; row += (int64_t)gridDim.x * kRowsPerBlock) {
+      const float mean = RMS ? 0.f : mean_in[row];
+      const float rstd = rstd_in[row];
+      // pass 1: row reductions (x, dy re-read in pass 2 hit L1/L2; keeps VGPRs for the partials)
+      float s1 = 0.f, s2 = 0.f;
+  #pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = (k * 64 + lane) * 8;
+        if (c < D) {
+          float a[8], d[8], g[8];
+          Vec8<T>::ld(x + row * D + c, a);
+          Vec8<T>::ld(dy + row * D + c, d);
+          if (gamma) Vec8<W>::ld(gamma + c, g); else for (int j = 0; j < 8; ++j) g[j] = 1.f;
+  #pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float gy = d[j] * g[j];
+            s1 += gy;
+            s2 = fmaf(gy, (a[j] - mean) * rstd, s2);
+          }
+        }
+      }
+      const float m1 = RMS ? 0.f : dev::wave_sum(s1) * invD;
+      const float m2 = dev::wave_sum(s2) * invD;
+  #pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = (k * 64 + lane) * 8;
+        if (c < D) {
+          float a[8], d[8], g[8], o[8];
+          Vec8<T>::ld(x + row * D + c, a);
+          Vec8<T>::ld(dy + row * D + c, d);
+          if (gamma) Vec8<W>::ld(gamma + c, g); else for (int j = 0; j < 8; ++j) g[j] = 1.f;
+  #pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xh = (a[j] - mean) * rstd;
+            o[j] = rstd * (d[j] * g[j] - m1 - xh * m2);
+            dg[k][j] = fmaf(d[j], xh, dg[k][j]);
+            db[k][j] += d[j];
+          }
+          if (RES) {
+            float r[8];
+            Vec8<T>::ld(res + row * D + c, r);
+  #pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              o[j] += r[j];
+              sr[RES ? k : 0][j] += r[j];
+              so[RES ? k : 0][j] += o[j];
+            }
+          }
+          Vec8<T>::st(dx + row * D + c, o);
+        }
       }
     }
   }
