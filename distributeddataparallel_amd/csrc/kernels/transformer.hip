@@ -263,8 +263,15 @@ std::vector<at::Tensor> bias_grad(const at::Tensor& g, const c10::optional<at::T
   auto dh = gelu ? at::empty_like(g) : at::Tensor();
   auto db = at::empty({N}, bias_like.options().memory_format(at::MemoryFormat::Contiguous));
   const int cpr = (int)(N / 8);
-  // ~128K threads: each sums rows / rgroups rows of its column chunk
-  const int rgroups = (int)std::max<int64_t>(1, std::min<int64_t>(rows, (131072 + cpr - 1) / cpr));
+  // each thread sums rows / rgroups rows of its column chunk. With GELU the pass also evaluates
+  // erf + exp per element and is latency/ALU-limited at 128K threads (8 waves per CU: 283 us,
+  // 4.4 TB/s on ViT-L/16's [50432, 4096]); 512K threads fill the CUs (XDDP_BIAS_GRAD_THREADS)
+  static const int64_t target_gelu = [] {
+    const char* e = std::getenv("XDDP_BIAS_GRAD_THREADS");
+    return e ? std::max<int64_t>(1024, std::atoll(e)) : (int64_t)524288;
+  }();
+  const int64_t target = gelu ? target_gelu : 131072;
+  const int rgroups = (int)std::max<int64_t>(1, std::min<int64_t>(rows, (target + cpr - 1) / cpr));
   auto part = at::empty({rgroups, N}, g.options().dtype(at::kFloat));
   if (rows == 0) {
     db.zero_();
