@@ -413,6 +413,8 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_kernel(
 }
 
 // dK, dV: one workgroup = 32·KW keys of one (batch, kv head), 8 waves in NG = 8 / KW groups of KW.
+// KW = 8 (D = 64, Sk <= 256: ViT's 197 tokens): ONE 256-key block and one group, so a (batch,
+// head) is one workgroup that reads each Q / dO tile once and needs no cross-group reduction.
 // Wave (group G, index wq) owns keys k0 + 32 wq .. +31; the groups split the (query head of the
 // GQA group, 32-row query tile) work items (G takes items G, G + NG, ...), so two waves share each
 // SIMD, and sum their dK^T / dV^T accumulators through LDS at the end. KW = 4 (128-key blocks) is
@@ -435,9 +437,11 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
   constexpr int TILE = QB * D * 2;                  // bytes of one Q (or dO) tile
   constexpr int STAGE = 2 * TILE + 2 * QB * 4;      // Q, dO, lse, delta
   constexpr int VBLK = BK * D * 2;                  // the workgroup's V rows
-  constexpr int RPI = 512 / D, NI = QB / RPI / KW;  // rows per 1-KB DMA instruction; instructions per wave
+  // rows per 1-KB DMA instruction; instructions per tile; per wave (KW = 8 at D = 64: half the
+  // waves issue one each)
+  constexpr int RPI = 512 / D, NIT = QB / RPI, NI = NIT >= KW ? NIT / KW : 1;
   constexpr int ACC = NT * 16 * 64;                 // floats of one wave's dK^T (or dV^T)
-  static_assert(KW >= 2 && KW * NG == 8 && NI * KW * RPI == QB, "wave split");
+  static_assert(KW >= 2 && KW * NG == 8 && NIT % NI == 0 && (NIT < KW || NI * KW == NIT), "wave split");
   static_assert((NG - 1) * KW * ACC * 4 <= VBLK + 2 * NG * STAGE, "group reduction must fit the LDS");
   __shared__ __attribute__((aligned(16))) uint8_t smem[VBLK + 2 * NG * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wq = w % KW, G = w / KW, g = lane >> 5;
@@ -485,6 +489,7 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int ins = wq * NI + i, r = ins * RPI + lane / (D / 8);
+      if (NIT < KW && ins >= NIT) break;  // (wave-uniform)
       const int c = uswz<D>(r, lane % (D / 8));  // the logical chunk that lands at this lane's slot
       const int64_t row = min(qt0 + r, Sq - 1);
       __builtin_amdgcn_global_load_lds((const void*)(Qb + row * qs.s + c * 8), (lds_ptr_t)(S + ins * 1024), 16, 0, 0);
@@ -755,9 +760,11 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
   {
     static const int kw_env = [] {
       const char* e = std::getenv("XDDP_FA_DKDV_KW");
-      return e ? std::atoi(e) : 4;
+      return e ? std::atoi(e) : 0;  // 0 = by shape
     }();
-    const int kwv = kw_env == 2 ? 2 : 4;
+    // short non-causal D = 64 sequences (ViT): the whole key range in one 8-wave block
+    // (XDDP_FA_DKDV_KW=4 keeps two 128-key blocks)
+    const int kwv = kw_env == 2 || kw_env == 4 ? kw_env : (D == 64 && !causal && Sk <= 256 ? 8 : 4);
     const int nkb = (int)((Sk + 32 * kwv - 1) / (32 * kwv));
     // GQA head split for causal attention (balance, see the kernel); XDDP_FA_DKDV_SPLIT overrides
     static const int split_env = [] {
@@ -788,6 +795,7 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
 #define XDDP_FA(D_, C_) \
   if (kwv == 4) go(fa_bwd_dkdv_kernel<D_, C_, 4>); else go(fa_bwd_dkdv_kernel<D_, C_, 2>)
     if (D == 128) { if (causal) { XDDP_FA(128, true); } else { XDDP_FA(128, false); } }
+    else if (kwv == 8) { go(fa_bwd_dkdv_kernel<64, false, 8>); }
     else { if (causal) { XDDP_FA(64, true); } else { XDDP_FA(64, false); } }
 #undef XDDP_FA
     if (nsplit > 1) {  // the split-sum writes dense [B, Sk, Hkv, D]: strided outputs get a copy

@@ -32,6 +32,10 @@ def _ref(q, k, v, causal, scale):
     (2, 130, 4, 4, 128, True),      # ragged causal
     (1, 64, 2, 1, 64, True),        # one tile
     (3, 300, 2, 2, 128, False),     # ragged non-causal, D 128
+    (2, 256, 4, 4, 64, False),      # one full 256-key dK/dV block (KW = 8 path)
+    (3, 33, 2, 2, 64, False),       # short: most of the 256-key block masked
+    (1, 100, 8, 2, 64, False),      # GQA on the one-block path
+    (1, 257, 2, 2, 64, False),      # just past one block: two 128-key blocks
 ])
 def test_flash_attention_matches_reference(B, S, H, Hkv, D, causal):
     torch.manual_seed(0)
