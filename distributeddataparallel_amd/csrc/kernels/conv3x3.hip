@@ -304,6 +304,8 @@ const uint16_t* zero_line(const at::Tensor& like) {
 int tile_choice(int N) {
   int t = N % 128 == 0 ? 0 : 4;  // 256x128 (8 waves, 1 block/CU); N = 64: 128x64 (4 waves, 2 blocks/CU)
   if (const char* e = std::getenv("XDDP_C3_TILE")) t = std::atoi(e);
+  if (N % 128 != 0)
+    if (const char* e = std::getenv("XDDP_C3_TILE64")) t = std::atoi(e);  // the 64-channel layers only
   if (N % 128 != 0 && t < 2) t += 2;  // 128-wide N tiles need N % 128 == 0
   return t;
 }
