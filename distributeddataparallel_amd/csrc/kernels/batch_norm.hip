@@ -218,8 +218,12 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
                                                           T* __restrict__ y, int64_t nvec, int C,
                                                           const float* __restrict__ scale,
                                                           const float* __restrict__ shift, int64_t* nbt_inc,
-                                                          uint8_t* __restrict__ mbits) {
+                                                          uint8_t* __restrict__ mbits, const float* __restrict__ rss,
+                                                          int64_t* nbt_inc2) {
+  // rss: the residual is the raw output of another BatchNorm (the downsample's) whose apply is
+  // folded in here: r -> r·rscale + rshift (rss = [2][C]); nbt_inc2 is that BN's counter
   if (nbt_inc && blockIdx.x == 0 && threadIdx.x == 0) nbt_inc[0] += 1;  // num_batches_tracked.add_(1), fused
+  if (nbt_inc2 && blockIdx.x == 0 && threadIdx.x == 0) nbt_inc2[0] += 1;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // channel offset advanced incrementally: no 64-bit modulo in the loop
@@ -229,7 +233,17 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
     const int64_t e = v * 8;
     float a[8], r[8];
     Vec8<T>::ld(x + e, a);
-    if (RES) Vec8<T>::ld(res + e, r);
+    if (RES) {
+      Vec8<T>::ld(res + e, r);
+      if (rss) {  // (uniform per launch)
+        float rs[8], rh[8];
+        dev::Vec8<float>::ld(rss + c0, rs);
+        dev::Vec8<float>::ld(rss + C + c0, rh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = fmaf(r[j], rs[j], rh[j]);
+        Vec8<T>::rt(r);  // at storage precision, as the downsample's own apply pass would store it
+      }
+    }
     const dev::f32x4 s0 = *reinterpret_cast<const dev::f32x4*>(scale + c0);
     const dev::f32x4 s1 = *reinterpret_cast<const dev::f32x4*>(scale + c0 + 4);
     const dev::f32x4 h0 = *reinterpret_cast<const dev::f32x4*>(shift + c0);
@@ -563,7 +577,7 @@ std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::
       auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
                            reinterpret_cast<const T*>(x.data_ptr()), res, reinterpret_cast<T*>(y.data_ptr()), nvec,
-                           (int)C, ss.data_ptr<float>(), ss.data_ptr<float>() + C, nbt_inc, mb);
+                           (int)C, ss.data_ptr<float>(), ss.data_ptr<float>() + C, nbt_inc, mb, nullptr, nullptr);
       };
       if (has_res) { if (relu) launch(bn_apply_kernel<T, true, true>); else launch(bn_apply_kernel<T, true, false>); }
       else { if (relu) launch(bn_apply_kernel<T, false, true>); else launch(bn_apply_kernel<T, false, false>); }
@@ -626,7 +640,9 @@ at::Tensor bn_grad_partials(const at::Tensor& dy_in, const at::Tensor& x, const 
 // statistics): y = [relu](x*scale + shift [+ residual]); optional ReLU bit mask; optional
 // num_batches_tracked += 1. Returns (y, mask_bits).
 std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, const c10::optional<at::Tensor>& residual,
-                                 bool relu, bool save_mask, const c10::optional<at::Tensor>& num_batches_tracked) {
+                                 bool relu, bool save_mask, const c10::optional<at::Tensor>& num_batches_tracked,
+                                 const c10::optional<at::Tensor>& residual_ss,
+                                 const c10::optional<at::Tensor>& residual_nbt) {
   check_nhwc(x);
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), Wd = x.size(3);
   TORCH_CHECK(ss.is_cuda() && ss.scalar_type() == at::kFloat && ss.numel() == 2 * C && ss.is_contiguous(),
@@ -636,6 +652,11 @@ std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, cons
     TORCH_CHECK(residual->sizes() == x.sizes() && residual->scalar_type() == x.scalar_type() &&
                     residual->is_contiguous(at::MemoryFormat::ChannelsLast),
                 "fused residual must match x (shape, dtype, channels_last)");
+  const bool has_rss = residual_ss.has_value() && residual_ss->defined();
+  if (has_rss)
+    TORCH_CHECK(has_res && residual_ss->is_cuda() && residual_ss->scalar_type() == at::kFloat &&
+                    residual_ss->numel() == 2 * C && residual_ss->is_contiguous(),
+                "bn_apply: residual scale/shift must be float [2, C] with a residual");
   auto y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
   at::Tensor mask_bits = (relu && save_mask) ? at::empty({N * H * Wd * C / 8}, x.options().dtype(at::kByte))
                                              : at::Tensor();
@@ -643,6 +664,9 @@ std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, cons
   const int64_t nvec = N * H * Wd * C / 8;
   int64_t* nbt_inc = (num_batches_tracked.has_value() && num_batches_tracked->defined())
                          ? num_batches_tracked->data_ptr<int64_t>() : nullptr;
+  int64_t* nbt_inc2 = (residual_nbt.has_value() && residual_nbt->defined()) ? residual_nbt->data_ptr<int64_t>()
+                                                                             : nullptr;
+  const float* rss = has_rss ? residual_ss->data_ptr<float>() : nullptr;
   uint8_t* mb = mask_bits.defined() ? mask_bits.data_ptr<uint8_t>() : nullptr;
   dispatch_act(x.scalar_type(), [&](auto tag_t) {
     using T = decltype(tag_t);
@@ -650,7 +674,7 @@ std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, cons
     auto launch = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
                          reinterpret_cast<const T*>(x.data_ptr()), res, reinterpret_cast<T*>(y.data_ptr()), nvec,
-                         (int)C, ss.data_ptr<float>(), ss.data_ptr<float>() + C, nbt_inc, mb);
+                         (int)C, ss.data_ptr<float>(), ss.data_ptr<float>() + C, nbt_inc, mb, rss, nbt_inc2);
     };
     if (has_res) { if (relu) launch(bn_apply_kernel<T, true, true>); else launch(bn_apply_kernel<T, true, false>); }
     else { if (relu) launch(bn_apply_kernel<T, false, true>); else launch(bn_apply_kernel<T, false, false>); }

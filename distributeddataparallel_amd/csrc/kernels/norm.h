@@ -24,7 +24,9 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy, const at::Tensor& x, c
 at::Tensor bn_moments(const at::Tensor& x);
 at::Tensor bn_grad_partials(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& mean);
 std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, const c10::optional<at::Tensor>& residual,
-                                 bool relu, bool save_mask, const c10::optional<at::Tensor>& num_batches_tracked);
+                                 bool relu, bool save_mask, const c10::optional<at::Tensor>& num_batches_tracked,
+                                 const c10::optional<at::Tensor>& residual_ss,
+                                 const c10::optional<at::Tensor>& residual_nbt);
 // 1x1 conv as an MFMA GEMM with BN prologue (previous BN's apply+ReLU) / epilogue (stats partials)
 std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride,
                                      const c10::optional<at::Tensor>& prologue_ss, bool stats,

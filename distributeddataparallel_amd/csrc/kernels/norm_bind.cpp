@@ -15,7 +15,8 @@ void bind_norm_kernels(py::module_& m) {
         py::arg("invstd"), py::arg("scale_shift"), py::arg("relu"), py::arg("need_dres"), py::arg("need_dweight"),
         py::arg("dy2") = py::none(), py::arg("mask_bits") = py::none(), py::arg("coef_only") = false);
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("scale_shift"), py::arg("residual"), py::arg("relu"),
-        py::arg("save_mask"), py::arg("num_batches_tracked"));
+        py::arg("save_mask"), py::arg("num_batches_tracked"), py::arg("residual_ss") = py::none(),
+        py::arg("residual_nbt") = py::none());
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("prologue_ss"),
         py::arg("stats"), py::arg("prologue_y") = py::none(), py::arg("w_t") = false, py::arg("epi_add") = py::none(),
         py::arg("epi_y") = py::none(), py::arg("epi_bits") = py::none(), py::arg("epi_mean") = py::none(),

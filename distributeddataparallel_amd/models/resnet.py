@@ -48,6 +48,14 @@ def _ds_link() -> bool:
     return os.environ.get("XDDP_CONV_EPI_DS", "1") != "0"
 
 
+def _ds_defer() -> bool:
+    """XDDP_DS_DEFER=0 keeps the downsample's own BN apply pass (A/B switch): by default the block's
+    final apply pass applies it to the raw downsample output on the fly."""
+    import os
+
+    return os.environ.get("XDDP_DS_DEFER", "1") != "0"
+
+
 def _bn_relu(norm_layer, c):
     """Return (bn, act). A fused norm layer (``fuses_relu``) absorbs the ReLU."""
     bn = norm_layer(c)
@@ -117,14 +125,16 @@ class Bottleneck(nn.Module):
             ds = self.downsample
             if ds is not None and not (ds[0].stride[0] == 2 and _ds_link()):
                 link = None
+            # the downsample's BN apply is folded into the final apply pass (ops/conv_bn.py:DeferredBN)
+            defer = _ds_defer()
             if ds is not None and link is None:
-                identity = conv1x1_bn_act(xr, ds[0], ds[1])
+                identity = conv1x1_bn_act(xr, ds[0], ds[1], defer=defer)
             out = conv1x1_bn_act(x, self.conv1, self.bn1, relu=True, link_x=link)
             out = self.act2(conv3x3_bn_relu(out, self.conv2, self.bn2))
             if ds is None:
                 identity = xr
             elif link is not None:  # issued after conv2: its backward runs before conv1's
-                identity = conv1x1_bn_act(xr, ds[0], ds[1], link_ds=link)
+                identity = conv1x1_bn_act(xr, ds[0], ds[1], link_ds=link, defer=defer)
             return conv1x1_bn_act(out, self.conv3, self.bn3, residual=identity, relu=True, dual_output=True,
                                   link_res=link if ds is None else None)
         identity = xr if self.downsample is None else self.downsample(xr)

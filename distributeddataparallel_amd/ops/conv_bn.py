@@ -61,6 +61,40 @@ class EpiLink:
         self.add_s2 = self.c1_done = False
 
 
+class DeferredBN:
+    """A downsample conv+BN whose BN apply is folded into its consumer: the downsample's output
+    tensor holds the raw conv output y, and the block's final apply pass computes
+    relu(bn3(y3) + y·scale + shift) (``bn_apply(..., residual_ss=...)``), so the identity branch
+    never makes its own read-y / write-identity pass. Autograd convention: the gradient that
+    reaches the downsample node is d(identity) — what its BN backward expects — since the only
+    consumer (the final node, or ``_ApplyDeferred`` on a fallback path) passes it through."""
+
+    __slots__ = ("ss", "nbt")
+
+    def __init__(self):
+        self.ss = self.nbt = None
+
+
+class _ApplyDeferred(torch.autograd.Function):
+    """identity = y·scale + shift for a consumer that cannot fold it (gradient passes through)."""
+
+    @staticmethod
+    def forward(ctx, y, ss, nbt):
+        C = y.size(1)
+        if nbt is not None:
+            nbt.add_(1)
+        return (y.float() * ss[:C].view(1, -1, 1, 1) + ss[C:].view(1, -1, 1, 1)).to(y.dtype).contiguous(
+            memory_format=torch.channels_last)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None, None
+
+
+def _deferred(t):
+    return getattr(t, "_xddp_bnss", None) if t is not None else None
+
+
 def _expand_s2(add, like):
     """Full-resolution gradient of a stride-2 1x1 conv's input from its compact form."""
     full = torch.zeros_like(like, memory_format=torch.channels_last)
@@ -110,7 +144,7 @@ def _same_tensor(a, b) -> bool:
 class _Conv1x1BN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, residual, relu, dual,
-                stride, link_out, link_x, link_res, link_in, link_ds):
+                stride, link_out, link_x, link_res, link_in, link_ds, defer, res_defer):
         C = load()
         ctx.set_materialize_grads(False)
         dma = _c1_dma(x, w)
@@ -131,7 +165,13 @@ class _Conv1x1BN(torch.autograd.Function):
         mean, invstd, ss = C.bn_stats_from_partials(part, M, weight, bias, running_mean, running_var, nbt, momentum,
                                                     cma, eps, dma)
         keep_mask = relu and residual is not None
-        out, bits = C.bn_apply(y, ss, residual, relu, keep_mask, nbt)
+        if defer is not None:  # the consumer applies this BN (DeferredBN): output the raw conv output
+            defer.ss, defer.nbt = ss, nbt
+            out, bits = y, None
+        elif res_defer is not None:
+            out, bits = C.bn_apply(y, ss, residual, relu, keep_mask, nbt, res_defer.ss, res_defer.nbt)
+        else:
+            out, bits = C.bn_apply(y, ss, residual, relu, keep_mask, nbt)
         ctx.relu, ctx.has_res, ctx.stride = relu, residual is not None, stride
         ctx.save_for_backward(x, w, y, bits if keep_mask else None, weight, mean, invstd, ss)
         ctx.link_out, ctx.link_x, ctx.link_res, ctx.link_in = link_out, link_x, link_res, link_in
@@ -174,7 +214,7 @@ class _Conv1x1BN(torch.autograd.Function):
         if dout is None:
             dout, dout2 = dout2, None
         if dout is None:
-            return (None,) * 19
+            return (None,) * 21
         need_bn_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         s = ctx.stride
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
@@ -260,12 +300,12 @@ class _Conv1x1BN(torch.autograd.Function):
 
 
 def _grads(ctx, dx, dw, dw_bn, db_bn, dres):
-    """The 19 input gradients of _Conv1x1BN; a linked residual gradient goes to the consumer link."""
+    """The 21 input gradients of _Conv1x1BN; a linked residual gradient goes to the consumer link."""
     if dres is not None and ctx.link_res is not None:
         ctx.link_res.add, dres = dres, None
     return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
             None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None, None, None, None,
-            None, None)
+            None, None, None, None)
 
 
 def _bwd_fused_ok(ctx, C, w) -> bool:
@@ -449,23 +489,31 @@ def conv3x3_bn_relu(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module):
 
 def conv1x1_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, residual: Optional[torch.Tensor] = None,
                    relu: bool = False, dual_output: bool = False, link_x: Optional[EpiLink] = None,
-                   link_res: Optional[EpiLink] = None, link_ds: Optional[EpiLink] = None):
+                   link_res: Optional[EpiLink] = None, link_ds: Optional[EpiLink] = None, defer: bool = False):
     """``relu(bn(conv(x)) [+ residual])`` with BN statistics from the conv epilogue when supported.
 
     link_x / link_res: the :class:`EpiLink` of the block output that is this conv's input /
     this op's residual (``x._xddp_epi`` of a dual output); with dual_output and residual + ReLU
     the returned output carries a fresh link for the next block. link_ds: this stride-2 conv is
-    the downsample sharing its input with a linked conv1 (compact input gradient to the link)."""
+    the downsample sharing its input with a linked conv1 (compact input gradient to the link).
+    defer: return the raw conv output and leave this BN's apply to the consumer that takes the
+    result as its ``residual`` (DeferredBN; only for a BN without ReLU or residual)."""
+    res_defer = _deferred(residual)
     if conv.kernel_size != (1, 1) or not conv_bn_supported(x, conv, bn) or (residual is not None and not (
             residual.shape[0] == x.shape[0] and residual.dtype == x.dtype
             and residual.is_contiguous(memory_format=torch.channels_last))):
+        if res_defer is not None:
+            residual = _ApplyDeferred.apply(residual, res_defer.ss, res_defer.nbt)
         return bn(conv(x), residual=residual, relu=relu, dual_output=dual_output)
+    dfr = DeferredBN() if (defer and residual is None and not relu and not dual_output) else None
     link_out = EpiLink() if (dual_output and residual is not None and relu and _epi()) else None
     link_in = getattr(x, "_xddp_bnr", None) if conv.stride[0] == 1 else None
     out = _Conv1x1BN.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                            bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), residual, relu,
                            dual_output, int(conv.stride[0]), link_out, link_x, link_res, link_in,
-                           link_ds if conv.stride[0] == 2 else None)
+                           link_ds if conv.stride[0] == 2 else None, dfr, res_defer)
+    if dfr is not None:
+        out._xddp_bnss = dfr
     if link_out is not None:
         out[0]._xddp_epi = link_out
     return out
