@@ -282,6 +282,7 @@ def test_downsample_epilogue_handoff_matches_separate_pass(monkeypatch):
     from distributeddataparallel_amd.models.resnet import Bottleneck, ResNet
     from distributeddataparallel_amd.ops import FusedBatchNorm2d
 
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)  # (see the DeferredBN test)
     torch.manual_seed(8)
     m = ResNet(Bottleneck, [1, 1, 2, 1], norm_layer=FusedBatchNorm2d).cuda().to(torch.bfloat16)
     m = m.to(memory_format=torch.channels_last)
@@ -348,6 +349,7 @@ def test_bottleneck_epilogue_handoff_matches_separate_pass(monkeypatch):
     from distributeddataparallel_amd.models.resnet import Bottleneck, ResNet
     from distributeddataparallel_amd.ops import FusedBatchNorm2d
 
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)  # (see the DeferredBN test)
     torch.manual_seed(6)
     m = ResNet(Bottleneck, [2, 2, 1, 1], norm_layer=FusedBatchNorm2d).cuda().to(torch.bfloat16)
     m = m.to(memory_format=torch.channels_last)
