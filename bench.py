@@ -76,6 +76,9 @@ def parse(argv=None):
                     help="hipBLASLt/rocBLAS GEMM solution selection via torch TunableOp: use = the tuned "
                          "results shipped in tuning/tunableop (auto: for transformer models), tune = search "
                          "and write gpurun_out/tunableop_<model>.csv")
+    ap.add_argument("--overlap-optim", choices=["auto", "0", "1"], default="auto",
+                    help="run the optimizer per bucket on a side stream during backward "
+                         "(DDP.register_overlapped_optimizer; auto = off)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     if a.batch_size is None:
@@ -370,6 +373,14 @@ def main(argv=None):
 
     B = args.batch_size
     micro = max(1, args.no_sync_accum)
+    # auto = off: measured no gain on one MI355X (Llama-3-8B 16,726 vs 16,779 tok/s, ViT-L/16 1,984 vs
+    # 1,970 img/s): hipBLASLt's backward GEMMs occupy every CU, so the side-stream AdamW interleaves
+    # with them instead of running beside them
+    overlap = args.overlap_optim == "1"
+    if overlap and not (args.impl == "xddp" and hasattr(opt, "step_params") and micro == 1 and not args.graphs):
+        raise SystemExit("--overlap-optim 1 needs the xddp DDP, an AdamW config, one micro-batch and no --graphs")
+    if overlap:
+        ddp.register_overlapped_optimizer(opt)
     g = torch.Generator(device=device).manual_seed(1234 + rank)
     ncls = num_classes(args, model)
     if is_lm(args):
@@ -403,7 +414,8 @@ def main(argv=None):
                 loss_fn(ddp(xs[i]), ys[i]).backward()
         loss = loss_fn(ddp(xs[-1]), ys[-1])
         loss.backward()
-        opt.step()
+        if not overlap:  # (overlapped: every bucket was stepped during backward)
+            opt.step()
         return loss
 
     for i in range(args.warmup):
@@ -481,6 +493,7 @@ def main(argv=None):
                 "norm": args.norm,
                 "optimizer": ("SGD(momentum=0.9, wd=1e-4)" + (" fp32 master weights" if gpu else "")
                               if (conv or args.model == "mlp") else "AdamW(wd=0.1) fp32 master weights"),
+                "optimizer_overlapped_with_backward": bool(overlap),
                 "channels_last": bool(args.channels_last),
                 "comm_dtype": args.comm_dtype,
                 "gradient_as_bucket_view": bool(args.grad_as_bucket_view),

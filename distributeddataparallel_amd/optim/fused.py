@@ -157,6 +157,45 @@ class FusedAdamW(Optimizer):
                     self._cpu_step(ps, gs, m1, m2, masters, group, step, grad_scale)
         return loss
 
+    @torch.no_grad()
+    def step_params(self, params, grads):
+        """Step only ``params`` with the given gradients (e.g. one DDP bucket's reduced views, from
+        an overlapped-optimizer comm hook): same update as ``step`` for those parameters."""
+        C = load()
+        if not hasattr(self, "_group_of"):
+            self._group_of = {id(p): gi for gi, grp in enumerate(self.param_groups) for p in grp["params"]}
+        per_group = defaultdict(list)
+        for p, g in zip(params, grads):
+            gi = self._group_of.get(id(p))
+            if gi is not None and g is not None:
+                per_group[gi].append((p, g))
+        for gi, pairs in per_group.items():
+            group = self.param_groups[gi]
+            b1, b2 = group["betas"]
+            buckets = defaultdict(lambda: ([], [], [], [], [], []))
+            for p, g in pairs:
+                st = self.state[p]
+                if "step" not in st:
+                    st["step"] = 0
+                    st["exp_avg"] = _dense_like(p).zero_()
+                    st["exp_avg_sq"] = _dense_like(p).zero_()
+                    if group["master_weights"] and p.dtype in (torch.bfloat16, torch.float16):
+                        st["master"] = p.detach().float().clone(memory_format=torch.preserve_format)
+                st["step"] += 1
+                b = buckets[_group_key(p, g) + (st["step"], "master" in st)]
+                b[0].append(p)
+                b[1].append(g)
+                b[2].append(st["exp_avg"])
+                b[3].append(st["exp_avg_sq"])
+                if "master" in st:
+                    b[4].append(st["master"])
+            for (dev, pdt, gdt, step, has_master), (ps, gs, m1, m2, masters, _) in buckets.items():
+                if dev.type == "cuda":
+                    C.fused_adam(ps, gs, m1, m2, masters, group["lr"], b1, b2, group["eps"], group["weight_decay"],
+                                 step, self._decoupled, group["maximize"], None)
+                else:
+                    self._cpu_step(ps, gs, m1, m2, masters, group, step, None)
+
     def _cpu_step(self, ps, gs, m1, m2, masters, group, step, grad_scale):
         b1, b2 = group["betas"]
         lr, eps, wd = group["lr"], group["eps"], group["weight_decay"]

@@ -698,6 +698,46 @@ class DistributedDataParallel(nn.Module, Joinable):
         else:
             raise ValueError(f"unknown builtin comm hook {comm_hook_type}")
 
+    def register_overlapped_optimizer(self, optimizer):
+        """Run ``optimizer.step_params`` for each bucket as soon as its all-reduce is done, on a side
+        HIP stream, so the (HBM-bound) optimizer update overlaps the (MFMA-bound) backward of the
+        layers whose buckets are still pending; the compute stream waits for the side stream at the
+        end of backward. Do not call ``optimizer.step()`` afterwards (the reference's
+        ``_register_fused_optim`` contract). Needs an optimizer with ``step_params(params, grads)``
+        (``FusedAdamW``, ``FusedAdam``)."""
+        if not hasattr(optimizer, "step_params"):
+            raise TypeError("register_overlapped_optimizer needs an optimizer with step_params (FusedAdamW)")
+        side = torch.cuda.Stream(self._param_device) if self.device_type == "cuda" else None
+        state = {"opt": optimizer, "side": side, "queued": False, "ddp": weakref.ref(self)}
+
+        def join():
+            state["queued"] = False
+            if side is not None:
+                torch.cuda.current_stream(side.device).wait_stream(side)
+
+        def hook(st, bucket):
+            ddp = st["ddp"]()
+            buf = bucket.buffer()
+            work = ddp.process_group.allreduce(buf, xdist.ReduceOp.AVG)
+            if st["side"] is None:
+                work.wait()
+                st["opt"].step_params(bucket.parameters(), bucket.gradients())
+            else:
+                # the side stream starts after everything the compute stream has enqueued (this
+                # bucket's gradients), then after the collective
+                st["side"].wait_stream(torch.cuda.current_stream(st["side"].device))
+                with torch.cuda.stream(st["side"]):
+                    work.wait()
+                    st["opt"].step_params(bucket.parameters(), bucket.gradients())
+                if not st["queued"]:
+                    st["queued"] = True
+                    torch.autograd.Variable._execution_engine.queue_callback(join)
+            fut = torch.futures.Future()
+            fut.set_result(buf)
+            return fut
+
+        self.register_comm_hook(state, hook)
+
     def _register_fused_optim(self, optim_cls, *args, optim_params=None, **kwargs):
         from .comm_hooks.optimizer_overlap_hooks import _OptimizerHookState, _hook_then_optimizer
         from .comm_hooks.default_hooks import allreduce_hook

@@ -409,3 +409,28 @@ def test_python_reducer_matches_torch_ddp():
     """T6k: the compiled-autograd "python reducer" mode (per-parameter post-accumulate-grad
     all-reduce) trains identically to torch DDP; comm hooks get (grad, param)."""
     run_ranks(_w_python_reducer, world=2)
+
+
+# --------------------------------------------------------------------------------------------
+def _w_overlapped_optimizer(rank, world):
+    import distributeddataparallel_amd as xddp
+    from distributeddataparallel_amd.optim import FusedAdamW
+
+    m1, m2 = _mlp(), _mlp()
+    d1 = xddp.DDP(m1, bucket_cap_mb=0.001)  # several buckets
+    d2 = xddp.DDP(m2)
+    d1.register_overlapped_optimizer(o1 := FusedAdamW(m1.parameters(), lr=1e-2, weight_decay=0.1))
+    o2 = FusedAdamW(m2.parameters(), lr=1e-2, weight_decay=0.1)
+    for x, y in _batches(1, 4, per_rank=4, seed=90 + rank):
+        o1.zero_grad()
+        F.cross_entropy(d1(x), y).backward()  # stepped per bucket inside backward
+        o2.zero_grad()
+        F.cross_entropy(d2(x), y).backward()
+        o2.step()
+    _assert_params_equal(m1, m2)
+
+
+def test_overlapped_optimizer_matches_step_after_backward():
+    """DDP.register_overlapped_optimizer: the per-bucket FusedAdamW.step_params inside backward
+    trains exactly like the usual backward-then-step."""
+    run_ranks(_w_overlapped_optimizer, world=2)

@@ -277,3 +277,37 @@ def test_mixed_precision_and_delayed_allreduce_gpu(pg):
         assert a.grad is not None and a.grad.dtype == torch.float32, n
         cos = F.cosine_similarity(a.grad.flatten(), b.grad.flatten(), dim=0)
         assert cos > 0.99, (n, float(cos))
+
+
+def test_overlapped_optimizer_matches_step_after_backward(pg):
+    """register_overlapped_optimizer on GPU: the per-bucket FusedAdamW steps run on a side HIP
+    stream during backward; the trained bf16 model (with fp32 masters) is bitwise the
+    backward-then-step one (stream ordering: the side stream waits for each bucket's gradients,
+    the compute stream for the side stream at the end of backward)."""
+    from distributeddataparallel_amd.models.llama import llama_tiny
+    from distributeddataparallel_amd.optim import FusedAdamW
+
+    def make():
+        torch.manual_seed(0)
+        return llama_tiny(max_seq_len=64).cuda().to(torch.bfloat16)
+
+    m1, m2 = make(), make()
+    d1 = xddp.DDP(m1, device_ids=[0], gradient_as_bucket_view=True, bucket_cap_mb=0.5)
+    d2 = xddp.DDP(m2, device_ids=[0], gradient_as_bucket_view=True, bucket_cap_mb=0.5)
+    o1 = FusedAdamW(m1.parameters(), lr=1e-3, weight_decay=0.1, master_weights=True)
+    o2 = FusedAdamW(m2.parameters(), lr=1e-3, weight_decay=0.1, master_weights=True)
+    d1.register_overlapped_optimizer(o1)
+    vocab = m1.tok_embeddings.weight.shape[0] if hasattr(m1, "tok_embeddings") else 256
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for _ in range(3):
+        x = torch.randint(0, vocab, (2, 64), device="cuda", generator=g)
+        y = torch.randint(0, vocab, (2, 64), device="cuda", generator=g)
+        for d, o, overlapped in ((d1, o1, True), (d2, o2, False)):
+            o.zero_grad(set_to_none=True)
+            out = d(x)
+            F.cross_entropy(out.float().view(-1, out.shape[-1]), y.view(-1)).backward()
+            if not overlapped:
+                o.step()
+    torch.cuda.synchronize()
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
