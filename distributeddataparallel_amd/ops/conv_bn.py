@@ -326,9 +326,9 @@ def _dgrad_in(ctx, C, g, w, coef, y):
     partials (epilogue second form)."""
     li = ctx.link_in
     # XDDP_CONV_EPI2=1 opts in. Off by default: measured 10,534 vs 10,808 img/s (ResNet-50 bs256,
-    # MI355X) — the masked-reduce epilogue on top of the BN-backward prologue pushes the dgrad GEMM
-    # past its 128-VGPR budget (45 spilled registers at 2 blocks/CU), costing more than BN2's
-    # separate reduce pass.
+    # MI355X) with 45 spilled registers at 2 blocks/CU, and still 11,746 vs 12,092-12,170 at one
+    # block/CU without spills (the EPI default since): the conv3 input-gradient GEMM re-reads y2
+    # per output tile, costing more than BN2's separate reduce pass.
     if li is None or not _epi() or os.environ.get("XDDP_CONV_EPI2", "0") != "1":
         return _dgrad(C, g, w, coef, y)
     dx, li.part = C.conv1x1_gemm(g, w, 1, coef, False, y, True, None, li.y, None, li.mean, li.ss)
