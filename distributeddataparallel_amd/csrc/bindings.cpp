@@ -221,6 +221,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("status", &PeerAllReduce::status)
       .def("close", &PeerAllReduce::close)
       .def_property_readonly("capacity", &PeerAllReduce::capacity);
+  m.def("make_peer_comm", &make_peer_comm, py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"),
+        py::arg("capacity") = 16 << 20, py::call_guard<py::gil_scoped_release>(),
+        "RCCL-free single-node communicator over IPC-mapped peer memory (device tensors)");
   m.def("make_fake_comm", &make_fake_comm, py::arg("rank"), py::arg("size"),
         "Communicator whose collectives complete locally without peers (testing at any world size)");
   m.def("install_crash_handler", &install_crash_handler,

@@ -136,6 +136,9 @@ std::shared_ptr<Comm> make_tcp_comm_host(std::shared_ptr<Store> store, int rank,
 std::shared_ptr<Comm> make_rccl_comm(std::shared_ptr<Store> store, int rank, int size, int device,
                                      std::chrono::milliseconds timeout, bool high_priority_stream);
 
+// Peer-memory backend (single node, device tensors; comm/peer_comm.cpp).
+std::shared_ptr<Comm> make_peer_comm(std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity);
+
 // Debug wrapper: per-collective cross-rank fingerprint check and/or NaN check.
 std::shared_ptr<Comm> make_debug_comm(std::shared_ptr<Comm> inner, bool fingerprint, bool nan_check);
 

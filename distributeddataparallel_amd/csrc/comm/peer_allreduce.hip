@@ -72,11 +72,15 @@ struct Acc<__half> {
   __device__ static __half put(float f) { return __float2half(f); }
 };
 
-template <typename T, bool BCAST>
+// MODE 0: all-reduce in place (MAXOP: max instead of sum); 1: broadcast from root in place;
+// 2: all-gather — io is this rank's input, out[r * n ...] receives rank r's.
+template <typename T, int MODE, bool MAXOP = false>
 __global__ __launch_bounds__(kThreads) void peer_kernel(T* __restrict__ io, int64_t n, PeerPtrs pp, int rank,
                                                         int size, int root, uint32_t* __restrict__ gen_dev,
                                                         int* __restrict__ status, float scale, bool do_scale,
-                                                        uint64_t timeout_ticks, int64_t slot_bytes, int64_t chunk) {
+                                                        uint64_t timeout_ticks, int64_t slot_bytes, int64_t chunk,
+                                                        T* __restrict__ out) {
+  constexpr bool BCAST = MODE == 1;
   constexpr int V = 16 / sizeof(T);  // elements per 16-B vector
   union Vec {
     uint4 u;
@@ -125,7 +129,15 @@ __global__ __launch_bounds__(kThreads) void peer_kernel(T* __restrict__ io, int6
 
   // 3. reduce (or read the root's copy) straight from the peers' slots
   const int64_t nv = (hi - lo) / V;
-  if (BCAST) {
+  if (MODE == 2) {
+    for (int r = 0; r < size; ++r) {
+      const T* src = reinterpret_cast<const T*>(pp.data[r] + off);
+      T* dst = out + (int64_t)r * n;
+      for (int64_t i = threadIdx.x; i < nv; i += kThreads)
+        reinterpret_cast<uint4*>(dst + lo)[i] = reinterpret_cast<const uint4*>(src + lo)[i];
+      for (int64_t i = lo + nv * V + threadIdx.x; i < hi; i += kThreads) dst[i] = src[i];
+    }
+  } else if (BCAST) {
     if (rank != root) {
       const T* src = reinterpret_cast<const T*>(pp.data[root] + off);
       for (int64_t i = threadIdx.x; i < nv; i += kThreads)
@@ -136,13 +148,14 @@ __global__ __launch_bounds__(kThreads) void peer_kernel(T* __restrict__ io, int6
     using A = typename Acc<T>::type;
     for (int64_t i = threadIdx.x; i < nv; i += kThreads) {
       A acc[V];
-#pragma unroll
-      for (int e = 0; e < V; ++e) acc[e] = A(0);
       for (int r = 0; r < size; ++r) {  // fixed rank order: every rank gets bitwise the same sum
         Vec v;
         v.u = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(pp.data[r] + off) + lo)[i];
 #pragma unroll
-        for (int e = 0; e < V; ++e) acc[e] += Acc<T>::get(v.e[e]);
+        for (int e = 0; e < V; ++e) {
+          const A x = Acc<T>::get(v.e[e]);
+          acc[e] = r == 0 ? x : (MAXOP ? (x > acc[e] ? x : acc[e]) : acc[e] + x);
+        }
       }
       Vec o;
 #pragma unroll
@@ -151,7 +164,10 @@ __global__ __launch_bounds__(kThreads) void peer_kernel(T* __restrict__ io, int6
     }
     for (int64_t i = lo + nv * V + threadIdx.x; i < hi; i += kThreads) {
       A acc = A(0);
-      for (int r = 0; r < size; ++r) acc += Acc<T>::get(reinterpret_cast<const T*>(pp.data[r] + off)[i]);
+      for (int r = 0; r < size; ++r) {
+        const A x = Acc<T>::get(reinterpret_cast<const T*>(pp.data[r] + off)[i]);
+        acc = r == 0 ? x : (MAXOP ? (x > acc ? x : acc) : acc + x);
+      }
       io[i] = Acc<T>::put(do_scale ? A(acc * scale) : acc);
     }
   }
@@ -233,16 +249,29 @@ bool PeerAllReduce::supports(const at::Tensor& t, RedOp op, bool bcast) const {
   if (bcast) return true;
   const auto st = t.scalar_type();
   const bool fl = st == at::kFloat || st == at::kBFloat16 || st == at::kHalf;
-  if (op == RedOp::SUM) return fl || st == at::kInt || st == at::kLong;
+  if (op == RedOp::SUM || op == RedOp::MAX) return fl || st == at::kInt || st == at::kLong;
   return op == RedOp::AVG && fl;
 }
 
 void PeerAllReduce::run(at::Tensor t, RedOp op, int root, bool bcast, hipStream_t s) {
   TORCH_CHECK(supports(t, op, bcast), "peer all-reduce: unsupported tensor / op");
+  launch(t, t, op, root, bcast ? 1 : 0, s);
+}
+
+void PeerAllReduce::allgather(at::Tensor out, at::Tensor in, hipStream_t s) {
+  TORCH_CHECK(supports(in, RedOp::SUM, true) && out.is_cuda() && out.is_contiguous() &&
+                  out.scalar_type() == in.scalar_type() && out.numel() == in.numel() * size_ &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "peer all-gather: unsupported tensors");
+  launch(in, out, RedOp::SUM, 0, 2, s);
+}
+
+void PeerAllReduce::launch(at::Tensor t, at::Tensor out, RedOp op, int root, int mode, hipStream_t s) {
   c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
-  // a broadcast moves bytes: as 4-B words when the size allows (whole 16-B vectors per thread)
-  const bool words = bcast && t.nbytes() % 4 == 0;
-  const int64_t esz = bcast ? (words ? 4 : 1) : t.element_size();
+  // data movement modes move bytes: as 4-B words when the size allows (whole 16-B vectors per thread)
+  const bool raw = mode != 0;
+  const bool words = raw && t.nbytes() % 4 == 0 && (mode != 2 || out.nbytes() % 4 == 0);
+  const int64_t esz = raw ? (words ? 4 : 1) : t.element_size();
   const int64_t n = (int64_t)t.nbytes() / esz, vec = 16 / esz;
   // >= 16 KiB per workgroup, at most kPeerMaxBlocks workgroups; chunks are whole 16-B vectors
   int64_t blocks = std::min<int64_t>(kPeerMaxBlocks, std::max<int64_t>(1, (int64_t)t.nbytes() / 16384));
@@ -251,23 +280,34 @@ void PeerAllReduce::run(at::Tensor t, RedOp op, int root, bool bcast, hipStream_
   blocks = (n + chunk - 1) / chunk;
   const float scale = 1.f / (float)size_;
   const bool do_scale = op == RedOp::AVG;
-  void* p = t.data_ptr();
-  auto go = [&](auto kern, auto* io) {
+  auto go = [&](auto kern, auto* io, auto* o) {
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kThreads), 0, s, io, n, impl_->pp, rank_, size_, root,
-                       impl_->gen_dev, impl_->status, scale, do_scale, impl_->timeout_ticks, (int64_t)cap_, chunk);
+                       impl_->gen_dev, impl_->status, scale, do_scale, impl_->timeout_ticks, (int64_t)cap_, chunk, o);
   };
-  if (bcast) {
-    if (words) go(peer_kernel<int32_t, true>, static_cast<int32_t*>(p));
-    else go(peer_kernel<uint8_t, true>, static_cast<uint8_t*>(p));
+  void* p = t.data_ptr();
+  void* q = out.data_ptr();
+  if (raw) {
+    if (words) {
+      if (mode == 1) go(peer_kernel<int32_t, 1>, static_cast<int32_t*>(p), static_cast<int32_t*>(q));
+      else go(peer_kernel<int32_t, 2>, static_cast<int32_t*>(p), static_cast<int32_t*>(q));
+    } else {
+      if (mode == 1) go(peer_kernel<uint8_t, 1>, static_cast<uint8_t*>(p), static_cast<uint8_t*>(q));
+      else go(peer_kernel<uint8_t, 2>, static_cast<uint8_t*>(p), static_cast<uint8_t*>(q));
+    }
   } else {
+    const bool mx = op == RedOp::MAX;
+#define XDDP_PK(T_)                                                                               \
+  if (mx) go(peer_kernel<T_, 0, true>, static_cast<T_*>(p), static_cast<T_*>(q));                 \
+  else go(peer_kernel<T_, 0, false>, static_cast<T_*>(p), static_cast<T_*>(q))
     switch (t.scalar_type()) {
-      case at::kFloat: go(peer_kernel<float, false>, static_cast<float*>(p)); break;
-      case at::kBFloat16: go(peer_kernel<uint16_t, false>, static_cast<uint16_t*>(p)); break;
-      case at::kHalf: go(peer_kernel<__half, false>, static_cast<__half*>(p)); break;
-      case at::kInt: go(peer_kernel<int32_t, false>, static_cast<int32_t*>(p)); break;
-      case at::kLong: go(peer_kernel<int64_t, false>, static_cast<int64_t*>(p)); break;
+      case at::kFloat: XDDP_PK(float); break;
+      case at::kBFloat16: XDDP_PK(uint16_t); break;
+      case at::kHalf: XDDP_PK(__half); break;
+      case at::kInt: XDDP_PK(int32_t); break;
+      case at::kLong: XDDP_PK(int64_t); break;
       default: TORCH_CHECK(false, "peer all-reduce: dtype");
     }
+#undef XDDP_PK
   }
   XDDP_HIP_CHECK(hipGetLastError());
 }

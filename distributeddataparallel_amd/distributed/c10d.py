@@ -7,7 +7,9 @@ API parity with the reference stack's ``torch.distributed`` surface that DDP use
 
 Backends (both native C++, see ``csrc/comm``):
   * ``"rccl"`` (alias ``"nccl"``) — RCCL over xGMI, one process per GPU;
-  * ``"cpu"``  (alias ``"gloo"``) — TCP ring collectives, used for GPU-free multi-process runs.
+  * ``"cpu"``  (alias ``"gloo"``) — TCP ring collectives, used for GPU-free multi-process runs;
+  * ``"peer"`` — one-shot collectives over IPC-mapped peer memory (single node, device tensors, no
+    RCCL): several ranks may share one GPU.
 """
 from __future__ import annotations
 
@@ -81,6 +83,8 @@ class Backend:
             return "cpu"
         if n == "fake":
             return "fake"
+        if n == "peer":
+            return "peer"
         raise ValueError(f"unknown backend {name!r}")
 
 
@@ -295,7 +299,7 @@ def _excepthook_prefix(rank: int):
 
 
 def _device_for(backend: str, device_id):
-    if backend != "rccl":
+    if backend not in ("rccl", "peer"):
         return torch.device("cpu")
     if device_id is None:
         local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -316,6 +320,9 @@ def _make_comm(backend: str, store, rank: int, size: int, device, timeout: timed
     if backend == "rccl":
         hp = os.environ.get("XDDP_COMM_HIGH_PRIORITY", "1") != "0"
         comm = C.make_rccl_comm(store, rank, size, device.index, timeout.total_seconds(), hp)
+    elif backend == "peer":  # IPC peer memory, one node, device tensors (csrc/comm/peer_comm.cpp)
+        cap = int(float(os.environ.get("XDDP_PEER_CAPACITY_MB", "16")) * (1 << 20)) // 4096 * 4096
+        comm = C.make_peer_comm(store, rank, size, device.index, max(cap, 4096))
     else:
         comm = C.make_cpu_comm(store, rank, size, timeout.total_seconds(), advertise_host(master_addr))
     detail = os.environ.get("XDDP_DEBUG", os.environ.get("TORCH_DISTRIBUTED_DEBUG", "OFF")).upper() == "DETAIL"
@@ -449,7 +456,7 @@ def new_group(ranks: Optional[Sequence[int]] = None, timeout: Optional[timedelta
     timeout = timeout or world.timeout
     sub_rank = ranks.index(world.rank())
     store = C.PrefixStore(name, _world.store)
-    comm = _make_comm(be, store, sub_rank, len(ranks), world.device if be == "rccl" else torch.device("cpu"),
+    comm = _make_comm(be, store, sub_rank, len(ranks), world.device if be in ("rccl", "peer") else torch.device("cpu"),
                       timeout, os.environ.get("MASTER_ADDR", "127.0.0.1"))
     pg = ProcessGroup(comm, store, sub_rank, len(ranks), be, ranks, world.device, name, timeout)
     _world.groups[name] = pg
@@ -524,7 +531,7 @@ def all_to_all_single(output, input, output_split_sizes=None, input_split_sizes=
     outs = list(output_split_sizes) if output_split_sizes is not None else [n_out // W] * W
     if len(ins) != W or len(outs) != W or sum(ins) != n_in or sum(outs) != n_out:
         raise ValueError("split sizes must have one entry per rank and sum to dim 0 of the tensors")
-    m = torch.tensor([max(ins + outs)], dtype=torch.int64, device=input.device if pg.backend == "rccl" else "cpu")
+    m = torch.tensor([max(ins + outs)], dtype=torch.int64, device=input.device if pg.backend in ("rccl", "peer") else "cpu")
     pg.allreduce(m, ReduceOp.MAX).wait()
     M = int(m.item())
     row = tuple(input.shape[1:])
@@ -610,7 +617,7 @@ def broadcast_object_list(object_list, src=0, group=None, device=None):
     import pickle
 
     pg = _resolve(group)
-    dev = pg.device if pg.backend == "rccl" else torch.device("cpu")
+    dev = pg.device if pg.backend in ("rccl", "peer") else torch.device("cpu")
     if pg.rank() == _group_rank(pg, src):
         payload = pickle.dumps(list(object_list))
         n = torch.tensor([len(payload)], dtype=torch.long, device=dev)
@@ -633,7 +640,7 @@ def all_gather_object(object_list, obj, group=None):
     import pickle
 
     pg = _resolve(group)
-    dev = pg.device if pg.backend == "rccl" else torch.device("cpu")
+    dev = pg.device if pg.backend in ("rccl", "peer") else torch.device("cpu")
     payload = pickle.dumps(obj)
     n = torch.tensor([len(payload)], dtype=torch.long, device=dev)
     sizes = torch.zeros(pg.size(), dtype=torch.long, device=dev)

@@ -125,3 +125,48 @@ print("forced-launch ok", n)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0 and "forced-launch ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+@pytest.mark.parametrize("grad_as_view,accum", [(True, 1), (False, 2)])
+def test_two_ranks_one_gpu_ddp_parity_peer_backend(grad_as_view, accum, monkeypatch):
+    """The same W=2 DDP parity on the RCCL-free peer-memory backend: bucket all-reduces, the
+    parameter/buffer broadcasts and the verification all-gather run as device-side one-shot
+    kernels between the two processes (csrc/comm/peer_comm.cpp); a 1 MiB staging capacity makes the
+    larger buckets take the chunked path."""
+    monkeypatch.setenv("XDDP_PEER_CAPACITY_MB", "1")
+    run_ranks(_w_gpu_parity, world=2, backend="peer", args=(grad_as_view, accum))
+
+
+def _w_peer_collectives(rank, world):
+    from distributeddataparallel_amd import distributed as dist
+
+    torch.cuda.set_device(0)
+    n = 300_001  # > the 64 KiB capacity set below: several chunks, ragged tail
+    base = torch.arange(n, device="cuda", dtype=torch.float32)
+    t = base + rank
+    dist.all_reduce(t)
+    torch.testing.assert_close(t, 2 * base + 1)
+    t = base * (rank + 1)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    torch.testing.assert_close(t, base * world)
+    t = (base + rank).to(torch.bfloat16)
+    dist.all_reduce(t, op=dist.ReduceOp.AVG)
+    torch.testing.assert_close(t.float(), (base + 0.5).to(torch.bfloat16).float(), rtol=1e-2, atol=1.0)
+    t = torch.full((n,), float(rank), device="cuda")
+    dist.broadcast(t, 1)
+    assert torch.equal(t, torch.ones(n, device="cuda"))
+    g = torch.empty(world * n, device="cuda")
+    dist.all_gather_into_tensor(g, base + 10 * rank)
+    assert torch.equal(g.view(world, n)[1], base + 10)
+    out = torch.empty(n, device="cuda")
+    dist.reduce_scatter_tensor(out, torch.cat([base, base + 1]) + rank)
+    torch.testing.assert_close(out, 2 * (base + rank) + 1)
+    dist.barrier()
+    torch.cuda.synchronize()
+
+
+def test_peer_backend_collectives(monkeypatch):
+    """init_process_group("peer"): all-reduce (SUM / MAX / AVG in bf16), broadcast from rank 1,
+    all-gather and reduce-scatter, all through the chunked path (64 KiB staging)."""
+    monkeypatch.setenv("XDDP_PEER_CAPACITY_MB", "0.0625")
+    run_ranks(_w_peer_collectives, world=2, backend="peer")
