@@ -51,7 +51,8 @@ def parse(argv=None):
     ap.add_argument("--batch-size", type=int, default=None, help="per-rank (micro-)batch")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
-    ap.add_argument("--backend", default=None, help="xddp backend: rccl (GPU default) or cpu")
+    ap.add_argument("--backend", default=None, help="xddp backend: rccl (GPU default), peer (IPC peer memory, "
+                    "ranks may share a GPU) or cpu")
     ap.add_argument("--impl", choices=["xddp", "torch"], default="xddp",
                     help="xddp = this framework; torch = torch.nn.parallel.DDP reference stack (comparison only)")
     ap.add_argument("--norm", choices=["xddp", "torch"], default="xddp", help="BatchNorm implementation")
@@ -327,9 +328,12 @@ def main(argv=None):
     import torch.nn.functional as F
 
     gpu = args.device == "cuda"
+    dev_index = local_rank
+    if gpu and args.backend in ("peer", "cpu"):  # these backends let several ranks share a GPU
+        dev_index = local_rank % max(1, torch.cuda.device_count())
     if gpu:
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
         torch.backends.cudnn.benchmark = bool(int(os.environ.get("XDDP_CUDNN_BENCHMARK", "0")))
     else:
         device = torch.device("cpu")
@@ -347,7 +351,7 @@ def main(argv=None):
         from distributeddataparallel_amd.parallel.bucket_policy import rccl_env_defaults
 
         rccl_env = rccl_env_defaults(world, args.backend)
-        dist.init_process_group(args.backend, device_id=local_rank if gpu else None)
+        dist.init_process_group(args.backend, device_id=dev_index if gpu else None)
     else:
         import torch.distributed as dist
 
@@ -358,7 +362,7 @@ def main(argv=None):
     conv = is_conv(args)
     if args.impl == "xddp":
         comm_dtype = None if args.comm_dtype == "none" else getattr(torch, args.comm_dtype)
-        ddp = xddp.DDP(model, device_ids=[local_rank] if gpu else None, bucket_cap_mb=args.bucket_cap_mb,
+        ddp = xddp.DDP(model, device_ids=[dev_index] if gpu else None, bucket_cap_mb=args.bucket_cap_mb,
                        bucket_policy=args.bucket_policy, gradient_as_bucket_view=bool(args.grad_as_bucket_view),
                        comm_dtype=comm_dtype)
         if conv or args.model == "mlp":

@@ -25,7 +25,7 @@ class PeerAllReduce {
   PeerAllReduce& operator=(const PeerAllReduce&) = delete;
 
   // Contiguous, 16-B aligned CUDA tensor on this device of at most capacity bytes; all-reduce:
-  // SUM / MAX of fp32/bf16/fp16/int32/int64 or AVG of the floating types; broadcast: any dtype.
+  // SUM / MAX of fp64/fp32/bf16/fp16/int32/int64 or AVG of the floating types; broadcast: any dtype.
   bool supports(const at::Tensor& t, RedOp op, bool bcast = false) const;
   // In-place on stream s (identical sequence of calls on every rank).
   void run(at::Tensor t, RedOp op, int root, bool bcast, hipStream_t s);

@@ -248,7 +248,7 @@ bool PeerAllReduce::supports(const at::Tensor& t, RedOp op, bool bcast) const {
   if (t.nbytes() == 0 || (int64_t)t.nbytes() > cap_ || reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) return false;
   if (bcast) return true;
   const auto st = t.scalar_type();
-  const bool fl = st == at::kFloat || st == at::kBFloat16 || st == at::kHalf;
+  const bool fl = st == at::kFloat || st == at::kBFloat16 || st == at::kHalf || st == at::kDouble;
   if (op == RedOp::SUM || op == RedOp::MAX) return fl || st == at::kInt || st == at::kLong;
   return op == RedOp::AVG && fl;
 }
@@ -301,6 +301,7 @@ void PeerAllReduce::launch(at::Tensor t, at::Tensor out, RedOp op, int root, int
   else go(peer_kernel<T_, 0, false>, static_cast<T_*>(p), static_cast<T_*>(q))
     switch (t.scalar_type()) {
       case at::kFloat: XDDP_PK(float); break;
+      case at::kDouble: XDDP_PK(double); break;
       case at::kBFloat16: XDDP_PK(uint16_t); break;
       case at::kHalf: XDDP_PK(__half); break;
       case at::kInt: XDDP_PK(int32_t); break;
