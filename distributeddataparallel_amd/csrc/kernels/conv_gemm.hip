@@ -1073,7 +1073,13 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
     const char* e = std::getenv("XDDP_GEMM_EPI_OCC");
     return e ? (std::atoi(e) == 4 ? 4 : 2) : 2;
   }();
-  const int kocc = epi_on ? epi_occ : occ;
+  // the BN-backward-prologue input gradients' own choice (XDDP_GEMM_PRO_OCC): 4 measured better
+  // (12,224-12,227 vs 12,117-12,123 img/s at 2, ResNet-50 bs256)
+  static const int pro_occ = [] {
+    const char* e = std::getenv("XDDP_GEMM_PRO_OCC");
+    return e ? (std::atoi(e) == 2 ? 2 : 4) : 4;
+  }();
+  const int kocc = epi_on ? epi_occ : (pro >= 2 ? pro_occ : occ);
   const int target = num_cus() * (kocc == 2 ? 1 : blocks_per_cu);
   int groups = std::max(1, std::min(mtiles, (target + ntiles - 1) / ntiles));
   at::Tensor part = stats ? at::empty({groups, 3, N}, x.options().dtype(at::kFloat))
