@@ -1054,7 +1054,18 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
                   "conv1x1_gemm: epilogue scale/shift must be float [2, N]");
     }
   }
-  const int BM = 128, BN = (N % 128 == 0) ? 128 : 64;
+  const int BN = (N % 128 == 0) ? 128 : 64;
+  // The BN-reduce epilogue GEMM on 64x128 tiles (8 waves of 32x32, two blocks per CU, 128 VGPRs
+  // without spills): half the live epilogue registers of the 128x128 tile, so two tiles' loads
+  // are in flight per CU — 271/157/89/73 vs 337/190/104/79 us on the ResNet-50 stage shapes
+  // (profiles/r2_epi_dgrad_shapes.txt), 12,418-12,422 vs 12,120-12,154 img/s.
+  // XDDP_GEMM_EPI_BM=128 keeps the 128x128 tile at one block per CU.
+  static const bool epi_bm64 = [] {
+    const char* e = std::getenv("XDDP_GEMM_EPI_BM");
+    return !(e && std::atoi(e) == 128);
+  }();
+  const bool bm64 = epi_on && epi_bm64 && BN == 128;
+  const int BM = bm64 ? 64 : 128;
   const int mtiles = (int)((M + BM - 1) / BM), ntiles = (int)(N / BN);
   // 2-3 blocks per CU resident (LDS 48-64 KB, <= 128 VGPRs): size the grid to a few rounds
   static const int blocks_per_cu = [] {
@@ -1079,7 +1090,7 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
     const char* e = std::getenv("XDDP_GEMM_PRO_OCC");
     return e ? (std::atoi(e) == 2 ? 2 : 4) : 4;
   }();
-  const int kocc = epi_on ? epi_occ : (pro >= 2 ? pro_occ : occ);
+  const int kocc = bm64 ? 4 : (epi_on ? epi_occ : (pro >= 2 ? pro_occ : occ));
   const int target = num_cus() * (kocc == 2 ? 1 : blocks_per_cu);
   int groups = std::max(1, std::min(mtiles, (target + ntiles - 1) / ntiles));
   at::Tensor part = stats ? at::empty({groups, 3, N}, x.options().dtype(at::kFloat))
@@ -1106,7 +1117,13 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
 #define XDDP_LG(BN_, WM_, WN_, OCC_)                                                                            \
   launch_gemm<128, BN_, WM_, WN_, OCC_>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, \
                                         mtiles, ntiles, groups, x2p, epi)
-  if (BN == 128) { if (kocc == 2) XDDP_LG(128, 4, 2, 2); else XDDP_LG(128, 4, 2, 4); }
+  if (bm64) {  // (EPI implies w_t; pro is 0 or the BN-backward form 2)
+    auto kern = pro == 2 ? conv1x1_gemm_kernel<64, 128, 2, 4, 2, false, false, true, true, 4>
+                         : conv1x1_gemm_kernel<64, 128, 2, 4, 0, false, false, true, true, 4>;
+    hipLaunchKernelGGL(kern, grid, dim3(512), lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,
+                       groups, x2p, epi);
+    XDDP_HIP_CHECK(hipGetLastError());
+  } else if (BN == 128) { if (kocc == 2) XDDP_LG(128, 4, 2, 2); else XDDP_LG(128, 4, 2, 4); }
   else { if (kocc == 2) XDDP_LG(64, 8, 1, 2); else XDDP_LG(64, 8, 1, 4); }
 #undef XDDP_LG
   return {y, part};
