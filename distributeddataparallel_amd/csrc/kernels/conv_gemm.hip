@@ -1064,7 +1064,17 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
     const char* e = std::getenv("XDDP_GEMM_EPI_BM");
     return !(e && std::atoi(e) == 128);
   }();
-  const bool bm64 = epi_on && epi_bm64 && BN == 128;
+  // A/B: XDDP_GEMM_BM64=fwd,pro also puts the forward-with-statistics GEMM and/or the
+  // BN-backward-prologue input gradient on 64x128 tiles (measured: fwd 12,304, pro 12,446 vs
+  // 12,438-12,454 img/s default — neither pays, unlike the epilogue-heavy EPI GEMM)
+  static const int bm64_other = [] {
+    const char* e = std::getenv("XDDP_GEMM_BM64");
+    const std::string v = e ? e : "";
+    return (v.find("fwd") != std::string::npos ? 1 : 0) | (v.find("pro") != std::string::npos ? 2 : 0);
+  }();
+  const bool bm64_gen = BN == 128 && !epi_on &&
+                        (((bm64_other & 1) && stats && pro == 0 && !w_t) || ((bm64_other & 2) && pro >= 2 && w_t));
+  const bool bm64 = (epi_on && epi_bm64 && BN == 128) || bm64_gen;
   const int BM = bm64 ? 64 : 128;
   const int mtiles = (int)((M + BM - 1) / BM), ntiles = (int)(N / BN);
   // 2-3 blocks per CU resident (LDS 48-64 KB, <= 128 VGPRs): size the grid to a few rounds
@@ -1117,7 +1127,10 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
 #define XDDP_LG(BN_, WM_, WN_, OCC_)                                                                            \
   launch_gemm<128, BN_, WM_, WN_, OCC_>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, \
                                         mtiles, ntiles, groups, x2p, epi)
-  if (bm64) {  // (EPI implies w_t; pro is 0 or the BN-backward form 2)
+  if (bm64_gen) {
+    launch_gemm<64, 128, 2, 4, 4>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles,
+                                  ntiles, groups, x2p, epi);
+  } else if (bm64) {  // (EPI implies w_t; pro is 0 or the BN-backward form 2)
     auto kern = pro == 2 ? conv1x1_gemm_kernel<64, 128, 2, 4, 2, false, false, true, true, 4>
                          : conv1x1_gemm_kernel<64, 128, 2, 4, 0, false, false, true, true, 4>;
     hipLaunchKernelGGL(kern, grid, dim3(512), lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,
