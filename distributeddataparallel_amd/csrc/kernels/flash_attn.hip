@@ -31,7 +31,8 @@
 // with the KEY on the lane, so P and dS are directly the B operands of dV^T += dO^T·P and
 // dK^T += Q^T·dS); dQ kernel (8 waves x 32 query rows; S^T and dP^T with the query on the lane,
 // dQ^T += K^T·dS^T). No atomics: dQ and dK/dV are separate passes (S and dP are recomputed in
-// both), each bitwise reproducible.
+// both), each bitwise reproducible — except when one workgroup holds every key of a head (D = 64,
+// non-causal, Sk <= 256: ViT), where the dK/dV kernel also produces dQ from its dS (FQ below).
 //
 // MI355X, Llama-3-8B shape (B1 S4096 H32/8 D128 causal): fwd 0.358 ms, fwd+bwd 1.434 ms vs torch
 // SDPA (AOTriton) 0.421 / 2.272 ms; ViT-L/16 (B64 S197 H16 D64): 0.038 / 0.278 vs 0.061 / 0.349 ms
@@ -50,6 +51,7 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 using dev::u32x4;
 
@@ -425,13 +427,21 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_kernel(
 // accumulators. Q / dO / lse / delta tiles go global -> LDS by LDS-DMA (no VGPR staging), two
 // stages per group: item k + 1 is in flight while item k is computed; one barrier per item.
 // Registers: K 32 + dK^T 64 + dV^T 64 + S, dP 32 (D = 128) stay under the 256 of two waves/SIMD.
-template <int D, bool CAUSAL, int KW>
+//
+// FQ (KW = 8 only: every key of the head is in this workgroup) also produces dQ, so the separate
+// dQ pass — a second read of Q, K, V, dO and a second S / dP evaluation — is skipped: each item's
+// dS (bf16, [32 queries][256 keys]) goes to LDS next to K^T ([64][256], staged once from the K
+// registers), and after one barrier every wave computes one 16 x 16 tile of dQ^T = K^T · dS^T on
+// mfma_f32_16x16x32_bf16 over all 256 keys (d = 16 (w & 3).., q = 16 (w >> 2)..): no cross-wave
+// reduction, no atomics. Both LDS images are [row][256] bf16 with the 16-B chunk index XOR'd by
+// row & 15, so the 16 rows a b128 lane group reads sit in 16 distinct bank groups.
+template <int D, bool CAUSAL, int KW, bool FQ = false>
 __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq, int Sk, int Hq, int Hkv, Strides qs, Strides ks,
     Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale, int nsplit,
-    float* __restrict__ wsk, float* __restrict__ wsv) {
+    float* __restrict__ wsk, float* __restrict__ wsv, uint16_t* __restrict__ dQo, Strides dqs) {
   constexpr int NG = 8 / KW, BK = 32 * KW;          // groups; keys per workgroup
   constexpr int KS = D / 16, NT = D / 32, QB = 32;  // query rows per work item
   constexpr int TILE = QB * D * 2;                  // bytes of one Q (or dO) tile
@@ -443,7 +453,9 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
   constexpr int ACC = NT * 16 * 64;                 // floats of one wave's dK^T (or dV^T)
   static_assert(KW >= 2 && KW * NG == 8 && NIT % NI == 0 && (NIT < KW || NI * KW == NIT), "wave split");
   static_assert((NG - 1) * KW * ACC * 4 <= VBLK + 2 * NG * STAGE, "group reduction must fit the LDS");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[VBLK + 2 * NG * STAGE];
+  static_assert(!FQ || (KW == 8 && D == 64 && !CAUSAL), "fused dQ: one 256-key block, D = 64, non-causal");
+  constexpr int FQB = FQ ? (D + QB) * BK * 2 : 0;  // K^T [D][BK] + dS [QB][BK], bf16
+  __shared__ __attribute__((aligned(16))) uint8_t smem[VBLK + 2 * NG * STAGE + FQB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wq = w % KW, G = w / KW, g = lane >> 5;
   // blockIdx.x = (batch, kv head, head split), blockIdx.y = key block: the dispatcher walks x
   // first, so every workgroup of key block 0 (the heaviest under a causal mask) starts first.
@@ -472,6 +484,20 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
   for (int s = 0; s < KS; ++s)
     kf[s] = krow < Sk ? *reinterpret_cast<const bf16x8*>(K + b * ks.b + hk * ks.h + (int64_t)krow * ks.s + 16 * s + 8 * g)
                       : bf16x8{};
+  // (FQ) byte offset of element [row][col] of a [row][BK] bf16 LDS image, chunk-swizzled
+  auto fq_off = [](int row, int col) { return row * (BK * 2) + (((col >> 3) ^ (row & 15)) << 4) + (col & 7) * 2; };
+  uint8_t* KT = smem + VBLK + 2 * NG * STAGE;
+  uint8_t* DSl = KT + D * BK * 2;
+  const int kl = 32 * wq + (lane & 31);  // this lane's key within the block
+  if constexpr (FQ) {  // K^T image from the K registers (zero rows past Sk come along)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const u32x4 kv = __builtin_bit_cast(u32x4, kf[s]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        *reinterpret_cast<uint16_t*>(KT + fq_off(16 * s + 8 * g + e, kl)) = (uint16_t)(kv[e >> 1] >> (16 * (e & 1)));
+    }
+  }
   f32x16 adk[NT], adv[NT];
 #pragma unroll
   for (int n = 0; n < NT; ++n)
@@ -540,10 +566,38 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
           dk4[e] = dev::pack_bf16x2(dp[8 * hh + 2 * e], dp[8 * hh + 2 * e + 1]);
         }
         const bf16x8 pf = __builtin_bit_cast(bf16x8, pk), sf = __builtin_bit_cast(bf16x8, dk4);
+        if constexpr (FQ) {  // dS[query][key] -> LDS (element 8 hh + 2 e + j: query kappa(g, 2 e + j) + 16 hh)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              *reinterpret_cast<uint16_t*>(DSl + fq_off(kappa(g, 2 * e + j) + 16 * hh, kl)) =
+                  (uint16_t)(dk4[e] >> (16 * j));
+        }
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
           adv[n] = mfma32(ld_trfrag<D>(Dt, 16 * hh, 32 * n, lane), pf, adv[n]);
           adk[n] = mfma32(ld_trfrag<D>(Qt, 16 * hh, 32 * n, lane), sf, adk[n]);
+        }
+      }
+      if constexpr (FQ) {  // (uniform: one group, non-causal) every wave's dS tile has landed
+        lds_barrier();
+        const int d0 = 16 * (w & 3), q0 = 16 * (w >> 2), r16 = lane & 15, kq = lane >> 4;
+        f32x4v aq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < BK / 32; ++s) {
+          const int col = 32 * s + 8 * kq;
+          aq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(KT + fq_off(d0 + r16, col)),
+                                                       *reinterpret_cast<const bf16x8*>(DSl + fq_off(q0 + r16, col)),
+                                                       aq, 0, 0, 0);
+        }
+        // lane: dQ[query q0 + r16][d0 + 4 kq .. + 3]
+        const int h = hk * grp + split * hpw + it / nqt, qrow = qt0 + q0 + r16;
+        if (qrow < Sq) {
+          uint2 o;
+          o.x = dev::pack_bf16x2(aq[0] * scale, aq[1] * scale);
+          o.y = dev::pack_bf16x2(aq[2] * scale, aq[3] * scale);
+          *reinterpret_cast<uint2*>(dQo + b * dqs.b + h * dqs.h + (int64_t)qrow * dqs.s + d0 + 4 * kq) = o;
         }
       }
     }
@@ -733,7 +787,20 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
     if (D == 128) go(fa_bwd_pre_kernel<128>, 16); else go(fa_bwd_pre_kernel<64>, 8);
   }
   const float sl2 = (float)(scale * 1.4426950408889634), sc = (float)scale;
-  {
+  static const int kw_env = [] {
+    const char* e = std::getenv("XDDP_FA_DKDV_KW");
+    return e ? std::atoi(e) : 0;  // 0 = by shape
+  }();
+  // short non-causal D = 64 sequences (ViT): the whole key range in one 8-wave block
+  // (XDDP_FA_DKDV_KW=4 keeps two 128-key blocks), which then also computes dQ
+  // (XDDP_FA_FUSED_DQ=0: the separate dQ pass instead)
+  const int kwv = kw_env == 2 || kw_env == 4 ? kw_env : (D == 64 && !causal && Sk <= 256 ? 8 : 4);
+  static const bool fdq_env = [] {
+    const char* e = std::getenv("XDDP_FA_FUSED_DQ");
+    return !(e && std::atoi(e) == 0);
+  }();
+  const bool fused_dq = kwv == 8 && fdq_env;
+  if (!fused_dq) {
     static const int nw_env = [] {
       const char* e = std::getenv("XDDP_FA_WAVES");
       return e ? std::atoi(e) : 0;
@@ -758,13 +825,6 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
 #undef XDDP_FA
   }
   {
-    static const int kw_env = [] {
-      const char* e = std::getenv("XDDP_FA_DKDV_KW");
-      return e ? std::atoi(e) : 0;  // 0 = by shape
-    }();
-    // short non-causal D = 64 sequences (ViT): the whole key range in one 8-wave block
-    // (XDDP_FA_DKDV_KW=4 keeps two 128-key blocks)
-    const int kwv = kw_env == 2 || kw_env == 4 ? kw_env : (D == 64 && !causal && Sk <= 256 ? 8 : 4);
     const int nkb = (int)((Sk + 32 * kwv - 1) / (32 * kwv));
     // GQA head split for causal attention (balance, see the kernel); XDDP_FA_DKDV_SPLIT overrides
     static const int split_env = [] {
@@ -789,13 +849,14 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
                          reinterpret_cast<uint16_t*>(dv.data_ptr()), (int)Sq, (int)Sk, (int)Hq, (int)Hkv, strides_of(q),
                          strides_of(k), strides_of(v), strides_of(dout), strides_of(dk), strides_of(dv), sl2, sc,
                          nsplit, nsplit > 1 ? wsk.data_ptr<float>() : nullptr,
-                         nsplit > 1 ? wsv.data_ptr<float>() : nullptr);
+                         nsplit > 1 ? wsv.data_ptr<float>() : nullptr, reinterpret_cast<uint16_t*>(dq.data_ptr()),
+                         strides_of(dq));
       XDDP_HIP_CHECK(hipGetLastError());
     };
 #define XDDP_FA(D_, C_) \
   if (kwv == 4) go(fa_bwd_dkdv_kernel<D_, C_, 4>); else go(fa_bwd_dkdv_kernel<D_, C_, 2>)
     if (D == 128) { if (causal) { XDDP_FA(128, true); } else { XDDP_FA(128, false); } }
-    else if (kwv == 8) { go(fa_bwd_dkdv_kernel<64, false, 8>); }
+    else if (kwv == 8) { if (fused_dq) go(fa_bwd_dkdv_kernel<64, false, 8, true>); else go(fa_bwd_dkdv_kernel<64, false, 8>); }
     else { if (causal) { XDDP_FA(64, true); } else { XDDP_FA(64, false); } }
 #undef XDDP_FA
     if (nsplit > 1) {  // the split-sum writes dense [B, Sk, Hkv, D]: strided outputs get a copy
