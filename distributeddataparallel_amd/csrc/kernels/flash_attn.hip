@@ -430,10 +430,10 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_kernel(
 //
 // FQ (KW = 8 only: every key of the head is in this workgroup) also produces dQ, so the separate
 // dQ pass — a second read of Q, K, V, dO and a second S / dP evaluation — is skipped: each item's
-// dS (bf16, [32 queries][256 keys]) goes to LDS next to K^T ([64][256], staged once from the K
-// registers), and after one barrier every wave computes one 16 x 16 tile of dQ^T = K^T · dS^T on
-// mfma_f32_16x16x32_bf16 over all 256 keys (d = 16 (w & 3).., q = 16 (w >> 2)..): no cross-wave
-// reduction, no atomics. Both LDS images are [row][256] bf16 with the 16-B chunk index XOR'd by
+// dS (bf16, [32 queries][256 keys]) goes to one of two LDS buffers next to K^T ([64][256], staged
+// once from the K registers), and after the NEXT item's barrier (no extra one) every wave computes
+// one 16 x 16 tile of that item's dQ^T = K^T · dS^T on mfma_f32_16x16x32_bf16 over all 256 keys
+// (d = 16 (w & 3).., q = 16 (w >> 2)..): no cross-wave reduction, no atomics. Both LDS images are [row][256] bf16 with the 16-B chunk index XOR'd by
 // row & 15, so the 16 rows a b128 lane group reads sit in 16 distinct bank groups.
 template <int D, bool CAUSAL, int KW, bool FQ = false>
 __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
@@ -454,7 +454,8 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
   static_assert(KW >= 2 && KW * NG == 8 && NIT % NI == 0 && (NIT < KW || NI * KW == NIT), "wave split");
   static_assert((NG - 1) * KW * ACC * 4 <= VBLK + 2 * NG * STAGE, "group reduction must fit the LDS");
   static_assert(!FQ || (KW == 8 && D == 64 && !CAUSAL), "fused dQ: one 256-key block, D = 64, non-causal");
-  constexpr int FQB = FQ ? (D + QB) * BK * 2 : 0;  // K^T [D][BK] + dS [QB][BK], bf16
+  constexpr int DSB = QB * BK * 2;                   // (FQ) one dS [QB][BK] bf16 buffer
+  constexpr int FQB = FQ ? D * BK * 2 + 2 * DSB : 0;  // K^T [D][BK] + two dS buffers
   __shared__ __attribute__((aligned(16))) uint8_t smem[VBLK + 2 * NG * STAGE + FQB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wq = w % KW, G = w / KW, g = lane >> 5;
   // blockIdx.x = (batch, kv head, head split), blockIdx.y = key block: the dispatcher walks x
@@ -528,11 +529,35 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(S + 2 * TILE + wq * QB * 4), 4, 0, 0);
     }
   };
+  // (FQ) dQ of item itq from its dS buffer: wave w owns the 16 x 16 tile d = 16 (w & 3).., q = 16 (w >> 2)..
+  auto dq_tile = [&](int itq, const uint8_t* dsb) {
+    const int d0 = 16 * (w & 3), q0 = 16 * (w >> 2), r16 = lane & 15, kq = lane >> 4;
+    f32x4v aq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < BK / 32; ++s) {
+      const int col = 32 * s + 8 * kq;
+      aq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(KT + fq_off(d0 + r16, col)),
+                                                   *reinterpret_cast<const bf16x8*>(dsb + fq_off(q0 + r16, col)), aq,
+                                                   0, 0, 0);
+    }
+    // lane: dQ[query q0 + r16][d0 + 4 kq .. + 3]
+    const int h = hk * grp + split * hpw + itq / nqt, qrow = qstart + (itq % nqt) * QB + q0 + r16;
+    if (qrow < Sq) {
+      uint2 o;
+      o.x = dev::pack_bf16x2(aq[0] * scale, aq[1] * scale);
+      o.y = dev::pack_bf16x2(aq[2] * scale, aq[3] * scale);
+      *reinterpret_cast<uint2*>(dQo + b * dqs.b + h * dqs.h + (int64_t)qrow * dqs.s + d0 + 4 * kq) = o;
+    }
+  };
   if (G < total) issue(G, 0);
   for (int k = 0; k < niter; ++k) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     const int it = G + NG * k;
     if (it + NG < total) issue(it + NG, (k + 1) & 1);  // into the stage item k - 1 was computed from
+    // (FQ: one group, non-causal, so every item is computed) item k - 1's dQ: its dS landed before
+    // the barrier above; the buffer is rewritten at item k + 1, after the next barrier
+    if constexpr (FQ)
+      if (k > 0) dq_tile(it - 1, DSl + ((k - 1) & 1) * DSB);
     const int qt0 = qstart + (it % nqt) * QB;
     if (it < total && (!CAUSAL || qt0 + QB - 1 >= kw)) {
       const uint8_t* Qt = gsm + (k & 1) * STAGE;
@@ -571,7 +596,7 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
           for (int e = 0; e < 4; ++e)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-              *reinterpret_cast<uint16_t*>(DSl + fq_off(kappa(g, 2 * e + j) + 16 * hh, kl)) =
+              *reinterpret_cast<uint16_t*>(DSl + (k & 1) * DSB + fq_off(kappa(g, 2 * e + j) + 16 * hh, kl)) =
                   (uint16_t)(dk4[e] >> (16 * j));
         }
 #pragma unroll
@@ -580,26 +605,12 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
           adk[n] = mfma32(ld_trfrag<D>(Qt, 16 * hh, 32 * n, lane), sf, adk[n]);
         }
       }
-      if constexpr (FQ) {  // (uniform: one group, non-causal) every wave's dS tile has landed
-        lds_barrier();
-        const int d0 = 16 * (w & 3), q0 = 16 * (w >> 2), r16 = lane & 15, kq = lane >> 4;
-        f32x4v aq = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < BK / 32; ++s) {
-          const int col = 32 * s + 8 * kq;
-          aq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(KT + fq_off(d0 + r16, col)),
-                                                       *reinterpret_cast<const bf16x8*>(DSl + fq_off(q0 + r16, col)),
-                                                       aq, 0, 0, 0);
-        }
-        // lane: dQ[query q0 + r16][d0 + 4 kq .. + 3]
-        const int h = hk * grp + split * hpw + it / nqt, qrow = qt0 + q0 + r16;
-        if (qrow < Sq) {
-          uint2 o;
-          o.x = dev::pack_bf16x2(aq[0] * scale, aq[1] * scale);
-          o.y = dev::pack_bf16x2(aq[2] * scale, aq[3] * scale);
-          *reinterpret_cast<uint2*>(dQo + b * dqs.b + h * dqs.h + (int64_t)qrow * dqs.s + d0 + 4 * kq) = o;
-        }
-      }
+    }
+  }
+  if constexpr (FQ) {  // the last item's dQ
+    if (niter > 0) {
+      lds_barrier();
+      dq_tile(niter - 1, DSl + ((niter - 1) & 1) * DSB);
     }
   }
   // groups 1..NG-1 hand their partial dK^T, then dV^T, to group 0 through the (now idle) LDS
