@@ -34,9 +34,9 @@
 // both), each bitwise reproducible — except when one workgroup holds every key of a head (D = 64,
 // non-causal, Sk <= 256: ViT), where the dK/dV kernel also produces dQ from its dS (FQ below).
 //
-// MI355X, Llama-3-8B shape (B1 S4096 H32/8 D128 causal): fwd 0.358 ms, fwd+bwd 1.434 ms vs torch
-// SDPA (AOTriton) 0.421 / 2.272 ms; ViT-L/16 (B64 S197 H16 D64): 0.038 / 0.278 vs 0.061 / 0.349 ms
-// (profiles/r2_flash_attn.txt).
+// MI355X, Llama-3-8B shape (B1 S4096 H32/8 D128 causal): fwd 0.174 ms, fwd+bwd 0.939 ms vs torch
+// SDPA (AOTriton) 0.423 / 2.286 ms; ViT-L/16 (B64 S197 H16 D64): 0.043 / 0.190 vs 0.062 / 0.352 ms
+// (profiles/r2_flash_attn_v3.txt).
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
