@@ -71,6 +71,8 @@ def parse(argv=None):
     ap.add_argument("--diag-steps", type=int, default=3,
                     help="untimed steps after the timed region with comm timers on every step")
     ap.add_argument("--busbw-iters", type=int, default=5, help="all-reduce bandwidth probe iterations (N>1)")
+    ap.add_argument("--probe-peer", type=int, default=0,
+                    help="N>1: also probe the two-shot peer-memory all-reduce at the bucket sizes")
     ap.add_argument("--baseline-json", default=None, help="N=1 result line -> scaling_efficiency")
     ap.add_argument("--launch-timeout", type=float, default=1500.0, help="self-launch: kill children after this")
     ap.add_argument("--tunableop", choices=["auto", "off", "use", "tune"], default="auto",
@@ -79,7 +81,8 @@ def parse(argv=None):
                          "and write gpurun_out/tunableop_<model>.csv")
     ap.add_argument("--overlap-optim", choices=["auto", "0", "1"], default="auto",
                     help="run the optimizer per bucket on a side stream during backward "
-                         "(DDP.register_overlapped_optimizer; auto = off)")
+                         "(DDP.register_overlapped_optimizer; auto = on for AdamW (transformer) configs at "
+                         "N>1, where it hides the last bucket's all-reduce, off otherwise)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     if a.batch_size is None:
@@ -377,11 +380,14 @@ def main(argv=None):
 
     B = args.batch_size
     micro = max(1, args.no_sync_accum)
-    # auto = off: measured no gain on one MI355X (Llama-3-8B 16,726 vs 16,779 tok/s, ViT-L/16 1,984 vs
-    # 1,970 img/s): hipBLASLt's backward GEMMs occupy every CU, so the side-stream AdamW interleaves
-    # with them instead of running beside them
-    overlap = args.overlap_optim == "1"
-    if overlap and not (args.impl == "xddp" and hasattr(opt, "step_params") and micro == 1 and not args.graphs):
+    # auto: at N=1 there is nothing to hide and it measured no gain on one MI355X (Llama-3-8B 16,726
+    # vs 16,779 tok/s, ViT-L/16 1,984 vs 1,970 img/s: hipBLASLt's backward GEMMs occupy every CU, so
+    # the side-stream AdamW interleaves with them). At N>1 the last bucket's all-reduce is exposed
+    # (Llama's 1.05 GB embedding gradient is ready last and forms the tail alone); the other
+    # buckets' updates run under it.
+    overlap_ok = args.impl == "xddp" and hasattr(opt, "step_params") and micro == 1 and not args.graphs
+    overlap = args.overlap_optim == "1" or (args.overlap_optim == "auto" and world > 1 and overlap_ok)
+    if overlap and not overlap_ok:
         raise SystemExit("--overlap-optim 1 needs the xddp DDP, an AdamW config, one micro-batch and no --graphs")
     if overlap:
         ddp.register_overlapped_optimizer(opt)
@@ -422,9 +428,12 @@ def main(argv=None):
             opt.step()
         return loss
 
+    first_loss = None
     for i in range(args.warmup):
         tw = time.perf_counter()
         loss = step()
+        if first_loss is None:
+            first_loss = float(loss.float().item())
         if rank == 0:
             sync()
             print(f"[bench] warmup step {i + 1}/{args.warmup}: {time.perf_counter() - tw:.2f}s", file=sys.stderr,
@@ -447,7 +456,7 @@ def main(argv=None):
     # ---------------- diagnostics (outside the timed region)
     diag = {}
     if args.impl == "xddp":
-        diag = diagnostics(args, ddp, step, sync, dist, device, world)
+        diag = diagnostics(args, ddp, step, sync, dist, device, world, overlap)
 
     ms = elapsed / args.steps * 1e3
     per_step_samples = B * micro * world
@@ -506,9 +515,13 @@ def main(argv=None):
                 "rccl_env_defaults": rccl_env,
                 "gemm_tuning": tunableop or "off",
             },
+            "initial_loss": round(first_loss, 4) if first_loss is not None else None,
             "final_loss": round(final_loss, 4),
             "scaling_efficiency": eff,
         }
+        if first_loss is not None and (final_loss != final_loss or final_loss > 2.0 * first_loss):
+            # diverging run guard: the number is still a throughput, but say the training blew up
+            out["warning"] = f"loss diverged: final {final_loss:.4g} > 2x first warmup step {first_loss:.4g}"
         if flops:
             tf = flops * per_step_samples / (ms * 1e-3) / 1e12
             out["model_tflops_per_gpu"] = round(tf / world, 1)
@@ -523,7 +536,7 @@ def main(argv=None):
     return 0
 
 
-def diagnostics(args, ddp, step, sync, dist, device, world):
+def diagnostics(args, ddp, step, sync, dist, device, world, overlap=False):
     """Comm observability: communicator rank count, rebuilt buckets, sampled
     backward comm / overlap (Reducer hipEvent timers on every diagnostic step), and the
     achieved all-reduce bus bandwidth of each bucket size when N>1."""
@@ -534,6 +547,18 @@ def diagnostics(args, ddp, step, sync, dist, device, world):
     out = {"nranks": int(pg.comm.size()), "comm_backend": pg.backend}
     sizes = list(red.bucket_sizes_bytes())
     out["buckets"] = {"count": len(sizes), "bytes": sizes, **ddp.bucket_plan.as_dict()}
+    from distributeddataparallel_amd.parallel.bucket_policy import tail_report
+
+    out["buckets"]["tail"] = tail_report(sizes, ddp.bucket_plan, world, overlap)
+    # what the communicator itself reports (RCCL at N>1: version, ranks, channels and rings parsed
+    # from its init log) and every rank's device
+    info = pg.comm_info()
+    if world > 1:
+        dev = torch.tensor([device.index if device.type == "cuda" else -1], dtype=torch.long, device=device)
+        allv = torch.zeros(world, dtype=torch.long, device=device)
+        pg.allgather_into_tensor(allv, dev).wait()
+        info["rank_devices"] = [int(v) for v in allv.tolist()]
+    out["comm_info"] = info
     if args.graphs or args.diag_steps <= 0:
         return out
     red.reset_runtime_stats()
@@ -542,42 +567,65 @@ def diagnostics(args, ddp, step, sync, dist, device, world):
         step()
         sync()  # timers are harvested at the next forward only once their events completed
     d = ddp._get_ddp_logging_data()
-    comm = d.get("avg_backward_comm_time", 0) / 1e6
-    ov = d.get("avg_backward_compute_comm_overlap_time", 0) / 1e6
+    launched = int(d.get("num_collectives_launched") or 0)
+    ms = lambda k: None if d.get(k) is None else round(d[k] / 1e6, 3)  # noqa: E731
+    # Comm = the collectives' own durations (hipEvents on the comm stream); exposed = backward end
+    # (last bucket launched) -> finalize end. Nothing is reported as comm when no collective crossed
+    # a link (N=1: every collective is a local identity).
+    comm = ms("avg_backward_comm_time") if launched else None
+    ov = ms("avg_backward_compute_comm_overlap_time") if launched else None
     out["comm"] = {
-        "avg_backward_compute_ms": round(d.get("avg_backward_compute_time", 0) / 1e6, 3),
-        "avg_backward_comm_ms": round(comm, 3),
-        "avg_overlap_ms": round(ov, 3),
-        "exposed_comm_ms": round(max(0.0, comm - ov), 3),
-        "overlap_pct": round(100.0 * ov / comm, 1) if comm > 0 else None,
-        "timed_iterations": int(d.get("num_timed_iterations", 0)),
-        "grouped_launches": int(d.get("num_grouped_launches", 0)),
+        "collectives_launched": launched,
+        "avg_backward_compute_ms": ms("avg_backward_compute_time"),
+        "avg_backward_comm_ms": comm,
+        "avg_overlap_ms": ov,
+        "exposed_comm_ms": ms("avg_backward_exposed_comm_time") if launched else None,
+        "overlap_pct": round(100.0 * ov / comm, 1) if (launched and comm) else None,
+        "per_bucket_comm_ms": [round(t / 1e6, 4) for t in d.get("bucket_comm_times", [])] if launched else None,
+        "timed_iterations": int(d.get("num_timed_iterations") or 0),
+        "grouped_launches": int(d.get("num_grouped_launches") or 0),
     }
     ddp._set_ddp_runtime_logging_sample_rate(100)
     if world > 1 and args.busbw_iters > 0:
-        probes = []
         dt = next(p for p in ddp.module.parameters()).dtype
         if ddp._comm_dtype is not None:
             dt = ddp._comm_dtype
         esz = torch.empty(0, dtype=dt).element_size()
-        for nbytes in sorted(set(sizes)):
+
+        def probe(run, nbytes):
             buf = torch.ones(max(1, nbytes // esz), dtype=dt, device=device)
             for _ in range(2):
-                pg.allreduce(buf, dist.ReduceOp.AVG).wait()
+                run(buf)
             sync()
             dist.barrier()
             t0 = time.perf_counter()
             for _ in range(args.busbw_iters):
-                pg.allreduce(buf, dist.ReduceOp.AVG).wait()
+                run(buf)
             sync()
             t = (time.perf_counter() - t0) / args.busbw_iters
             tt = torch.tensor([t], dtype=torch.float64, device=device)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             t = float(tt.item())
-            probes.append({"bytes": nbytes, "ms": round(t * 1e3, 4),
-                           "busbw_GBps": round(2.0 * (world - 1) / world * nbytes / t / 1e9, 1)})
-            del buf
-        out["allreduce_busbw"] = probes
+            return {"bytes": nbytes, "ms": round(t * 1e3, 4),
+                    "busbw_GBps": round(2.0 * (world - 1) / world * nbytes / t / 1e9, 1)}
+
+        out["allreduce_busbw"] = [probe(lambda b: pg.allreduce(b, dist.ReduceOp.AVG).wait(), n)
+                                  for n in sorted(set(sizes))]
+        if args.probe_peer and pg.backend == "rccl" and device.type == "cuda" and world <= 8:
+            # the same sizes through the two-shot peer-memory all-reduce (all 7 xGMI links)
+            from distributeddataparallel_amd._native import load
+
+            C = load()
+            peer = C.PeerAllReduce(C.PrefixStore("bench_peer", pg.store), pg.rank(), world, device.index,
+                                   1 << 20, 64 << 20, 60.0)
+            try:
+                out["peer_two_shot_busbw"] = [probe(lambda b: peer.allreduce_two_shot(b, 1), n)
+                                              for n in sorted(set(sizes))]
+                if peer.status() != 0:
+                    out["peer_two_shot_busbw"] = "timed out"
+            finally:
+                sync()
+                peer.close()
     return out
 
 

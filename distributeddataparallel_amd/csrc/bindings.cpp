@@ -153,7 +153,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("is_completed", &Work::is_completed, py::call_guard<py::gil_scoped_release>())
       .def("synchronize", &Work::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("result", &Work::result)
-      .def_readonly("seq", &Work::seq);
+      .def_readonly("seq", &Work::seq)
+      .def_readonly("collective", &Work::collective)
+      .def("timing_state", [](Work& w) {
+        auto s = w.timing_state();
+        return s == Work::Timing::kNone ? "none" : (s == Work::Timing::kPending ? "pending" : "ready");
+      })
+      .def("comm_ms", &Work::comm_ms);
 
   py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
       .def("rank", &Comm::rank)
@@ -172,6 +178,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("group_end", &Comm::group_end, py::call_guard<py::gil_scoped_release>())
       .def("abort", &Comm::abort, py::call_guard<py::gil_scoped_release>())
       .def("shutdown", &Comm::shutdown, py::call_guard<py::gil_scoped_release>())
+      .def("set_timing", &Comm::set_timing)
+      .def("timing", &Comm::timing)
+      .def("info", &Comm::info)
       .def("flight_records", [](Comm& c) {
         py::list out;
         for (auto& e : c.flight().dump()) {
@@ -206,24 +215,44 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       }, py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("timeout_s") = 600.0,
       py::arg("high_priority") = true, py::call_guard<py::gil_scoped_release>());
   py::class_<PeerAllReduce, std::shared_ptr<PeerAllReduce>>(m, "PeerAllReduce",
-      "One-shot small-message all-reduce / broadcast over IPC-mapped peer buffers (xGMI)")
-      .def(py::init<std::shared_ptr<Store>, int, int, int, int64_t>(), py::arg("store"), py::arg("rank"),
-           py::arg("size"), py::arg("device"), py::arg("capacity") = 1 << 20, py::call_guard<py::gil_scoped_release>())
+      "Peer-memory collectives over IPC-mapped staging buffers (xGMI): one-shot and two-shot all-reduce")
+      .def(py::init([](std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity,
+                       int64_t two_shot_capacity, double timeout_s) {
+             return std::make_shared<PeerAllReduce>(std::move(store), rank, size, device, capacity, two_shot_capacity,
+                                                    std::chrono::milliseconds(static_cast<int64_t>(timeout_s * 1000)));
+           }), py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("capacity") = 1 << 20,
+           py::arg("two_shot_capacity") = 0, py::arg("timeout_s") = 600.0, py::call_guard<py::gil_scoped_release>())
       .def("supports", [](PeerAllReduce& p, const at::Tensor& t, int op, bool bcast) {
              return p.supports(t, static_cast<RedOp>(op), bcast);
            }, py::arg("t"), py::arg("op") = 0, py::arg("bcast") = false)
+      .def("supports_two_shot", [](PeerAllReduce& p, const at::Tensor& t, int op) {
+             return p.supports_two_shot(t, static_cast<RedOp>(op));
+           }, py::arg("t"), py::arg("op") = 0)
       .def("allreduce", [](PeerAllReduce& p, at::Tensor t, int op) {
              p.allreduce(t, static_cast<RedOp>(op), c10::hip::getCurrentHIPStream(t.device().index()).stream());
+           }, py::arg("t"), py::arg("op") = 0)
+      .def("allreduce_two_shot", [](PeerAllReduce& p, at::Tensor t, int op) {
+             p.allreduce_two_shot(t, static_cast<RedOp>(op),
+                                  c10::hip::getCurrentHIPStream(t.device().index()).stream());
            }, py::arg("t"), py::arg("op") = 0)
       .def("broadcast", [](PeerAllReduce& p, at::Tensor t, int root) {
              p.broadcast(t, root, c10::hip::getCurrentHIPStream(t.device().index()).stream());
            }, py::arg("t"), py::arg("root") = 0)
+      .def("allgather", [](PeerAllReduce& p, at::Tensor out, at::Tensor in) {
+             p.allgather(out, in, c10::hip::getCurrentHIPStream(in.device().index()).stream());
+           }, py::arg("out"), py::arg("in"))
       .def("status", &PeerAllReduce::status)
       .def("close", &PeerAllReduce::close)
-      .def_property_readonly("capacity", &PeerAllReduce::capacity);
-  m.def("make_peer_comm", &make_peer_comm, py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"),
-        py::arg("capacity") = 16 << 20, py::call_guard<py::gil_scoped_release>(),
-        "RCCL-free single-node communicator over IPC-mapped peer memory (device tensors)");
+      .def_property_readonly("capacity", &PeerAllReduce::capacity)
+      .def_property_readonly("two_shot_capacity", &PeerAllReduce::two_shot_capacity)
+      .def_property_readonly("timeout_ms", &PeerAllReduce::timeout_ms);
+  m.def("make_peer_comm", [](std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity,
+                             int64_t two_shot_capacity, double timeout_s) {
+        return make_peer_comm(std::move(store), rank, size, device, capacity, two_shot_capacity,
+                              std::chrono::milliseconds(static_cast<int64_t>(timeout_s * 1000)));
+      }, py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("capacity") = 16 << 20,
+      py::arg("two_shot_capacity") = 64 << 20, py::arg("timeout_s") = 600.0, py::call_guard<py::gil_scoped_release>(),
+      "RCCL-free single-node communicator over IPC-mapped peer memory (device tensors)");
   m.def("make_fake_comm", &make_fake_comm, py::arg("rank"), py::arg("size"),
         "Communicator whose collectives complete locally without peers (testing at any world size)");
   m.def("install_crash_handler", &install_crash_handler,
@@ -312,6 +341,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("check_finalized", &Reducer::check_finalized)
       .def("static_graph", &Reducer::static_graph)
       .def("runtime_stats", &Reducer::runtime_stats)
+      .def("bucket_comm_times", &Reducer::bucket_comm_times)
       .def("construction_data", &Reducer::construction_data)
       .def("native_launches", &Reducer::native_launches)
       .def("remove_autograd_hooks", &Reducer::remove_autograd_hooks)

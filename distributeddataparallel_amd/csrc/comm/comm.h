@@ -17,6 +17,7 @@
 #include <deque>
 #include <exception>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -27,8 +28,16 @@
 
 namespace xddp {
 
+// A point in time a collective's interval can be compared against: a hipEvent recorded on the
+// same device (device backends) or a steady-clock timestamp (CPU backend).
+struct TimeRef {
+  hipEvent_t ev = nullptr;
+  int64_t ns = 0;
+};
+
 class Work {
  public:
+  enum class Timing { kNone, kPending, kReady };
   virtual ~Work() = default;
   // Non-blocking completion query.
   virtual bool is_completed() = 0;
@@ -38,8 +47,20 @@ class Work {
   // Block the host until the collective has finished on the device.
   virtual void synchronize() { wait(); }
   virtual std::vector<at::Tensor> result() { return outputs; }
+
+  // Collective timing, measured where the collective ran (timing-enabled hipEvents around the
+  // launch on the comm stream; the worker thread's clock on the CPU backend). Only works issued
+  // while Comm::set_timing(true) are timed. A grouped launch (RCCL group) is timed as one interval
+  // reported by the first work of the group; the others report 0 ms.
+  virtual Timing timing_state() { return Timing::kNone; }
+  virtual double comm_ms() { return 0.0; }
+  // Milliseconds of the collective's interval that lie before `ref` (clamped to [0, comm_ms]).
+  virtual double comm_ms_before(const TimeRef& /*ref*/) { return 0.0; }
+
   std::vector<at::Tensor> outputs;
   int64_t seq = -1;
+  // false: nothing crossed a link (a one-rank identity; the fake backend)
+  bool collective = true;
 };
 
 struct FlightEntry {
@@ -111,6 +132,21 @@ class Comm : public std::enable_shared_from_this<Comm> {
   virtual void group_end() {}
   virtual void abort() {}
   virtual void shutdown() {}
+  // Time the collectives issued from now on (see Work::comm_ms). Off by default: the events
+  // cost a little on every launch, so the Reducer turns it on only for its sampled iterations.
+  virtual void set_timing(bool on) { timing_ = on; }
+  bool timing() const { return timing_; }
+  // The works issued while timing was on, in launch order (cleared by the call). The Reducer
+  // drains them after a sampled backward: bucket all-reduces, comm-hook collectives, the
+  // find-unused bitmap — everything that crossed a link during that backward.
+  virtual std::vector<std::shared_ptr<Work>> drain_timed_works() {
+    std::lock_guard<std::mutex> g(timed_mu_);
+    std::vector<std::shared_ptr<Work>> out;
+    out.swap(timed_log_);
+    return out;
+  }
+  // Backend facts for logs/benchmarks (RCCL: version, channel count seen at init, ...).
+  virtual std::map<std::string, std::string> info() const { return {{"backend", backend()}}; }
 
   virtual FlightRecorder& flight() { return flight_; }
   // Writes the flight record to $XDDP_FLIGHT_DUMP_PREFIX<rank>.json (default
@@ -121,8 +157,15 @@ class Comm : public std::enable_shared_from_this<Comm> {
   bool debug_fingerprint = false;
 
  protected:
+  void log_timed(std::shared_ptr<Work> w) {
+    std::lock_guard<std::mutex> g(timed_mu_);
+    if (timed_log_.size() < 4096) timed_log_.push_back(std::move(w));
+  }
   int rank_, size_;
   FlightRecorder flight_;
+  std::atomic<bool> timing_{false};
+  std::mutex timed_mu_;
+  std::vector<std::shared_ptr<Work>> timed_log_;
 };
 
 // CPU backend ---------------------------------------------------------------------------
@@ -136,8 +179,10 @@ std::shared_ptr<Comm> make_tcp_comm_host(std::shared_ptr<Store> store, int rank,
 std::shared_ptr<Comm> make_rccl_comm(std::shared_ptr<Store> store, int rank, int size, int device,
                                      std::chrono::milliseconds timeout, bool high_priority_stream);
 
-// Peer-memory backend (single node, device tensors; comm/peer_comm.cpp).
-std::shared_ptr<Comm> make_peer_comm(std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity);
+// Peer-memory backend (single node, device tensors; comm/peer_comm.cpp). capacity = one-shot
+// staging bytes, two_shot_capacity = two-shot staging bytes (0: one-shot only).
+std::shared_ptr<Comm> make_peer_comm(std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity,
+                                     int64_t two_shot_capacity, std::chrono::milliseconds timeout);
 
 // Debug wrapper: per-collective cross-rank fingerprint check and/or NaN check.
 std::shared_ptr<Comm> make_debug_comm(std::shared_ptr<Comm> inner, bool fingerprint, bool nan_check);

@@ -54,6 +54,12 @@ class DebugComm : public Comm {
   void group_end() override { inner_->group_end(); }
   void abort() override { inner_->abort(); }
   void shutdown() override { inner_->shutdown(); }
+  void set_timing(bool on) override {
+    Comm::set_timing(on);
+    inner_->set_timing(on);
+  }
+  std::map<std::string, std::string> info() const override { return inner_->info(); }
+  std::vector<std::shared_ptr<Work>> drain_timed_works() override { return inner_->drain_timed_works(); }
   std::shared_ptr<Comm> inner() const { return inner_; }
   FlightRecorder& flight() override { return inner_->flight(); }
 

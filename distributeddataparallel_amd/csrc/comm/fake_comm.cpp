@@ -43,6 +43,7 @@ class FakeComm : public Comm {
  private:
   std::shared_ptr<Work> done(const char* name, const at::Tensor& meta, std::vector<at::Tensor> outs) {
     auto w = std::make_shared<DoneWork>();
+    w->collective = false;
     w->seq = flight_.record(name, meta.defined() ? meta.numel() : 0, meta.defined() ? meta.scalar_type() : at::kByte);
     flight_.finish(w->seq, "completed");
     w->outputs = std::move(outs);

@@ -1,23 +1,35 @@
-// One-shot all-reduce / broadcast over IPC-mapped peer buffers (xGMI), for latency-bound small
-// messages: DDP's per-forward buffer broadcast, the 1 MiB first bucket,
-// the find-unused bitmap, join/no_sync flags.
+// Peer-memory collectives over IPC-mapped staging buffers on an MI355X node (SURVEY.md §5.8
+// item 3). Every GPU has a direct xGMI link to each of the other seven, so a collective does not
+// need a ring: ranks stage their input in their own IPC-exported buffer and read each other's
+// staged copies straight over the links.
 //
-// On an MI355X node every GPU has a direct xGMI link to every other one, so a small message does
-// not need a ring: each rank stages its input in its own (uncached, IPC-exported) buffer, raises
-// a flag in every peer's buffer, waits for the peers' flags, then reads all peers' staged copies
-// straight over xGMI and reduces them in registers — one kernel, one network hop, no RCCL
-// protocol setup. Per workgroup the message chunk is independent (its own flags), so there is no
-// grid-wide barrier.
+// Two lanes, each with its own staging buffer, flags and per-workgroup call counters:
 //
-// Synchronisation (per workgroup b, per call):
-//   gen = gen_dev[b] + 1 (a device-side counter: the same kernel replayed from a HIP graph still
-//   advances it); stage into slot gen & 1; fence (system scope); store gen into flag [b][me] of
-//   every rank (release, system scope); spin until every flag [b][r] of my buffer is >= gen
-//   (acquire; a fast peer may already have written gen + 1); read the peers' slot gen & 1.
-//   Double-buffered slots are safe: a peer can only overwrite slot gen & 1 again at call gen + 2,
-//   which needs my flag for gen + 1, raised only after my call gen finished (stream order).
-// Every spin is bounded by the wall clock (XDDP_PEER_TIMEOUT_MS, default 10 s): a missing peer
-// sets the status word and the workgroup exits, so the grid always drains.
+//  * one-shot (latency-bound messages: the per-forward buffer broadcast, the find-unused bitmap,
+//    the small first bucket): stage, one flag barrier, every rank reads ALL peers' copies and
+//    reduces them in registers. One network hop, but each rank pulls (W-1)·S bytes.
+//  * two-shot (bucket-sized messages): stage, barrier, rank r reduces slice r (1/W of the
+//    message) by reading that slice from all W-1 peers at once, writes the result back into its
+//    own staging slot, barrier, then every rank gathers the other W-1 reduced slices. Each rank
+//    pulls 2(W-1)/W·S bytes and the reads of one launch are spread over all seven links — the
+//    all-links bound of §5.8 (≈7 × 153 GB/s) instead of one ring's single link.
+//
+// Synchronisation, per lane and per workgroup b:
+//   gen = gen_dev[b] + 1 is this workgroup's call number (a device-side counter, so a HIP-graph
+//   replay of the same kernel still advances it). EVERY launch of a lane runs the lane's whole grid
+//   — workgroups without data only take part in the barriers — so all workgroups of a lane agree on
+//   gen and the double-buffer slot (gen & 1) is a property of the CALL, not of the workgroup: a
+//   fast rank's call k+1 writes the other slot than the one its peers may still be reading for call
+//   k, whatever the chunking of the two calls. A barrier raises flag [b][me] in every rank's buffer
+//   (release, system scope) and spins until all flags [b][r] of my buffer reach the value (acquire;
+//   a fast peer may already be further). One-shot calls use the value 2·gen, two-shot calls 2·gen-1
+//   and 2·gen (flags only grow). Slot reuse is safe: a rank writes slot gen & 1 again at call
+//   gen + 2, which needs every peer's first flag of call gen + 1, raised only after that peer's
+//   call gen had finished (stream order).
+// Every spin is bounded by the wall clock. A workgroup whose peer does not arrive in time sets the
+// host-mapped status word (the communicator's watchdog and Work completion read it without a
+// device sync and turn it into an error), still advances its counter and exits, so the grid always
+// drains; the collective's output is then invalid and the communicator is torn down.
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_fp16.h>
@@ -34,7 +46,6 @@ namespace xddp {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kFlagBytes = kPeerMaxBlocks * kPeerMaxRanks * 4;
 
 struct PeerPtrs {
   uint8_t* data[kPeerMaxRanks];  // rank r's staging slots (slot s at s * slot_bytes)
@@ -47,6 +58,30 @@ __device__ __forceinline__ uint32_t ld_acquire_sys(const uint32_t* p) {
 
 __device__ __forceinline__ void st_release_sys(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Cross-rank barrier of workgroup b at value `val`. Returns false (and raises the status word)
+// when a peer did not arrive within the timeout.
+__device__ __forceinline__ bool flag_barrier(const PeerPtrs& pp, int b, int rank, int size, uint32_t val,
+                                             int* status, uint64_t timeout_ticks, int* s_ok) {
+  __threadfence_system();  // every thread's staging stores are visible system-wide before the flags go out
+  __syncthreads();
+  if (threadIdx.x < size) {
+    st_release_sys(pp.flags[threadIdx.x] + b * kPeerMaxRanks + rank, val);
+    const uint32_t* f = pp.flags[rank] + b * kPeerMaxRanks + threadIdx.x;
+    const uint64_t t0 = wall_clock64();
+    while (ld_acquire_sys(f) < val) {
+      if (wall_clock64() - t0 > timeout_ticks) {
+        *s_ok = 0;
+        __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __threadfence_system();  // acquire side for the threads that did not poll
+  return *s_ok != 0;
 }
 
 // element <-> accumulator conversions (bf16 and fp16 reduce in fp32, integers in their own type)
@@ -72,12 +107,23 @@ struct Acc<__half> {
   __device__ static __half put(float f) { return __float2half(f); }
 };
 
+template <typename T>
+__device__ __forceinline__ void copy_range(T* __restrict__ dst, const T* __restrict__ src, int64_t lo, int64_t hi) {
+  constexpr int V = 16 / sizeof(T);
+  if (hi <= lo) return;
+  const int64_t nv = (hi - lo) / V;  // lo is a multiple of V
+  for (int64_t i = threadIdx.x; i < nv; i += kThreads)
+    reinterpret_cast<uint4*>(dst + lo)[i] = reinterpret_cast<const uint4*>(src + lo)[i];
+  for (int64_t i = lo + nv * V + threadIdx.x; i < hi; i += kThreads) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------------------------- one-shot
 // MODE 0: all-reduce in place (MAXOP: max instead of sum); 1: broadcast from root in place;
 // 2: all-gather — io is this rank's input, out[r * n ...] receives rank r's.
 template <typename T, int MODE, bool MAXOP = false>
 __global__ __launch_bounds__(kThreads) void peer_kernel(T* __restrict__ io, int64_t n, PeerPtrs pp, int rank,
                                                         int size, int root, uint32_t* __restrict__ gen_dev,
-                                                        int* __restrict__ status, float scale, bool do_scale,
+                                                        int* status, float scale, bool do_scale,
                                                         uint64_t timeout_ticks, int64_t slot_bytes, int64_t chunk,
                                                         T* __restrict__ out) {
   constexpr bool BCAST = MODE == 1;
@@ -95,80 +141,123 @@ __global__ __launch_bounds__(kThreads) void peer_kernel(T* __restrict__ io, int6
   }
   __syncthreads();
   const uint32_t gen = s_gen;
-  const int64_t lo = (int64_t)b * chunk, hi = min(n, lo + chunk);  // chunk is a multiple of V
+  const int64_t lo = min(n, (int64_t)b * chunk), hi = min(n, lo + chunk);  // chunk is a multiple of V
   const int64_t off = (int64_t)(gen & 1u) * slot_bytes;
   T* mine = reinterpret_cast<T*>(pp.data[rank] + off);
 
-  // 1. stage this workgroup's chunk
-  if (!BCAST || rank == root) {
+  // 1. stage this workgroup's chunk (empty for the workgroups past the end of the message)
+  if (!BCAST || rank == root) copy_range(mine, io, lo, hi);
+  // 2. cross-rank barrier on this workgroup's flags
+  if (flag_barrier(pp, b, rank, size, 2u * gen, status, timeout_ticks, &s_ok)) {
+    // 3. reduce (or read the root's copy) straight from the peers' slots
     const int64_t nv = (hi - lo) / V;
-    for (int64_t i = threadIdx.x; i < nv; i += kThreads)
-      reinterpret_cast<uint4*>(mine + lo)[i] = reinterpret_cast<const uint4*>(io + lo)[i];
-    for (int64_t i = lo + nv * V + threadIdx.x; i < hi; i += kThreads) mine[i] = io[i];
-  }
-  // 2. cross-rank barrier on this workgroup's flags (every thread's staging stores are made
-  // visible system-wide before the flags go out)
-  __threadfence_system();
-  __syncthreads();
-  if (threadIdx.x < size) {
-    st_release_sys(pp.flags[threadIdx.x] + b * kPeerMaxRanks + rank, gen);
-    const uint32_t* f = pp.flags[rank] + b * kPeerMaxRanks + threadIdx.x;
-    const uint64_t t0 = wall_clock64();
-    while (ld_acquire_sys(f) < gen) {
-      if (wall_clock64() - t0 > timeout_ticks) {
-        s_ok = 0;
-        __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-  if (!s_ok) return;  // a peer never arrived: leave io untouched, status says why
-  __threadfence_system();  // acquire side for the threads that did not poll
-
-  // 3. reduce (or read the root's copy) straight from the peers' slots
-  const int64_t nv = (hi - lo) / V;
-  if (MODE == 2) {
-    for (int r = 0; r < size; ++r) {
-      const T* src = reinterpret_cast<const T*>(pp.data[r] + off);
-      T* dst = out + (int64_t)r * n;
-      for (int64_t i = threadIdx.x; i < nv; i += kThreads)
-        reinterpret_cast<uint4*>(dst + lo)[i] = reinterpret_cast<const uint4*>(src + lo)[i];
-      for (int64_t i = lo + nv * V + threadIdx.x; i < hi; i += kThreads) dst[i] = src[i];
-    }
-  } else if (BCAST) {
-    if (rank != root) {
-      const T* src = reinterpret_cast<const T*>(pp.data[root] + off);
-      for (int64_t i = threadIdx.x; i < nv; i += kThreads)
-        reinterpret_cast<uint4*>(io + lo)[i] = reinterpret_cast<const uint4*>(src + lo)[i];
-      for (int64_t i = lo + nv * V + threadIdx.x; i < hi; i += kThreads) io[i] = src[i];
-    }
-  } else {
-    using A = typename Acc<T>::type;
-    for (int64_t i = threadIdx.x; i < nv; i += kThreads) {
-      A acc[V];
-      for (int r = 0; r < size; ++r) {  // fixed rank order: every rank gets bitwise the same sum
-        Vec v;
-        v.u = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(pp.data[r] + off) + lo)[i];
+    if (MODE == 2) {
+      for (int r = 0; r < size; ++r)
+        copy_range(out + (int64_t)r * n, reinterpret_cast<const T*>(pp.data[r] + off), lo, hi);
+    } else if (BCAST) {
+      if (rank != root) copy_range(io, reinterpret_cast<const T*>(pp.data[root] + off), lo, hi);
+    } else {
+      using A = typename Acc<T>::type;
+      for (int64_t i = threadIdx.x; i < nv; i += kThreads) {
+        A acc[V];
+        for (int r = 0; r < size; ++r) {  // fixed rank order: every rank gets bitwise the same sum
+          Vec v;
+          v.u = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(pp.data[r] + off) + lo)[i];
 #pragma unroll
-        for (int e = 0; e < V; ++e) {
-          const A x = Acc<T>::get(v.e[e]);
-          acc[e] = r == 0 ? x : (MAXOP ? (x > acc[e] ? x : acc[e]) : acc[e] + x);
+          for (int e = 0; e < V; ++e) {
+            const A x = Acc<T>::get(v.e[e]);
+            acc[e] = r == 0 ? x : (MAXOP ? (x > acc[e] ? x : acc[e]) : acc[e] + x);
+          }
         }
+        Vec o;
+#pragma unroll
+        for (int e = 0; e < V; ++e) o.e[e] = Acc<T>::put(do_scale ? A(acc[e] * scale) : acc[e]);
+        reinterpret_cast<uint4*>(io + lo)[i] = o.u;
       }
+      for (int64_t i = lo + nv * V + threadIdx.x; i < hi; i += kThreads) {
+        A acc = A(0);
+        for (int r = 0; r < size; ++r) {
+          const A x = Acc<T>::get(reinterpret_cast<const T*>(pp.data[r] + off)[i]);
+          acc = r == 0 ? x : (MAXOP ? (x > acc ? x : acc) : acc + x);
+        }
+        io[i] = Acc<T>::put(do_scale ? A(acc * scale) : acc);
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) gen_dev[b] = gen;  // also after a timeout: the call is over for this workgroup
+}
+
+// ---------------------------------------------------------------------------------- two-shot
+// Workgroup b owns chunk [b*chunk, (b+1)*chunk) of the message; slice s of the chunk is
+// [lo + s*cs, lo + (s+1)*cs), cs = chunk / W (a multiple of the 16-B vector). Rank r reduces slice r.
+template <typename T, int W>
+__global__ __launch_bounds__(kThreads) void two_shot_kernel(T* __restrict__ io, int64_t n, PeerPtrs pp, int rank,
+                                                            uint32_t* __restrict__ gen_dev, int* status, float scale,
+                                                            bool do_scale, uint64_t timeout_ticks, int64_t slot_bytes,
+                                                            int64_t chunk) {
+  constexpr int V = 16 / sizeof(T);
+  using A = typename Acc<T>::type;
+  union Vec {
+    uint4 u;
+    T e[V];
+  };
+  const int b = blockIdx.x;
+  __shared__ uint32_t s_gen;
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) {
+    s_gen = gen_dev[b] + 1u;
+    s_ok = 1;
+  }
+  __syncthreads();
+  const uint32_t gen = s_gen;
+  const int64_t off = (int64_t)(gen & 1u) * slot_bytes;
+  const int64_t cs = chunk / W;
+  const int64_t lo = min(n, (int64_t)b * chunk), hi = min(n, lo + chunk);
+  const int64_t my_lo = min(hi, lo + rank * cs), my_hi = min(hi, my_lo + cs);
+  T* mine = reinterpret_cast<T*>(pp.data[rank] + off);
+
+  // 1. stage the slices the peers will reduce (not my own: I reduce it from io directly)
+  copy_range(mine, io, lo, my_lo);
+  copy_range(mine, io, my_hi, hi);
+  if (flag_barrier(pp, b, rank, W, 2u * gen - 1u, status, timeout_ticks, &s_ok)) {
+    // 2. reduce my slice from every rank, in rank order (every rank gets bitwise the same sum);
+    // the result goes to io and to my staging slot, where the peers gather it from
+    const T* src[W];
+#pragma unroll
+    for (int r = 0; r < W; ++r) src[r] = r == rank ? io : reinterpret_cast<const T*>(pp.data[r] + off);
+    const int64_t nv = (my_hi - my_lo) / V;
+    for (int64_t i = threadIdx.x; i < nv; i += kThreads) {
+      Vec v[W];
+#pragma unroll
+      for (int r = 0; r < W; ++r) v[r].u = reinterpret_cast<const uint4*>(src[r] + my_lo)[i];  // W loads in flight
       Vec o;
 #pragma unroll
-      for (int e = 0; e < V; ++e) o.e[e] = Acc<T>::put(do_scale ? A(acc[e] * scale) : acc[e]);
-      reinterpret_cast<uint4*>(io + lo)[i] = o.u;
-    }
-    for (int64_t i = lo + nv * V + threadIdx.x; i < hi; i += kThreads) {
-      A acc = A(0);
-      for (int r = 0; r < size; ++r) {
-        const A x = Acc<T>::get(reinterpret_cast<const T*>(pp.data[r] + off)[i]);
-        acc = r == 0 ? x : (MAXOP ? (x > acc ? x : acc) : acc + x);
+      for (int e = 0; e < V; ++e) {
+        A acc = Acc<T>::get(v[0].e[e]);
+#pragma unroll
+        for (int r = 1; r < W; ++r) acc += Acc<T>::get(v[r].e[e]);
+        o.e[e] = Acc<T>::put(do_scale ? A(acc * scale) : acc);
       }
-      io[i] = Acc<T>::put(do_scale ? A(acc * scale) : acc);
+      reinterpret_cast<uint4*>(io + my_lo)[i] = o.u;
+      reinterpret_cast<uint4*>(mine + my_lo)[i] = o.u;
+    }
+    for (int64_t i = my_lo + nv * V + threadIdx.x; i < my_hi; i += kThreads) {
+      A acc = Acc<T>::get(src[0][i]);
+#pragma unroll
+      for (int r = 1; r < W; ++r) acc += Acc<T>::get(src[r][i]);
+      const T o = Acc<T>::put(do_scale ? A(acc * scale) : acc);
+      io[i] = o;
+      mine[i] = o;
+    }
+    // 3. gather the other ranks' reduced slices
+    if (flag_barrier(pp, b, rank, W, 2u * gen, status, timeout_ticks, &s_ok)) {
+#pragma unroll
+      for (int r = 0; r < W; ++r) {
+        if (r == rank) continue;
+        const int64_t s_lo = min(hi, lo + r * cs), s_hi = min(hi, s_lo + cs);
+        copy_range(io, reinterpret_cast<const T*>(pp.data[r] + off), s_lo, s_hi);
+      }
     }
   }
   __syncthreads();
@@ -177,50 +266,82 @@ __global__ __launch_bounds__(kThreads) void peer_kernel(T* __restrict__ io, int6
 
 }  // namespace
 
-struct PeerAllReduce::Impl {
+// One staging buffer (flags + two slots) per lane, IPC-mapped into every rank.
+struct PeerLane {
   PeerPtrs pp{};
   uint8_t* own = nullptr;
   uint32_t* gen_dev = nullptr;
-  int* status = nullptr;
+  int blocks = 0;
+  int64_t slot_bytes = 0;
+
+  void open(const std::shared_ptr<Store>& store, const std::string& tag, int rank, int size, int nblocks,
+            int64_t slot) {
+    blocks = nblocks;
+    slot_bytes = slot;
+    const int64_t flag_bytes = ((int64_t)nblocks * kPeerMaxRanks * 4 + 4095) / 4096 * 4096;
+    const size_t bytes = flag_bytes + 2 * (size_t)slot;
+    // uncached: the flags and staged data are read by the peers over xGMI while this GPU writes them
+    XDDP_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&own), bytes, hipDeviceMallocUncached));
+    XDDP_HIP_CHECK(hipMemset(own, 0, bytes));
+    XDDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&gen_dev), nblocks * sizeof(uint32_t)));
+    XDDP_HIP_CHECK(hipMemset(gen_dev, 0, nblocks * sizeof(uint32_t)));
+    XDDP_HIP_CHECK(hipDeviceSynchronize());
+    hipIpcMemHandle_t h;
+    XDDP_HIP_CHECK(hipIpcGetMemHandle(&h, own));
+    store->set("peer/h/" + tag + "/" + std::to_string(rank),
+               std::string(reinterpret_cast<const char*>(&h), sizeof(h)));
+    for (int r = 0; r < size; ++r) {
+      uint8_t* base = own;
+      if (r != rank) {
+        std::string s = store->get("peer/h/" + tag + "/" + std::to_string(r));
+        TORCH_CHECK(s.size() == sizeof(hipIpcMemHandle_t), "peer all-reduce: bad IPC handle from rank ", r);
+        hipIpcMemHandle_t ph;
+        std::memcpy(&ph, s.data(), sizeof(ph));
+        void* p = nullptr;
+        XDDP_HIP_CHECK(hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess));
+        base = static_cast<uint8_t*>(p);
+      }
+      pp.flags[r] = reinterpret_cast<uint32_t*>(base);
+      pp.data[r] = base + flag_bytes;
+    }
+  }
+
+  void close(int rank, int size) {
+    if (!own) return;
+    for (int r = 0; r < size; ++r)
+      if (r != rank && pp.flags[r]) (void)hipIpcCloseMemHandle(pp.flags[r]);
+    (void)hipFree(own);
+    (void)hipFree(gen_dev);
+    own = nullptr;
+  }
+};
+
+struct PeerAllReduce::Impl {
+  PeerLane one, two;
+  int* status_host = nullptr;  // host-mapped, coherent
+  int* status_dev = nullptr;
   uint64_t timeout_ticks = 0;
 };
 
-PeerAllReduce::PeerAllReduce(std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity)
-    : rank_(rank), size_(size), device_(device), cap_(capacity), impl_(new Impl) {
+PeerAllReduce::PeerAllReduce(std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity,
+                             int64_t two_shot_capacity, std::chrono::milliseconds timeout)
+    : rank_(rank), size_(size), device_(device), cap_(capacity), cap2_(two_shot_capacity), impl_(new Impl) {
   TORCH_CHECK(size >= 1 && size <= kPeerMaxRanks, "peer all-reduce: 1..", kPeerMaxRanks, " ranks");
   TORCH_CHECK(capacity > 0 && capacity % 4096 == 0, "peer all-reduce: capacity must be a positive multiple of 4 KiB");
+  TORCH_CHECK(two_shot_capacity >= 0 && two_shot_capacity % 4096 == 0,
+              "peer all-reduce: two-shot capacity must be a multiple of 4 KiB");
   c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
-  const size_t bytes = kFlagBytes + 2 * (size_t)capacity;
-  // uncached: the flags and staged data are read by the peers over xGMI while this GPU writes them
-  XDDP_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&impl_->own), bytes, hipDeviceMallocUncached));
-  XDDP_HIP_CHECK(hipMemset(impl_->own, 0, bytes));
-  XDDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&impl_->gen_dev), kPeerMaxBlocks * sizeof(uint32_t)));
-  XDDP_HIP_CHECK(hipMemset(impl_->gen_dev, 0, kPeerMaxBlocks * sizeof(uint32_t)));
-  XDDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&impl_->status), sizeof(int)));
-  XDDP_HIP_CHECK(hipMemset(impl_->status, 0, sizeof(int)));
-  XDDP_HIP_CHECK(hipDeviceSynchronize());
-  hipIpcMemHandle_t h;
-  XDDP_HIP_CHECK(hipIpcGetMemHandle(&h, impl_->own));
-  store->set("peer/h/" + std::to_string(rank), std::string(reinterpret_cast<const char*>(&h), sizeof(h)));
-  for (int r = 0; r < size; ++r) {
-    uint8_t* base = impl_->own;
-    if (r != rank) {
-      std::string s = store->get("peer/h/" + std::to_string(r));
-      TORCH_CHECK(s.size() == sizeof(hipIpcMemHandle_t), "peer all-reduce: bad IPC handle from rank ", r);
-      hipIpcMemHandle_t ph;
-      std::memcpy(&ph, s.data(), sizeof(ph));
-      void* p = nullptr;
-      XDDP_HIP_CHECK(hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess));
-      base = static_cast<uint8_t*>(p);
-    }
-    impl_->pp.flags[r] = reinterpret_cast<uint32_t*>(base);
-    impl_->pp.data[r] = base + kFlagBytes;
-  }
+  XDDP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&impl_->status_host), sizeof(int),
+                               hipHostMallocMapped | hipHostMallocCoherent));
+  *impl_->status_host = 0;
+  XDDP_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&impl_->status_dev), impl_->status_host, 0));
+  impl_->one.open(store, "1", rank, size, kPeerMaxBlocks, capacity);
+  if (two_shot_capacity > 0) impl_->two.open(store, "2", rank, size, kPeerTwoShotBlocks, two_shot_capacity);
   int khz = 0;
   XDDP_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
   const char* t = std::getenv("XDDP_PEER_TIMEOUT_MS");
-  const double ms = t ? std::atof(t) : 10000.0;
-  impl_->timeout_ticks = (uint64_t)(ms * (khz > 0 ? khz : 100000));
+  timeout_ms_ = t ? std::atof(t) : static_cast<double>(timeout.count());
+  impl_->timeout_ticks = (uint64_t)(timeout_ms_ * (khz > 0 ? khz : 100000));
   // every rank mapped every buffer before the first call raises a flag in it
   store->set("peer/ok/" + std::to_string(rank), "1");
   for (int r = 0; r < size; ++r) store->get("peer/ok/" + std::to_string(r));
@@ -232,25 +353,31 @@ PeerAllReduce::~PeerAllReduce() {
 }
 
 void PeerAllReduce::close() {
-  if (!impl_ || !impl_->own) return;
+  if (!impl_ || !impl_->one.own) return;
   c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
   (void)hipDeviceSynchronize();  // best effort: close() also runs on error paths
-  for (int r = 0; r < size_; ++r)
-    if (r != rank_ && impl_->pp.flags[r]) (void)hipIpcCloseMemHandle(impl_->pp.flags[r]);
-  (void)hipFree(impl_->own);
-  (void)hipFree(impl_->gen_dev);
-  (void)hipFree(impl_->status);
-  impl_->own = nullptr;
+  impl_->one.close(rank_, size_);
+  impl_->two.close(rank_, size_);
+  if (impl_->status_host) (void)hipHostFree(impl_->status_host);
+  impl_->status_host = nullptr;
+  impl_->status_dev = nullptr;
 }
 
 bool PeerAllReduce::supports(const at::Tensor& t, RedOp op, bool bcast) const {
-  if (!impl_->own || !t.is_cuda() || !t.is_contiguous() || t.device().index() != device_) return false;
+  if (!impl_->one.own || !t.is_cuda() || !t.is_contiguous() || t.device().index() != device_) return false;
   if (t.nbytes() == 0 || (int64_t)t.nbytes() > cap_ || reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) return false;
   if (bcast) return true;
   const auto st = t.scalar_type();
   const bool fl = st == at::kFloat || st == at::kBFloat16 || st == at::kHalf || st == at::kDouble;
   if (op == RedOp::SUM || op == RedOp::MAX) return fl || st == at::kInt || st == at::kLong;
   return op == RedOp::AVG && fl;
+}
+
+bool PeerAllReduce::supports_two_shot(const at::Tensor& t, RedOp op) const {
+  if (!impl_->two.own || !t.is_cuda() || !t.is_contiguous() || t.device().index() != device_) return false;
+  if (t.nbytes() == 0 || reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) return false;
+  const auto st = t.scalar_type();
+  return (op == RedOp::SUM || op == RedOp::AVG) && (st == at::kFloat || st == at::kBFloat16 || st == at::kHalf);
 }
 
 void PeerAllReduce::run(at::Tensor t, RedOp op, int root, bool bcast, hipStream_t s) {
@@ -268,21 +395,22 @@ void PeerAllReduce::allgather(at::Tensor out, at::Tensor in, hipStream_t s) {
 
 void PeerAllReduce::launch(at::Tensor t, at::Tensor out, RedOp op, int root, int mode, hipStream_t s) {
   c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
+  auto& L = impl_->one;
   // data movement modes move bytes: as 4-B words when the size allows (whole 16-B vectors per thread)
   const bool raw = mode != 0;
   const bool words = raw && t.nbytes() % 4 == 0 && (mode != 2 || out.nbytes() % 4 == 0);
   const int64_t esz = raw ? (words ? 4 : 1) : t.element_size();
   const int64_t n = (int64_t)t.nbytes() / esz, vec = 16 / esz;
-  // >= 16 KiB per workgroup, at most kPeerMaxBlocks workgroups; chunks are whole 16-B vectors
-  int64_t blocks = std::min<int64_t>(kPeerMaxBlocks, std::max<int64_t>(1, (int64_t)t.nbytes() / 16384));
-  int64_t chunk = (n + blocks - 1) / blocks;
+  // >= 16 KiB per workgroup that has data; the grid is always the lane's full width
+  const int64_t busy = std::min<int64_t>(L.blocks, std::max<int64_t>(1, (int64_t)t.nbytes() / 16384));
+  int64_t chunk = (n + busy - 1) / busy;
   chunk = (chunk + vec - 1) / vec * vec;
-  blocks = (n + chunk - 1) / chunk;
+  TORCH_CHECK(chunk * L.blocks >= n, "peer all-reduce: chunking");
   const float scale = 1.f / (float)size_;
   const bool do_scale = op == RedOp::AVG;
   auto go = [&](auto kern, auto* io, auto* o) {
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kThreads), 0, s, io, n, impl_->pp, rank_, size_, root,
-                       impl_->gen_dev, impl_->status, scale, do_scale, impl_->timeout_ticks, (int64_t)cap_, chunk, o);
+    hipLaunchKernelGGL(kern, dim3((unsigned)L.blocks), dim3(kThreads), 0, s, io, n, L.pp, rank_, size_, root,
+                       L.gen_dev, impl_->status_dev, scale, do_scale, impl_->timeout_ticks, L.slot_bytes, chunk, o);
   };
   void* p = t.data_ptr();
   void* q = out.data_ptr();
@@ -313,11 +441,71 @@ void PeerAllReduce::launch(at::Tensor t, at::Tensor out, RedOp op, int root, int
   XDDP_HIP_CHECK(hipGetLastError());
 }
 
-int PeerAllReduce::status() {
+namespace {
+
+template <typename T, int W>
+void launch_two_shot_w(T* io, int64_t n, PeerLane& L, int rank, int* status, float scale, bool do_scale,
+                       uint64_t ticks, hipStream_t s) {
+  constexpr int64_t V = 16 / sizeof(T);
+  int64_t chunk = (n + L.blocks - 1) / L.blocks;
+  chunk = (chunk + W * V - 1) / (W * V) * (W * V);  // every slice a whole number of vectors
+  hipLaunchKernelGGL((two_shot_kernel<T, W>), dim3((unsigned)L.blocks), dim3(kThreads), 0, s, io, n, L.pp, rank,
+                     L.gen_dev, status, scale, do_scale, ticks, L.slot_bytes, chunk);
+}
+
+template <typename T>
+void launch_two_shot(T* io, int64_t n, PeerLane& L, int rank, int size, int* status, float scale, bool do_scale,
+                     uint64_t ticks, hipStream_t s) {
+  switch (size) {
+    case 2: launch_two_shot_w<T, 2>(io, n, L, rank, status, scale, do_scale, ticks, s); break;
+    case 3: launch_two_shot_w<T, 3>(io, n, L, rank, status, scale, do_scale, ticks, s); break;
+    case 4: launch_two_shot_w<T, 4>(io, n, L, rank, status, scale, do_scale, ticks, s); break;
+    case 5: launch_two_shot_w<T, 5>(io, n, L, rank, status, scale, do_scale, ticks, s); break;
+    case 6: launch_two_shot_w<T, 6>(io, n, L, rank, status, scale, do_scale, ticks, s); break;
+    case 7: launch_two_shot_w<T, 7>(io, n, L, rank, status, scale, do_scale, ticks, s); break;
+    case 8: launch_two_shot_w<T, 8>(io, n, L, rank, status, scale, do_scale, ticks, s); break;
+    default: TORCH_CHECK(false, "peer two-shot all-reduce: 2..8 ranks");
+  }
+}
+
+}  // namespace
+
+void PeerAllReduce::allreduce_two_shot(at::Tensor t, RedOp op, hipStream_t s) {
+  TORCH_CHECK(supports_two_shot(t, op), "peer two-shot all-reduce: unsupported tensor / op");
+  if (size_ == 1) {
+    return;  // one rank: SUM and AVG are identities
+  }
   c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
-  int v = 0;
-  XDDP_HIP_CHECK(hipMemcpy(&v, impl_->status, sizeof(int), hipMemcpyDeviceToHost));
-  return v;
+  auto& L = impl_->two;
+  const int64_t esz = t.element_size();
+  const int64_t step = cap2_ / esz;  // capacity is a multiple of 4 KiB: whole vectors
+  const int64_t n = t.numel();
+  const float scale = 1.f / (float)size_;
+  const bool do_scale = op == RedOp::AVG;
+  for (int64_t off = 0; off < n; off += step) {  // one launch per staging-sized chunk
+    const int64_t len = std::min(step, n - off);
+    switch (t.scalar_type()) {
+      case at::kFloat:
+        launch_two_shot(t.data_ptr<float>() + off, len, L, rank_, size_, impl_->status_dev, scale, do_scale,
+                        impl_->timeout_ticks, s);
+        break;
+      case at::kBFloat16:
+        launch_two_shot(reinterpret_cast<uint16_t*>(t.data_ptr()) + off, len, L, rank_, size_, impl_->status_dev,
+                        scale, do_scale, impl_->timeout_ticks, s);
+        break;
+      case at::kHalf:
+        launch_two_shot(reinterpret_cast<__half*>(t.data_ptr()) + off, len, L, rank_, size_, impl_->status_dev,
+                        scale, do_scale, impl_->timeout_ticks, s);
+        break;
+      default: TORCH_CHECK(false, "peer two-shot all-reduce: dtype");
+    }
+    XDDP_HIP_CHECK(hipGetLastError());
+  }
+}
+
+int PeerAllReduce::status() const {
+  if (!impl_->status_host) return 0;
+  return __atomic_load_n(impl_->status_host, __ATOMIC_ACQUIRE);
 }
 
 }  // namespace xddp

@@ -1,25 +1,34 @@
-// PeerComm: an RCCL-free single-node communicator for device tensors, built on the one-shot
-// peer-memory kernels of peer_allreduce.hip (IPC-mapped staging buffers, xGMI loads). Backend
-// "peer" of init_process_group.
+// PeerComm: an RCCL-free single-node communicator for device tensors, built on the peer-memory
+// kernels of peer_allreduce.hip (IPC-mapped staging buffers, xGMI loads). Backend "peer" of
+// init_process_group.
 //
 // Every collective runs on one dedicated HIP stream that first waits for the caller's stream
 // (event), so it is ordered after the producer of its input; Work.wait() makes the caller's stream
-// wait for the collective's completion event (no host blocking). Messages larger than the staging
-// capacity (XDDP_PEER_CAPACITY_MB, default 16 MiB) are walked in capacity-sized chunks, each one a
-// kernel with its own flag barrier. All-reduce (SUM / AVG / MAX; PREMUL_SUM as SUM + scale),
-// broadcast, all-gather, reduce-scatter (all-reduce + own slice) and barrier are supported;
-// all-to-all and point-to-point are not (use the RCCL backend).
+// wait for the collective's completion event (no host blocking). All-reduce takes the two-shot
+// kernel (reduce-scatter + all-gather over all links) from XDDP_PEER_TWO_SHOT_MIN_BYTES (default
+// 256 KiB) up and the one-shot kernel below; messages larger than a lane's staging capacity are
+// walked in capacity-sized chunks. Broadcast, all-gather, reduce-scatter (all-reduce + own slice)
+// and barrier are supported; all-to-all and point-to-point are not (use the RCCL backend).
 //
-// Why it exists: on a 1-GPU box two ranks can share the device through it (RCCL refuses duplicate
-// devices), so the W > 1 DDP path — bucket launches, stream ordering, Work semantics — runs
-// against device-side collectives, not the host-staged CPU backend; on a node it is the same
-// peer-memory protocol the RCCL communicator uses for small messages (XDDP_PEER_ALLREDUCE).
+// Failure handling: a watchdog thread polls the in-flight completion events (flight records are
+// marked completed only when their event has fired) and the peer kernels' host-mapped status word.
+// A peer that never arrived (XDDP_PEER_TIMEOUT_MS, default = the process-group timeout) puts the
+// communicator in an error state: the flight record is dumped, the error is posted to the store so
+// the other ranks fail too, and every later Work query / launch raises.
+//
+// Why it exists: on a 1-GPU box several ranks can share the device through it (RCCL refuses
+// duplicate devices), so the W > 1 DDP path — bucket launches, stream ordering, Work semantics —
+// runs against device-side collectives, not the host-staged CPU backend; on a node it is the same
+// peer-memory protocol the RCCL communicator can route messages to (XDDP_PEER_ALLREDUCE).
 #include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <iostream>
+#include <list>
 #include <memory>
+#include <thread>
 
 #include "comm/comm.h"
 #include "comm/peer.h"
@@ -28,40 +37,108 @@ namespace xddp {
 
 namespace {
 
+// Shared error state of one communicator: 0 ok, 1 peer timeout, 3 a peer rank reported an error.
+struct PeerState {
+  std::atomic<int> err{0};
+  PeerAllReduce* peer = nullptr;
+  void check() {
+    int e = err.load();
+    if (e == 0 && peer && peer->status() != 0) {
+      e = 1;
+      err.store(1);
+    }
+    TORCH_CHECK(e == 0, "xddp peer: communicator is in error state (",
+                e == 1 ? "a peer rank did not arrive within XDDP_PEER_TIMEOUT_MS; the collective's output is invalid"
+                       : "a peer rank reported a communicator error",
+                "); re-create the process group");
+  }
+};
+
 class PeerWork : public Work {
  public:
-  PeerWork(int device, hipEvent_t ev) : device_(device), ev_(ev) {}
+  PeerWork(int device, hipEvent_t ev, hipEvent_t t0, hipEvent_t t1, std::shared_ptr<PeerState> st)
+      : device_(device), ev_(ev), t0_(t0), t1_(t1), st_(std::move(st)) {}
   ~PeerWork() override {
-    if (ev_) (void)hipEventDestroy(ev_);
+    for (auto e : {ev_, t0_, t1_})
+      if (e) (void)hipEventDestroy(e);
   }
-  bool is_completed() override { return hipEventQuery(ev_) == hipSuccess; }
+  bool is_completed() override {
+    st_->check();
+    const bool done = hipEventQuery(ev_) == hipSuccess;
+    if (done) st_->check();
+    return done;
+  }
   void wait() override {
+    st_->check();
     c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
     XDDP_HIP_CHECK(hipStreamWaitEvent(c10::hip::getCurrentHIPStream(device_).stream(), ev_, 0));
   }
-  void synchronize() override { XDDP_HIP_CHECK(hipEventSynchronize(ev_)); }
+  void synchronize() override {
+    st_->check();
+    XDDP_HIP_CHECK(hipEventSynchronize(ev_));
+    st_->check();
+  }
+  Timing timing_state() override {
+    if (!t0_) return Timing::kNone;
+    return hipEventQuery(t1_) == hipSuccess ? Timing::kReady : Timing::kPending;
+  }
+  double comm_ms() override {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, t0_, t1_);
+    return ms;
+  }
+  double comm_ms_before(const TimeRef& ref) override {
+    if (!ref.ev) return 0.0;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, t0_, ref.ev) != hipSuccess) return 0.0;
+    return std::max(0.0, std::min<double>(ms, comm_ms()));
+  }
+  hipEvent_t event() const { return ev_; }
 
  private:
   int device_;
-  hipEvent_t ev_;
+  hipEvent_t ev_, t0_, t1_;
+  std::shared_ptr<PeerState> st_;
 };
 
 class PeerComm : public Comm {
  public:
-  PeerComm(std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity)
+  PeerComm(std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity, int64_t two_shot_capacity,
+           std::chrono::milliseconds timeout)
       : Comm(rank, size),
+        store_(store),
         device_(device),
         stream_(c10::hip::getStreamFromPool(true, static_cast<c10::DeviceIndex>(device))),
-        peer_(std::make_unique<PeerAllReduce>(std::move(store), rank, size, device, capacity)) {}
+        peer_(std::make_unique<PeerAllReduce>(std::move(store), rank, size, device, capacity, two_shot_capacity,
+                                              timeout)),
+        st_(std::make_shared<PeerState>()) {
+    st_->peer = peer_.get();
+    const char* m = std::getenv("XDDP_PEER_TWO_SHOT_MIN_BYTES");
+    two_shot_min_ = m ? std::atoll(m) : (256 << 10);
+    watchdog_ = std::thread([this] { watchdog_loop(); });
+  }
+  ~PeerComm() override { stop_watchdog(); }
 
   std::string backend() const override { return "peer"; }
+  std::map<std::string, std::string> info() const override {
+    return {{"backend", "peer"},
+            {"one_shot_capacity_bytes", std::to_string(peer_->capacity())},
+            {"two_shot_capacity_bytes", std::to_string(peer_->two_shot_capacity())},
+            {"two_shot_min_bytes", std::to_string(two_shot_min_)},
+            {"timeout_ms", std::to_string(peer_->timeout_ms())}};
+  }
 
   std::shared_ptr<Work> allreduce(at::Tensor t, RedOp op, double premul) override {
     TORCH_CHECK(op == RedOp::SUM || op == RedOp::AVG || op == RedOp::MAX || op == RedOp::PREMUL_SUM,
                 "peer backend: all-reduce supports SUM, AVG, MAX and PREMUL_SUM");
     const RedOp kop = op == RedOp::PREMUL_SUM ? RedOp::SUM : op;
-    return launch("allreduce", t, {t}, [&](hipStream_t s) {
-      for_chunks(t, [&](at::Tensor c) { peer_->allreduce(c, kop, s); });
+    const bool two = (int64_t)t.nbytes() >= two_shot_min_ && peer_->supports_two_shot(t, kop);
+    return launch(two ? "allreduce_two_shot" : "allreduce", t, {t}, [&](hipStream_t s) {
+      if (two) {
+        peer_->allreduce_two_shot(t, kop, s);
+      } else {
+        for_chunks(t, [&](at::Tensor c) { peer_->allreduce(c, kop, s); });
+      }
       if (op == RedOp::PREMUL_SUM) t.mul_(premul);  // (on the comm stream: the guard below)
     });
   }
@@ -122,7 +199,10 @@ class PeerComm : public Comm {
     return w;
   }
 
-  void shutdown() override { peer_->close(); }
+  void shutdown() override {
+    stop_watchdog();
+    peer_->close();
+  }
 
  private:
   int64_t chunk_elems(const at::Tensor& t) const {
@@ -140,42 +220,133 @@ class PeerComm : public Comm {
     for (int64_t off = 0; off < n; off += step) f(flat.narrow(0, off, std::min(step, n - off)));
   }
 
+  static hipEvent_t make_event(bool timed) {
+    hipEvent_t e;
+    XDDP_HIP_CHECK(hipEventCreateWithFlags(&e, timed ? hipEventDefault : hipEventDisableTiming));
+    return e;
+  }
+
   template <typename F>
   std::shared_ptr<Work> launch(const char* name, const at::Tensor& meta, std::vector<at::Tensor> keep, F&& body) {
+    st_->check();
     c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
     auto cur = c10::hip::getCurrentHIPStream(device_);
-    hipEvent_t pre;
-    XDDP_HIP_CHECK(hipEventCreateWithFlags(&pre, hipEventDisableTiming));
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    XDDP_HIP_CHECK(hipStreamIsCapturing(cur.stream(), &cap));
+    const bool capturing = cap == hipStreamCaptureStatusActive;
+    hipEvent_t pre = make_event(false);
     XDDP_HIP_CHECK(hipEventRecord(pre, cur.stream()));
     XDDP_HIP_CHECK(hipStreamWaitEvent(stream_.stream(), pre, 0));
     XDDP_HIP_CHECK(hipEventDestroy(pre));
     const int64_t seq = flight_.record(name, meta.numel(), meta.scalar_type());
+    const bool timed = timing_.load() && !capturing;
+    hipEvent_t t0 = timed ? make_event(true) : nullptr, t1 = timed ? make_event(true) : nullptr;
+    if (t0) XDDP_HIP_CHECK(hipEventRecord(t0, stream_.stream()));
     {
       c10::hip::HIPStreamGuard sg(stream_);  // torch ops in the body (chunk copies, scaling) too
       body(stream_.stream());
     }
-    for (auto& t : keep)
-      if (t.defined() && t.is_cuda()) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_);
-    hipEvent_t done;
-    XDDP_HIP_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    if (t1) XDDP_HIP_CHECK(hipEventRecord(t1, stream_.stream()));
+    if (!capturing) {
+      for (auto& t : keep)
+        if (t.defined() && t.is_cuda()) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_);
+    }
+    hipEvent_t done = make_event(false);
     XDDP_HIP_CHECK(hipEventRecord(done, stream_.stream()));
-    flight_.finish(seq, "completed");  // (enqueued; completion is the event)
-    auto w = std::make_shared<PeerWork>(device_, done);
+    auto w = std::make_shared<PeerWork>(device_, done, t0, t1, st_);
     w->outputs = std::move(keep);
     w->seq = seq;
+    w->collective = size_ > 1;
+    if (timed && w->collective) log_timed(w);
+    if (capturing) {
+      flight_.finish(seq, "captured");  // a graph node, not a live collective
+    } else {
+      std::lock_guard<std::mutex> g(wd_mu_);
+      inflight_.push_back(w);
+    }
     return w;
   }
 
+  void watchdog_loop() {
+    int64_t last_store_poll = 0;
+    while (!wd_stop_) {
+      std::vector<std::shared_ptr<PeerWork>> done;
+      {
+        std::unique_lock<std::mutex> g(wd_mu_);
+        wd_cv_.wait_for(g, std::chrono::milliseconds(50), [&] { return wd_stop_.load(); });
+        if (wd_stop_) break;
+        for (auto it = inflight_.begin(); it != inflight_.end();) {
+          if (hipEventQuery((*it)->event()) == hipSuccess) {
+            done.push_back(*it);
+            it = inflight_.erase(it);
+          } else {
+            ++it;
+          }
+        }
+      }
+      const bool timed_out = peer_->status() != 0;
+      for (auto& w : done) flight_.finish(w->seq, timed_out ? "failed" : "completed");
+      if (timed_out && st_->err.load() == 0) {
+        st_->err.store(1);
+        const std::string reason = "a peer did not arrive within " + std::to_string((int64_t)peer_->timeout_ms()) +
+                                   " ms (XDDP_PEER_TIMEOUT_MS)";
+        std::cerr << "[xddp rank " << rank_ << "] peer watchdog: " << reason << "; communicator is in error state\n";
+        {
+          std::lock_guard<std::mutex> g(wd_mu_);
+          for (auto& w : inflight_) flight_.finish(w->seq, "failed");
+        }
+        dump_flight(reason);
+        try {
+          store_->set("peer/error", "rank " + std::to_string(rank_) + ": " + reason);
+        } catch (...) {
+        }
+      }
+      // a collective in flight for over a second: has a peer already failed?
+      const int64_t now = now_ns();
+      bool busy;
+      {
+        std::lock_guard<std::mutex> g(wd_mu_);
+        busy = !inflight_.empty();
+      }
+      if (st_->err.load() == 0 && busy && now - last_store_poll > 1000000000LL) {
+        last_store_poll = now;
+        try {
+          if (store_->check({"peer/error"})) {
+            std::cerr << "[xddp rank " << rank_ << "] peer watchdog: " << store_->get("peer/error") << "\n";
+            st_->err.store(3);
+            dump_flight("peer error: " + store_->get("peer/error"));
+          }
+        } catch (...) {
+        }
+      }
+    }
+  }
+
+  void stop_watchdog() {
+    wd_stop_ = true;
+    wd_cv_.notify_all();
+    if (watchdog_.joinable()) watchdog_.join();
+  }
+
+  std::shared_ptr<Store> store_;
   int device_;
   c10::hip::HIPStream stream_;
   std::unique_ptr<PeerAllReduce> peer_;
+  std::shared_ptr<PeerState> st_;
+  int64_t two_shot_min_ = 0;
   at::Tensor barrier_buf_;
+  std::thread watchdog_;
+  std::atomic<bool> wd_stop_{false};
+  std::mutex wd_mu_;
+  std::condition_variable wd_cv_;
+  std::list<std::shared_ptr<PeerWork>> inflight_;
 };
 
 }  // namespace
 
-std::shared_ptr<Comm> make_peer_comm(std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity) {
-  return std::make_shared<PeerComm>(std::move(store), rank, size, device, capacity);
+std::shared_ptr<Comm> make_peer_comm(std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity,
+                                     int64_t two_shot_capacity, std::chrono::milliseconds timeout) {
+  return std::make_shared<PeerComm>(std::move(store), rank, size, device, capacity, two_shot_capacity, timeout);
 }
 
 }  // namespace xddp

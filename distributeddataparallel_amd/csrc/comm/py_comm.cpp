@@ -78,6 +78,7 @@ class PyComm : public Comm {
     py::object w = std::apply([&](auto&&... a) { return impl_->attr(fn)(a...); }, args);
     auto pw = std::make_shared<PyWork>(std::move(w));
     pw->seq = seq;
+    pw->collective = size_ > 1;
     flight_.finish(seq, "scheduled");
     return pw;
   }

@@ -75,6 +75,7 @@ ncclRedOp_t to_nccl(RedOp op, at::ScalarType t) {
 
 class EventPool {
  public:
+  explicit EventPool(bool timing = false) : timing_(timing) {}
   hipEvent_t get() {
     std::lock_guard<std::mutex> g(mu_);
     if (!free_.empty()) {
@@ -83,7 +84,7 @@ class EventPool {
       return e;
     }
     hipEvent_t e;
-    XDDP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    XDDP_HIP_CHECK(hipEventCreateWithFlags(&e, timing_ ? hipEventDefault : hipEventDisableTiming));
     return e;
   }
   void put(hipEvent_t e) {
@@ -92,8 +93,20 @@ class EventPool {
   }
 
  private:
+  bool timing_;
   std::mutex mu_;
   std::vector<hipEvent_t> free_;
+};
+
+// Comm-stream interval of one (or one group of) RCCL launches, shared by the works it covers.
+struct Interval {
+  Interval(std::shared_ptr<EventPool> p) : pool(std::move(p)), t0(pool->get()), t1(pool->get()) {}
+  ~Interval() {
+    pool->put(t0);
+    pool->put(t1);
+  }
+  std::shared_ptr<EventPool> pool;
+  hipEvent_t t0, t1;
 };
 
 }  // namespace
@@ -102,8 +115,9 @@ class RcclComm;
 
 class RcclWork : public Work {
  public:
-  RcclWork(std::shared_ptr<EventPool> pool, int device, std::shared_ptr<std::atomic<int>> err)
-      : pool_(std::move(pool)), device_(device), err_(std::move(err)) {
+  RcclWork(std::shared_ptr<EventPool> pool, int device, std::shared_ptr<std::atomic<int>> err,
+           std::shared_ptr<PeerAllReduce> peer)
+      : pool_(std::move(pool)), device_(device), err_(std::move(err)), peer_(std::move(peer)) {
     ev = pool_->get();
     t_start = now_ns();
   }
@@ -111,7 +125,9 @@ class RcclWork : public Work {
   bool is_completed() override {
     check_error();
     if (captured) return true;
-    return hipEventQuery(ev) == hipSuccess;
+    const bool done = hipEventQuery(ev) == hipSuccess;
+    if (done) check_error();
+    return done;
   }
   void wait() override {
     check_error();
@@ -126,19 +142,46 @@ class RcclWork : public Work {
   }
   void check_error() {
     int e = err_->load();
+    if (e == 0 && peer_ && peer_->status() != 0) {  // host-mapped word: no device sync
+      int z = 0;
+      err_->compare_exchange_strong(z, 4);
+      e = err_->load();
+    }
     TORCH_CHECK(e == 0, "xddp rccl: communicator is in error state (",
-                e == 1 ? "collective timed out; watchdog aborted the communicator"
-                       : (e == 3 ? "a peer rank reported a communicator error" : "asynchronous RCCL error"),
+                e == 1   ? "collective timed out; watchdog aborted the communicator"
+                : e == 3 ? "a peer rank reported a communicator error"
+                : e == 4 ? "a peer-memory collective timed out (a rank did not arrive within XDDP_PEER_TIMEOUT_MS); "
+                           "its output is invalid"
+                         : "asynchronous RCCL error",
                 ")");
+  }
+  Timing timing_state() override {
+    if (!iv) return Timing::kNone;
+    return hipEventQuery(iv->t1) == hipSuccess ? Timing::kReady : Timing::kPending;
+  }
+  double comm_ms() override {
+    if (!iv || !owns_interval) return 0.0;
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, iv->t0, iv->t1);
+    return ms;
+  }
+  double comm_ms_before(const TimeRef& ref) override {
+    if (!iv || !owns_interval || !ref.ev) return 0.0;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, iv->t0, ref.ev) != hipSuccess) return 0.0;
+    return std::max(0.0, std::min<double>(ms, comm_ms()));
   }
   hipEvent_t ev;
   int64_t t_start;
   bool captured = false;
+  std::shared_ptr<Interval> iv;  // timed works only
+  bool owns_interval = true;     // false for the 2nd.. works of a grouped launch
 
  private:
   std::shared_ptr<EventPool> pool_;
   int device_;
   std::shared_ptr<std::atomic<int>> err_;
+  std::shared_ptr<PeerAllReduce> peer_;
 };
 
 class RcclComm : public Comm {
@@ -151,7 +194,9 @@ class RcclComm : public Comm {
         timeout_(timeout),
         stream_(c10::hip::getStreamFromPool(high_priority, static_cast<c10::DeviceIndex>(device))),
         pool_(std::make_shared<EventPool>()),
+        tpool_(std::make_shared<EventPool>(true)),
         err_(std::make_shared<std::atomic<int>>(0)) {
+    high_priority_ = high_priority;
     c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
     ncclUniqueId id;
     if (rank == 0) {
@@ -186,8 +231,13 @@ class RcclComm : public Comm {
   std::shared_ptr<Work> allreduce(at::Tensor t, RedOp op, double premul) override {
     check_tensor(t);
     if (size_ == 1 && !force_launch_ && op != RedOp::PREMUL_SUM) return local_noop("allreduce", t);  // identity
-    if (use_peer(t, op, false))
-      return launch("allreduce_peer", t, {t}, [&](hipStream_t s) { peer_->allreduce(t, op, s); });
+    switch (peer_route(t, op, false)) {
+      case PeerRoute::kOneShot:
+        return launch_peer("allreduce_peer", t, {t}, [&](hipStream_t s) { peer_->allreduce(t, op, s); });
+      case PeerRoute::kTwoShot:
+        return launch_peer("allreduce_two_shot", t, {t}, [&](hipStream_t s) { peer_->allreduce_two_shot(t, op, s); });
+      default: break;
+    }
     return launch("allreduce", t, {t}, [&](hipStream_t s) {
       if (op == RedOp::PREMUL_SUM) {
         TORCH_CHECK(at::isFloatingType(t.scalar_type()), "PREMUL_SUM needs a floating-point tensor");
@@ -212,8 +262,8 @@ class RcclComm : public Comm {
   std::shared_ptr<Work> broadcast(at::Tensor t, int root) override {
     check_tensor(t);
     if (size_ == 1 && !force_launch_) return local_noop("broadcast", t);
-    if (use_peer(t, RedOp::SUM, true))
-      return launch("broadcast_peer", t, {t}, [&](hipStream_t s) { peer_->broadcast(t, root, s); });
+    if (peer_route(t, RedOp::SUM, true) == PeerRoute::kOneShot)
+      return launch_peer("broadcast_peer", t, {t}, [&](hipStream_t s) { peer_->broadcast(t, root, s); });
     return launch("broadcast", t, {t}, [&](hipStream_t s) {
       XDDP_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, s));
     });
@@ -278,11 +328,12 @@ class RcclComm : public Comm {
     in_group_++;
   }
   void group_end() override {
-    XDDP_NCCL_CHECK(ncclGroupEnd());
-    if (--in_group_ == 0) {
-      for (auto& w : group_works_) finish_launch(w);
-      group_works_.clear();
+    if (in_group_ == 1) {
+      end_group_launch(1);
+    } else {
+      XDDP_NCCL_CHECK(ncclGroupEnd());
     }
+    --in_group_;
   }
 
   void abort() override {
@@ -305,20 +356,36 @@ class RcclComm : public Comm {
     if (peer_) peer_->close();
   }
 
-  // XDDP_PEER_ALLREDUCE=1 (node-local groups of 2..8 ranks): messages up to
-  // XDDP_PEER_ALLREDUCE_BYTES (default 256 KiB) take the one-shot peer-memory kernel
-  // (comm/peer_allreduce.hip) instead of an RCCL ring — the latency-bound per-forward buffer
-  // broadcast, find-unused bitmap and small first bucket. Every rank must agree: each posts
-  // whether its IPC mapping worked and the path is used only if all did.
+  // Peer-memory routing (comm/peer_allreduce.hip), node-local groups of 2..8 ranks:
+  //   XDDP_PEER_ALLREDUCE=1: messages up to XDDP_PEER_ALLREDUCE_BYTES (default 256 KiB) take the
+  //     one-shot kernel instead of an RCCL ring — the latency-bound per-forward buffer broadcast,
+  //     find-unused bitmap and small first bucket;
+  //   XDDP_PEER_ALLREDUCE=2: additionally, fp32/bf16/fp16 SUM/AVG all-reduces from
+  //     XDDP_PEER_TWO_SHOT_MIN_BYTES (default 1 MiB) up to XDDP_PEER_TWO_SHOT_MAX_BYTES (default
+  //     unlimited) take the two-shot kernel, which reads from all seven xGMI links at once
+  //     (staging XDDP_PEER_TWO_SHOT_MB per slot, default 64; larger messages are chunked).
+  // The route depends only on facts identical on every rank (size, dtype, op) — never on group
+  // state — so all ranks issue the same sequence. Every rank must agree the path works: each
+  // posts whether its IPC mapping succeeded and the path is used only if all did.
   void init_peer(const std::shared_ptr<Store>& store) {
     const char* e = std::getenv("XDDP_PEER_ALLREDUCE");
-    if (!e || std::string(e) != "1" || size_ < 2 || size_ > kPeerMaxRanks) return;
-    const char* b = std::getenv("XDDP_PEER_ALLREDUCE_BYTES");
-    peer_bytes_ = b ? std::atoll(b) : (256 << 10);
+    const int mode = e ? std::atoi(e) : 0;
+    if (mode <= 0 || size_ < 2 || size_ > kPeerMaxRanks) return;
+    auto env_i64 = [](const char* k, int64_t d) {
+      const char* v = std::getenv(k);
+      return v ? static_cast<int64_t>(std::atof(v)) : d;
+    };
+    peer_bytes_ = env_i64("XDDP_PEER_ALLREDUCE_BYTES", 256 << 10);
     const int64_t cap = std::max<int64_t>(4096, (peer_bytes_ + 4095) / 4096 * 4096);
+    int64_t cap2 = 0;
+    if (mode >= 2) {
+      two_shot_min_ = env_i64("XDDP_PEER_TWO_SHOT_MIN_BYTES", 1 << 20);
+      two_shot_max_ = env_i64("XDDP_PEER_TWO_SHOT_MAX_BYTES", INT64_MAX);
+      cap2 = std::max<int64_t>(4096, static_cast<int64_t>(env_i64("XDDP_PEER_TWO_SHOT_MB", 64) * (1 << 20)) / 4096 * 4096);
+    }
     std::string ok = "1";
     try {
-      peer_ = std::make_unique<PeerAllReduce>(store, rank_, size_, device_, cap);
+      peer_ = std::make_shared<PeerAllReduce>(store, rank_, size_, device_, cap, cap2, timeout_);
     } catch (const std::exception& ex) {
       ok = "0";
       peer_.reset();
@@ -328,10 +395,31 @@ class RcclComm : public Comm {
     bool all = true;
     for (int r = 0; r < size_; ++r) all = all && store->get("peer/use/" + std::to_string(r)) == "1";
     if (!all) peer_.reset();
+    peer_mode_ = peer_ ? mode : 0;
   }
 
-  bool use_peer(const at::Tensor& t, RedOp op, bool bcast) const {
-    return peer_ && in_group_ == 0 && (int64_t)t.nbytes() <= peer_bytes_ && peer_->supports(t, op, bcast);
+  enum class PeerRoute { kRccl, kOneShot, kTwoShot };
+  PeerRoute peer_route(const at::Tensor& t, RedOp op, bool bcast) const {
+    if (!peer_) return PeerRoute::kRccl;
+    const int64_t nb = static_cast<int64_t>(t.nbytes());
+    if (nb <= peer_bytes_ && peer_->supports(t, op, bcast)) return PeerRoute::kOneShot;
+    if (!bcast && peer_mode_ >= 2 && nb >= two_shot_min_ && nb <= two_shot_max_ && peer_->supports_two_shot(t, op))
+      return PeerRoute::kTwoShot;
+    return PeerRoute::kRccl;
+  }
+
+  std::map<std::string, std::string> info() const override {
+    int dev = -1;
+    if (comm_) ncclCommCuDevice(comm_, &dev);
+    return {{"backend", "rccl"},
+            {"rccl_version", rccl_version()},
+            {"nranks", std::to_string(size_)},
+            {"rank", std::to_string(rank_)},
+            {"device", std::to_string(dev)},
+            {"high_priority_stream", high_priority_ ? "1" : "0"},
+            {"peer_mode", std::to_string(peer_mode_)},
+            {"peer_one_shot_max_bytes", std::to_string(peer_ ? peer_bytes_ : 0)},
+            {"peer_two_shot_min_bytes", std::to_string(peer_mode_ >= 2 ? two_shot_min_ : 0)}};
   }
 
   hipStream_t stream() const { return stream_.stream(); }
@@ -363,9 +451,16 @@ class RcclComm : public Comm {
     XDDP_HIP_CHECK(hipEventRecord(pre, cur.stream()));
     XDDP_HIP_CHECK(hipStreamWaitEvent(stream_.stream(), pre, 0));
     pool_->put(pre);
-    auto w = std::make_shared<RcclWork>(pool_, device_, err_);
+    auto w = std::make_shared<RcclWork>(pool_, device_, err_, peer_);
     w->seq = flight_.record(name, meta.numel(), meta.scalar_type());
+    const bool timed = timing_.load() && !capturing_;
+    // Inside a group the RCCL kernels are enqueued at ncclGroupEnd: the group is timed there.
+    if (timed && in_group_ == 0) {
+      w->iv = std::make_shared<Interval>(tpool_);
+      XDDP_HIP_CHECK(hipEventRecord(w->iv->t0, stream_.stream()));
+    }
     body(stream_.stream());
+    if (w->iv) XDDP_HIP_CHECK(hipEventRecord(w->iv->t1, stream_.stream()));
     if (!capturing_) {
       for (auto& t : keep) {
         if (t.defined() && t.is_cuda())
@@ -374,19 +469,67 @@ class RcclComm : public Comm {
     }
     w->outputs = std::move(keep);
     w->captured = capturing_;
-    if (in_group_ > 0) group_works_.push_back(w);
-    else finish_launch(w);
+    if (timed) log_timed(w);
+    if (in_group_ > 0) {
+      if (timed) timed_group_ = true;
+      group_works_.push_back(w);
+    } else {
+      finish_launch(w);
+    }
     return w;
+  }
+
+  // A peer-memory collective issued inside an RCCL group: the group's pending RCCL launches go
+  // out first (ncclGroupEnd down to depth 0, then reopened at the same depth), so the stream
+  // order of peer and RCCL kernels is the issue order — identical on every rank, whatever the
+  // local grouping (a joined rank shadows all buckets in one group while training ranks launch
+  // them one by one).
+  template <typename F>
+  std::shared_ptr<Work> launch_peer(const char* name, const at::Tensor& meta, std::vector<at::Tensor> keep,
+                                    F&& body) {
+    const int depth = in_group_;
+    if (depth > 0) {
+      end_group_launch(depth);
+      in_group_ = 0;
+    }
+    auto w = launch(name, meta, std::move(keep), std::forward<F>(body));
+    for (int k = 0; k < depth; ++k) XDDP_NCCL_CHECK(ncclGroupStart());
+    in_group_ = depth;
+    return w;
+  }
+
+  // Close `depth` levels of ncclGroupStart (RCCL launches the group's kernels when the depth
+  // reaches 0) and hand the grouped works to the watchdog; with timing on, the whole grouped
+  // launch is one comm-stream interval reported by its first work.
+  void end_group_launch(int depth) {
+    std::shared_ptr<Interval> iv;
+    if (timed_group_ && !group_works_.empty()) {
+      c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
+      iv = std::make_shared<Interval>(tpool_);
+      XDDP_HIP_CHECK(hipEventRecord(iv->t0, stream_.stream()));
+    }
+    for (int k = 0; k < depth; ++k) XDDP_NCCL_CHECK(ncclGroupEnd());
+    if (iv) XDDP_HIP_CHECK(hipEventRecord(iv->t1, stream_.stream()));
+    for (size_t i = 0; i < group_works_.size(); ++i) {
+      if (iv) {
+        group_works_[i]->iv = iv;
+        group_works_[i]->owns_interval = i == 0;
+      }
+      finish_launch(group_works_[i]);
+    }
+    group_works_.clear();
+    timed_group_ = false;
   }
 
   // One-rank collectives that are identities: no RCCL launch, a Work that is already ordered.
   std::shared_ptr<Work> local_noop(const char* name, const at::Tensor& t) {
     TORCH_CHECK(err_->load() == 0, "xddp rccl: communicator is in error state");
-    auto w = std::make_shared<RcclWork>(pool_, device_, err_);
+    auto w = std::make_shared<RcclWork>(pool_, device_, err_, peer_);
     w->seq = flight_.record(name, t.numel(), t.scalar_type());
     XDDP_HIP_CHECK(hipEventRecord(w->ev, c10::hip::getCurrentHIPStream(device_).stream()));
     flight_.finish(w->seq, "completed");
     w->outputs = {t};
+    w->collective = false;  // one rank: nothing crossed a link
     return w;
   }
 
@@ -445,6 +588,12 @@ class RcclComm : public Comm {
         } catch (...) {
         }
       }
+      if (err_->load() == 0 && peer_ && peer_->status() != 0) {
+        reason = "peer-memory collective: a rank did not arrive within " +
+                 std::to_string(static_cast<int64_t>(peer_->timeout_ms())) + " ms (XDDP_PEER_TIMEOUT_MS)";
+        std::cerr << "[xddp rank " << rank_ << "] watchdog: " << reason << "; aborting communicator\n";
+        err_->store(4);
+      }
       if (err_->load() == 0 && comm_ && !aborted_ && !destroyed_) {
         ncclResult_t ae = ncclSuccess;
         if (ncclCommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
@@ -494,13 +643,19 @@ class RcclComm : public Comm {
   std::chrono::milliseconds timeout_;
   c10::hip::HIPStream stream_;
   std::shared_ptr<EventPool> pool_;
+  std::shared_ptr<EventPool> tpool_;  // timing-enabled events (Comm::set_timing)
   std::shared_ptr<std::atomic<int>> err_;
   ncclComm_t comm_ = nullptr;
   std::mutex comm_mu_;
   bool aborted_ = false;
   bool destroyed_ = false;
-  std::unique_ptr<PeerAllReduce> peer_;
+  std::shared_ptr<PeerAllReduce> peer_;
+  int peer_mode_ = 0;
   int64_t peer_bytes_ = 0;
+  int64_t two_shot_min_ = 0;
+  int64_t two_shot_max_ = 0;
+  bool high_priority_ = true;
+  bool timed_group_ = false;
   bool force_launch_ = false;
   int in_group_ = 0;
   bool capturing_ = false;

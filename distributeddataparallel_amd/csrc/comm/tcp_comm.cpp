@@ -42,10 +42,21 @@ class CpuWork : public Work {
     }
     cv.notify_all();
   }
+  Timing timing_state() override {
+    if (!timed) return Timing::kNone;
+    std::lock_guard<std::mutex> g(mu);
+    return done ? Timing::kReady : Timing::kPending;
+  }
+  double comm_ms() override { return (t1 - t0) * 1e-6; }
+  double comm_ms_before(const TimeRef& ref) override {
+    return std::max<double>(0.0, std::min<int64_t>(ref.ns, t1) - t0) * 1e-6;
+  }
   std::mutex mu;
   std::condition_variable cv;
   bool done = false;
   std::exception_ptr err;
+  bool timed = false;
+  int64_t t0 = 0, t1 = 0;  // worker-thread clock around the collective (timed works)
 };
 
 // A host-staged collective on device tensors: wait() finishes the host collective, then copies
@@ -53,6 +64,9 @@ class CpuWork : public Work {
 class StagedWork : public Work {
  public:
   bool is_completed() override { return inner->is_completed(); }
+  Timing timing_state() override { return inner->timing_state(); }
+  double comm_ms() override { return inner->comm_ms(); }
+  double comm_ms_before(const TimeRef& ref) override { return inner->comm_ms_before(ref); }
   void wait() override {
     inner->wait();
     std::lock_guard<std::mutex> g(mu);
@@ -183,6 +197,7 @@ class TcpComm : public Comm {
     w->inner = std::move(inner);
     w->back = std::move(back);
     w->seq = w->inner->seq;
+    w->collective = w->inner->collective;
     for (auto& p : w->back) w->outputs.push_back(p.first);
     return w;
   }
@@ -315,6 +330,9 @@ class TcpComm : public Comm {
     TORCH_CHECK(!meta.defined() || meta.device().is_cpu(), "xddp cpu backend: tensors must live on the CPU");
     auto w = std::make_shared<CpuWork>();
     w->outputs = std::move(outs);
+    w->collective = size_ > 1;
+    w->timed = timing_.load();
+    if (w->timed && w->collective) log_timed(w);
     w->seq = flight_.record(name, meta.defined() ? meta.numel() : 0, meta.defined() ? meta.scalar_type() : at::kByte);
     {
       std::lock_guard<std::mutex> g(qmu_);
@@ -322,7 +340,9 @@ class TcpComm : public Comm {
       if (error_) std::rethrow_exception(error_);
       q_.push_back([this, w, fn = std::move(fn)] {
         try {
+          w->t0 = now_ns();
           fn();
+          w->t1 = now_ns();
           flight_.finish(w->seq, "completed");
           w->finish(nullptr);
         } catch (...) {

@@ -539,7 +539,8 @@ __global__ __launch_bounds__(256) void bn_partial_finalize_kernel(
   const float dm = n > 0.f ? s1 / n : 0.f;
   const float mean = K + dm;
   const float m2 = fmaxf(s2 - s1 * dm, 0.f);
-  const float var = fmaxf(m2 / (float)M, 0.f);
+  const float Mf = M > 0 ? (float)M : n;  // M <= 0: the partials' own counts (uneven SyncBN shards)
+  const float var = Mf > 0.f ? fmaxf(m2 / Mf, 0.f) : 0.f;
   const float inv = rsqrtf(var + eps);
   mean_out[c] = mean;
   invstd_out[c] = inv;
@@ -550,7 +551,7 @@ __global__ __launch_bounds__(256) void bn_partial_finalize_kernel(
   if (running_mean) {
     float mom = momentum;
     if (cma && nbt) mom = 1.f / (float)(nbt[0] + 1);
-    const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
+    const float unbiased = Mf > 1.f ? var * Mf / (Mf - 1.f) : var;
     dev::Elem<W, float>::st(running_mean, c, (1.f - mom) * dev::Elem<W, float>::ld(running_mean, c) + mom * mean);
     dev::Elem<W, float>::st(running_var, c, (1.f - mom) * dev::Elem<W, float>::ld(running_var, c) + mom * unbiased);
   }
@@ -1331,7 +1332,7 @@ at::Tensor conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stri
 }
 
 // partials [groups, 3, N] (or [3, N, groups] when group_minor) -> (mean, invstd, scale_shift
-// [2, N]); updates running stats.
+// [2, N]); updates running stats. M = rows behind the partials; M <= 0 = sum the partials' counts.
 std::vector<at::Tensor> bn_stats_from_partials(const at::Tensor& part, int64_t M,
                                                const c10::optional<at::Tensor>& weight,
                                                const c10::optional<at::Tensor>& bias,

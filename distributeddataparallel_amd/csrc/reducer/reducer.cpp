@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <deque>
+#include <limits>
 #include <sstream>
 #include <unordered_set>
 
@@ -297,24 +298,51 @@ void Reducer::timer_record(int slot) {
 
 void Reducer::harvest_timings() {
   if (!timing_pending_) return;
-  double fwd, bwd, comm, overlap;
+  // the collectives' own comm-stream intervals must be complete as well
+  for (auto& bw : timed_works_)
+    if (bw.second->timing_state() == Work::Timing::kPending) return;
+  double fwd, bwd, tail;
+  TimeRef bwd_end;
   if (on_gpu()) {
     for (auto e : gpu_ev_)
       if (hipEventQuery(e) != hipSuccess) return;  // not done yet; try next iteration
-    float ms[4] = {0, 0, 0, 0};
+    float ms[3] = {0, 0, 0};
     (void)hipEventElapsedTime(&ms[0], gpu_ev_[0], gpu_ev_[1]);
     (void)hipEventElapsedTime(&ms[1], gpu_ev_[1], gpu_ev_[2]);
-    (void)hipEventElapsedTime(&ms[2], gpu_ev_[3], gpu_ev_[4]);
-    (void)hipEventElapsedTime(&ms[3], gpu_ev_[3], gpu_ev_[2]);
-    fwd = ms[0] * 1e6; bwd = ms[1] * 1e6; comm = ms[2] * 1e6; overlap = std::max(0.f, ms[3]) * 1e6;
+    (void)hipEventElapsedTime(&ms[2], gpu_ev_[2], gpu_ev_[4]);
+    fwd = ms[0] * 1e6; bwd = ms[1] * 1e6; tail = std::max(0.f, ms[2]) * 1e6;
+    bwd_end.ev = gpu_ev_[2];
   } else {
     fwd = double(cpu_ts_[1] - cpu_ts_[0]);
     bwd = double(cpu_ts_[2] - cpu_ts_[1]);
-    comm = double(cpu_ts_[4] - cpu_ts_[3]);
-    overlap = std::max<double>(0, double(cpu_ts_[2] - cpu_ts_[3]));
+    tail = std::max<double>(0, double(cpu_ts_[4] - cpu_ts_[2]));
+    bwd_end.ns = cpu_ts_[2];
   }
-  sum_fwd_ += fwd; sum_bwd_ += bwd; sum_comm_ += comm; sum_overlap_ += overlap;
+  sum_fwd_ += fwd; sum_bwd_ += bwd;
   n_timed_++;
+  // Communication = what the collectives themselves took where they ran (comm-stream events /
+  // the CPU backend's worker clock), not an interval on the compute stream. Iterations in which
+  // nothing crossed a link (one rank) contribute no comm sample at all.
+  int64_t launched = 0;
+  double comm = 0, overlap = 0;
+  for (auto& bw : timed_works_) {
+    auto& w = bw.second;
+    if (!w->collective) continue;
+    launched++;
+    if (w->timing_state() != Work::Timing::kReady) continue;
+    const double c = w->comm_ms() * 1e6;
+    comm += c;
+    overlap += w->comm_ms_before(bwd_end) * 1e6;
+    const size_t b = static_cast<size_t>(bw.first);
+    if (bucket_comm_sum_.size() <= b) bucket_comm_sum_.resize(b + 1, 0.0);
+    bucket_comm_sum_[b] += c;
+  }
+  timed_works_.clear();
+  collectives_launched_ += launched;
+  if (launched > 0) {
+    sum_comm_ += comm; sum_overlap_ += overlap; sum_tail_ += tail;
+    n_comm_timed_++;
+  }
   timing_pending_ = false;
 }
 
@@ -360,6 +388,7 @@ void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs) {
     TORCH_CHECK(false, os.str());
   }
   timer_record(1);
+  if (timing_this_iter_) comm_->set_timing(true);
   expect_hooks_ = true;
   require_finalize_ = true;
   finalize_queued_ = false;
@@ -672,7 +701,12 @@ void Reducer::finalize_backward() {
   for (auto& f : post_bwd_futs_) f->wait();
   post_bwd_futs_.clear();
   timer_record(4);
-  if (timing_this_iter_) timing_pending_ = true;
+  if (timing_this_iter_) {
+    timing_pending_ = true;
+    comm_->set_timing(false);
+    auto ws = comm_->drain_timed_works();
+    for (size_t i = 0; i < ws.size(); ++i) timed_works_.emplace_back(static_cast<int64_t>(i), std::move(ws[i]));
+  }
   timing_this_iter_ = false;
   if (!has_rebuilt_) prev_ready_order_ = ready_order_;
   expect_hooks_ = false;
@@ -788,8 +822,16 @@ void Reducer::install_post_backward_futures(std::vector<std::shared_ptr<HookResu
 
 void Reducer::reset_runtime_stats() {
   std::lock_guard<std::mutex> g(mu_);
-  sum_fwd_ = sum_bwd_ = sum_comm_ = sum_overlap_ = 0;
-  n_timed_ = 0;
+  sum_fwd_ = sum_bwd_ = sum_comm_ = sum_overlap_ = sum_tail_ = 0;
+  n_timed_ = n_comm_timed_ = collectives_launched_ = 0;
+  bucket_comm_sum_.clear();
+}
+
+std::vector<double> Reducer::bucket_comm_times() const {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<double> r(bucket_comm_sum_.size());
+  for (size_t b = 0; b < r.size(); ++b) r[b] = n_comm_timed_ ? bucket_comm_sum_[b] / n_comm_timed_ : 0.0;
+  return r;
 }
 
 std::vector<std::vector<int64_t>> Reducer::sync_bucket_indices(std::vector<std::vector<int64_t>> indices,
@@ -837,6 +879,7 @@ bool Reducer::rebuild_buckets() {
   auto limits = res.second;
   auto idx = sync_bucket_indices(res.first, limits);
   initialize_buckets(idx, limits);
+  bucket_comm_sum_.clear();  // per-bucket comm samples refer to the layout they were taken on
   return true;
 }
 
@@ -871,8 +914,15 @@ std::map<std::string, double> Reducer::runtime_stats() const {
   const double n = std::max<int64_t>(1, n_timed_);
   m["avg_forward_compute_time"] = sum_fwd_ / n;
   m["avg_backward_compute_time"] = sum_bwd_ / n;
-  m["avg_backward_comm_time"] = sum_comm_ / n;
-  m["avg_backward_compute_comm_overlap_time"] = sum_overlap_ / n;
+  // comm fields only from iterations that launched collectives (NaN = never measured; Python
+  // reports it as null): at one rank every collective is a local identity
+  const double nan = std::numeric_limits<double>::quiet_NaN();
+  const double nc = static_cast<double>(n_comm_timed_);
+  m["avg_backward_comm_time"] = n_comm_timed_ ? sum_comm_ / nc : nan;
+  m["avg_backward_compute_comm_overlap_time"] = n_comm_timed_ ? sum_overlap_ / nc : nan;
+  m["avg_backward_exposed_comm_time"] = n_comm_timed_ ? sum_tail_ / nc : nan;
+  m["num_comm_timed_iterations"] = nc;
+  m["num_collectives_launched"] = static_cast<double>(collectives_launched_);
   m["num_timed_iterations"] = static_cast<double>(n_timed_);
   m["iteration"] = static_cast<double>(num_iterations_);
   m["num_native_launches"] = static_cast<double>(native_launches_);

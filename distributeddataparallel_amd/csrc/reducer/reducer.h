@@ -120,6 +120,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
 
   // Timing/logging (c10d::Logger analogue); values in ns.
   std::map<std::string, double> runtime_stats() const;
+  // Average comm-stream duration (ns) of each bucket's collective over the timed iterations.
+  std::vector<double> bucket_comm_times() const;
   std::map<std::string, std::string> construction_data() const;
 
   // Test hook: number of native multi-tensor launches issued so far.
@@ -208,8 +210,14 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<hipEvent_t> gpu_ev_;
   std::vector<int64_t> cpu_ts_;
   bool timing_pending_ = false;
-  double sum_fwd_ = 0, sum_bwd_ = 0, sum_comm_ = 0, sum_overlap_ = 0;
+  double sum_fwd_ = 0, sum_bwd_ = 0, sum_comm_ = 0, sum_overlap_ = 0, sum_tail_ = 0;
   int64_t n_timed_ = 0;
+  int64_t n_comm_timed_ = 0;          // timed iterations that launched >= 1 collective
+  int64_t collectives_launched_ = 0;  // over the timed iterations
+  // (launch index, work) awaiting harvest: the collectives of a sampled backward in launch order
+  // (= bucket order for the built-in all-reduce)
+  std::vector<std::pair<int64_t, std::shared_ptr<Work>>> timed_works_;
+  std::vector<double> bucket_comm_sum_;  // ns, per launch index
   void harvest_timings();
 };
 

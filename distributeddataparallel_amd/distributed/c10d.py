@@ -23,6 +23,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from .._native import load
+from . import rccl_info
 from .rendezvous import advertise_host, rendezvous
 
 __all__ = [
@@ -270,6 +271,16 @@ class ProcessGroup:
     def flight_records(self):
         return self.comm.flight_records()
 
+    def comm_info(self) -> dict:
+        """What the communicator reports about itself: the native backend facts plus, for RCCL at
+        W > 1, RCCL's own view parsed from its init log (version, ranks, channels, rings)."""
+        out = dict(self.comm.info())
+        extra = _comm_info.get(id(self.comm), {})
+        out.update(extra)
+        if extra.get("rccl_log"):
+            out["rccl"] = rccl_info.parse(extra["rccl_log"])
+        return out
+
     def shutdown(self):
         self.comm.shutdown()
 
@@ -315,21 +326,29 @@ def _make_comm(backend: str, store, rank: int, size: int, device, timeout: timed
     """Create the native communicator; XDDP_DEBUG=DETAIL / XDDP_NAN_CHECK=1 wrap it in the debug
     communicator (cross-rank collective fingerprints / NaN scan)."""
     C = load()
+    info = {}
     if backend == "fake":
         return C.make_fake_comm(rank, size)
     if backend == "rccl":
         hp = os.environ.get("XDDP_COMM_HIGH_PRIORITY", "1") != "0"
+        log = rccl_info.prepare(rank, size)  # RCCL's own view of the job (W > 1), parsed after init
         comm = C.make_rccl_comm(store, rank, size, device.index, timeout.total_seconds(), hp)
+        info = rccl_info.collect(log)
     elif backend == "peer":  # IPC peer memory, one node, device tensors (csrc/comm/peer_comm.cpp)
-        cap = int(float(os.environ.get("XDDP_PEER_CAPACITY_MB", "16")) * (1 << 20)) // 4096 * 4096
-        comm = C.make_peer_comm(store, rank, size, device.index, max(cap, 4096))
+        mb = lambda k, d: max(0, int(float(os.environ.get(k, d)) * (1 << 20)) // 4096 * 4096)  # noqa: E731
+        comm = C.make_peer_comm(store, rank, size, device.index, max(mb("XDDP_PEER_CAPACITY_MB", "16"), 4096),
+                                mb("XDDP_PEER_TWO_SHOT_MB", "64"), timeout.total_seconds())
     else:
         comm = C.make_cpu_comm(store, rank, size, timeout.total_seconds(), advertise_host(master_addr))
     detail = os.environ.get("XDDP_DEBUG", os.environ.get("TORCH_DISTRIBUTED_DEBUG", "OFF")).upper() == "DETAIL"
     nan = os.environ.get("XDDP_NAN_CHECK", "0") == "1"
     if detail or nan:
         comm = C.make_debug_comm(comm, detail, nan)
+    _comm_info[id(comm)] = info
     return comm
+
+
+_comm_info: dict = {}  # id(native comm) -> facts parsed at creation (RCCL debug log)
 
 
 def init_process_group(backend: Optional[str] = None, init_method: Optional[str] = None,

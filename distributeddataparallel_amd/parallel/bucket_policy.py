@@ -8,11 +8,13 @@ buckets from a two-term cost model of one all-reduce of S bytes over W ranks::
 
     t(S) = alpha + 2 (W-1)/W * S / B
 
-* ``alpha``  - fixed cost per RCCL all-reduce launch (kernel launch + ring latency), ~30 us at
-  W=8 for small messages;
-* ``B``      - achieved bus bandwidth for large messages. Bounded by 7 x 153 GB/s; the default
-  assumes 350 GB/s, and ``bench.py`` measures the real per-bucket busbw at N>1 so the
-  assumption can be replaced by a measurement (``XDDP_RCCL_BUSBW_GBPS``).
+* ``alpha``  - fixed cost per RCCL all-reduce launch (kernel launch + ring latency). ASSUMED
+  30 us at W=8 (not yet measured on an 8-GPU node; ``XDDP_RCCL_ALPHA_US`` overrides);
+* ``B``      - achieved all-reduce BUS bandwidth for large messages, i.e. what RCCL's rings
+  sustain over the node, not one link: bounded below by one xGMI link (~153 GB/s, a single ring)
+  and above by all seven (~1,071 GB/s). ASSUMED 350 GB/s (RCCL spreads several rings over the
+  links); ``bench.py`` measures the per-bucket busbw at N>1 so a measurement can replace it
+  (``XDDP_RCCL_BUSBW_GBPS``). docs/ARCHITECTURE.md uses the same two constants.
 
 Decisions, in gradient-ready order (the order buckets launch in):
 
@@ -36,12 +38,19 @@ Decisions, in gradient-ready order (the order buckets launch in):
 
 At W=1 nothing is communicated and the policy only changes the bucket layout.
 
-RCCL knobs (:func:`rccl_env_defaults`) are set only where the user has not set them, and
-only for W>1:
+A tail bucket cannot split a tensor: when the last-ready gradient is itself large (Llama-3-8B's
+1.05 GB token embedding) the tail IS that tensor and its all-reduce (~5 ms modelled at W=8) is
+exposed whatever the caps. :func:`tail_report` states the modelled exposed time and the
+mitigation in use: with the overlapped optimizer (``DDP.register_overlapped_optimizer``, the
+bench default for transformer configs at W>1) every other bucket's AdamW update runs on a side
+stream while the tail all-reduce is in flight, so the tail hides behind optimizer work that the
+step has to do anyway.
 
-* ``NCCL_MAX_NCHANNELS`` = 32: RCCL runs one workgroup per channel; 32 channels give every
-  one of the 7 links >= 4 channels while leaving 224 of the 256 CUs to the backward kernels
-  that the all-reduce overlaps (backward is compute-bound here; comm is not).
+RCCL knobs (:func:`rccl_env_defaults`): none are forced. RCCL picks its channel count for the
+node's topology; an unmeasured cap could cut large-bucket bandwidth on the 7-link mesh. A cap
+can be requested explicitly with ``XDDP_RCCL_MAX_CHANNELS`` (exported as ``NCCL_MAX_NCHANNELS``
+when the user has not set that), e.g. to leave CUs to the backward kernels once an 8-GPU
+measurement shows it pays.
 """
 from __future__ import annotations
 
@@ -128,22 +137,45 @@ def bucket_bytes(sizes_bytes: Sequence[int], layout: List[List[int]]) -> List[in
     return [sum(sizes_bytes[i] for i in b) for b in layout]
 
 
-def exposed_tail_us(sizes: List[int], world_size: int, alpha_us: float = DEFAULT_ALPHA_US,
-                    busbw_gbps: float = DEFAULT_BUSBW_GBPS) -> float:
+def exposed_tail_us(sizes: List[int], world_size: int, alpha_us: float | None = None,
+                    busbw_gbps: float | None = None) -> float:
     """Modelled time of the last bucket's all-reduce (the part of comm backward cannot hide)."""
+    alpha = alpha_us if alpha_us is not None else _env_float("XDDP_RCCL_ALPHA_US", DEFAULT_ALPHA_US)
+    bw = busbw_gbps if busbw_gbps is not None else _env_float("XDDP_RCCL_BUSBW_GBPS", DEFAULT_BUSBW_GBPS)
     w = max(2, world_size)
-    return alpha_us + 2.0 * (w - 1) / w * sizes[-1] / (busbw_gbps * 1e3)
+    return alpha + 2.0 * (w - 1) / w * sizes[-1] / (bw * 1e3)
+
+
+def tail_report(sizes: List[int], plan: BucketPlan, world_size: int, overlapped_optimizer: bool) -> dict:
+    """The tail bucket as built, its modelled exposed all-reduce time, and what hides it."""
+    if not sizes:
+        return {}
+    exposed = exposed_tail_us(sizes, world_size) if world_size > 1 else 0.0
+    over_cap = plan.tail_bytes > 0 and sizes[-1] > plan.tail_bytes
+    if world_size <= 1:
+        mitigation = "none needed (one rank: nothing is communicated)"
+    elif overlapped_optimizer:
+        mitigation = ("overlapped optimizer: the other buckets' updates run on a side stream while the tail "
+                      "all-reduce is in flight")
+    elif plan.tail_bytes > 0 and not over_cap:
+        mitigation = f"tail cap: the last bucket holds <= {plan.tail_bytes} B"
+    else:
+        mitigation = "none"
+    return {"tail_bytes": int(sizes[-1]), "tail_cap_bytes": int(plan.tail_bytes),
+            "tail_is_one_tensor_over_cap": bool(over_cap), "exposed_tail_us_model": round(exposed, 1),
+            "mitigation": mitigation}
 
 
 def rccl_env_defaults(world_size: int, backend: str) -> dict:
-    """Set RCCL env defaults that are unset; returns what was set (reported by bench.py)."""
-    if world_size <= 1 or backend != "rccl" or os.environ.get("XDDP_RCCL_ENV_DEFAULTS", "1") == "0":
+    """Export the RCCL knobs the user asked for through XDDP_* variables (nothing is forced);
+    returns what was set (reported by bench.py)."""
+    if world_size <= 1 or backend != "rccl":
         return {}
     applied = {}
-    for k, v in (("NCCL_MAX_NCHANNELS", "32"),):
-        if k not in os.environ:
-            os.environ[k] = v
-            applied[k] = v
+    ch = os.environ.get("XDDP_RCCL_MAX_CHANNELS")
+    if ch and "NCCL_MAX_NCHANNELS" not in os.environ:
+        os.environ["NCCL_MAX_NCHANNELS"] = ch
+        applied["NCCL_MAX_NCHANNELS"] = ch
     return applied
 
 

@@ -149,8 +149,14 @@ class _DDPJoinHook(JoinHook):
         op and the unused-parameter bitmap — or nothing more when that iteration does not sync."""
         ddp = self.ddp
         ddp.reducer.rebuild_buckets()
-        ddp._check_and_sync_module_buffers()
+        # buffers go through the same hook-or-broadcast helper, at the same place, as on the
+        # training ranks: PRE_FORWARD (or the default broadcast) before the sync flag, a
+        # POST_FORWARD hook after it
+        if ddp._check_sync_bufs_pre_fwd():
+            ddp._sync_buffers(joined=True)
         should_sync = ddp._check_global_requires_backward_grad_sync(is_joined_rank=True)
+        if ddp._check_sync_bufs_post_fwd():
+            ddp._sync_buffers(joined=True)
         # a skipped-sync iteration means the next forward does not broadcast buffers either
         ddp.require_forward_param_sync = should_sync
         if not should_sync:
@@ -620,15 +626,18 @@ class DistributedDataParallel(nn.Module, Joinable):
             raise ValueError("BUG! Expected rank_cond to be true for at least one process.")
         return r
 
-    def _sync_buffers(self, src: int = 0):
+    def _sync_buffers(self, src: int = 0, joined: bool = False):
+        """Per-forward buffer sync: the registered buffer comm hook, or a coalesced broadcast from
+        ``src`` (under Join: from a rank still training). ``joined=True`` is the shadow a joined
+        rank runs in ``_DDPJoinHook.main_hook`` — the same collectives in the same order."""
         with torch.no_grad():
-            if self._join_config.enable:
-                src = self._find_common_rank(self.process_group.rank(), True)
+            if self._join_config.enable or joined:
+                src = self._find_common_rank(self.process_group.rank(), not joined)
             hook = getattr(self, "buffer_hook", None)
             if hook is not None:
                 futs = hook[0](hook[1], self.named_module_buffers)
                 if futs:
-                    if torch.is_grad_enabled() and self.require_backward_grad_sync:
+                    if not joined and torch.is_grad_enabled() and self.require_backward_grad_sync:
                         self.reducer.install_post_backward_futures(list(futs))
                     else:
                         for f in futs:
@@ -641,11 +650,7 @@ class DistributedDataParallel(nn.Module, Joinable):
 
     def _check_and_sync_module_buffers(self):
         if self.will_sync_module_buffers():
-            src = self._find_common_rank(self.process_group.rank(), False)
-            C = load()
-            bufs = [b for b in self._buffers_list if b.numel() > 0]
-            if bufs:
-                C.broadcast_coalesced(self.process_group.comm, bufs, self.broadcast_bucket_size, src)
+            self._sync_buffers(joined=True)
 
     def _sync_final_model(self, is_last_joiner: bool):
         src = self._find_common_rank(self.process_group.rank(), is_last_joiner)
@@ -757,7 +762,10 @@ class DistributedDataParallel(nn.Module, Joinable):
         d = dict(self.reducer.construction_data())
         d["bucket_policy"] = self.bucket_plan.policy
         for k, v in self.reducer.runtime_stats().items():
-            d[k] = int(v) if float(v).is_integer() else v
+            v = float(v)
+            # NaN = never measured (e.g. comm fields when no collective crossed a link)
+            d[k] = None if v != v else (int(v) if v.is_integer() else v)
+        d["bucket_comm_times"] = [round(t) for t in self.reducer.bucket_comm_times()]
         d["module_name"] = type(self.module).__name__
         d["device_ids"] = "" if not self.device_ids else ", ".join(str(x.index) for x in self.device_ids)
         d["broadcast_buffers"] = int(self.broadcast_buffers)

@@ -68,15 +68,17 @@ class _SyncBN(torch.autograd.Function):
         shape = [1, C] + [1] * (x.dim() - 2)
         dyf, xf = dy.float(), x.float()
         xmu = xf - mean.view(shape)
-        sums = torch.stack([dyf.sum(dims), (dyf * xmu).sum(dims)])
+        # [C, 2] = (sum dy, sum dy·(x - mean)): the same payload layout as the native path, so ranks
+        # that take different paths (layout / alignment differs) still reduce matching channels
+        sums = torch.stack([dyf.sum(dims), (dyf * xmu).sum(dims)], dim=1).contiguous()
         local_sums = sums.clone()
         ctx.pg.allreduce(sums).wait()
-        sum_dy, sum_dy_xmu = sums[0], sums[1]
+        sum_dy, sum_dy_xmu = sums[:, 0], sums[:, 1]
         g = weight.float() if weight is not None else torch.ones(C, device=x.device)
         dx = (dyf - (sum_dy / n).view(shape) - xmu * (invstd ** 2 * sum_dy_xmu / n).view(shape)) \
             * (g * invstd).view(shape)
-        dw = (local_sums[1] * invstd).to(weight.dtype) if weight is not None else None
-        db = local_sums[0].to(weight.dtype) if weight is not None else None
+        dw = (local_sums[:, 1] * invstd).to(weight.dtype) if weight is not None else None
+        db = local_sums[:, 0].to(weight.dtype) if weight is not None else None
         return dx.to(x.dtype), dw, db, None, None, None, None, None
 
 
@@ -95,12 +97,14 @@ class _SyncBNNative(torch.autograd.Function):
         local = C.bn_moments(x)  # [3, C]: count, mean, M2
         gathered = torch.empty((pg.size(),) + tuple(local.shape), device=x.device, dtype=torch.float32)
         pg.allgather_into_tensor(gathered, local).wait()
-        M = int(x.numel() // x.shape[1]) * pg.size()  # equal shards (the counts in `gathered` are exact)
-        mean, invstd, ss = C.bn_stats_from_partials(gathered, M, weight, bias, running_mean, running_var, None,
+        # M = 0: the finalize sums the gathered per-rank counts on the device, so uneven shards (a
+        # short last batch, uneven samplers) get exact statistics without a host sync
+        mean, invstd, ss = C.bn_stats_from_partials(gathered, 0, weight, bias, running_mean, running_var, None,
                                                     momentum, False, eps)
         y, _ = C.bn_apply(x, ss, None, False, False, None)
-        ctx.save_for_backward(x, weight, mean, invstd)
-        ctx.pg, ctx.M = pg, M
+        count = gathered[:, 0, :1].sum(0)  # [1]: global rows behind the statistics (device)
+        ctx.save_for_backward(x, weight, mean, invstd, count)
+        ctx.pg = pg
         return y
 
     @staticmethod
@@ -108,7 +112,7 @@ class _SyncBNNative(torch.autograd.Function):
         from .._native import load
 
         C = load()
-        x, weight, mean, invstd = ctx.saved_tensors
+        x, weight, mean, invstd, count = ctx.saved_tensors
         part = C.bn_grad_partials(dy, x, mean)  # [blocks, C, 2]: sum dy, sum dy·(x - mean)
         local = part.sum(0, keepdim=True)
         total = local.clone()
@@ -118,7 +122,9 @@ class _SyncBNNative(torch.autograd.Function):
         if need_w:  # local dweight / dbias, computed while the all-reduce is in flight
             _, dw, db = C.bn_backward_from_partials(local, x.numel() // x.shape[1], weight, mean, invstd, True, False)
         work.wait()
-        coef, _, _ = C.bn_backward_from_partials(total, ctx.M, weight, mean, invstd, False, False)
+        # the finalize scales the sums by 1/M: hand it sums / global count with M = 1 (exact for
+        # uneven shards, no host sync)
+        coef, _, _ = C.bn_backward_from_partials(total / count, 1, weight, mean, invstd, False, False)
         dx = C.bn_backward_elem(dy.contiguous(memory_format=torch.channels_last), x, mean, coef)
         return dx, dw, db, None, None, None, None, None
 

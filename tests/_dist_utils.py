@@ -17,9 +17,9 @@ def _entry(rank, fn, world, backend, args):
         xdist.destroy_process_group()
 
 
-def run_ranks(fn, world=2, backend="cpu", args=()):
+def run_ranks(fn, world=2, backend="cpu", args=(), env=None):
     from distributeddataparallel_amd.utils.spawn import free_port, spawn
 
     env = {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port()), "OMP_NUM_THREADS": "1",
-           "XDDP_TEST_TORCH_PORT": str(free_port())}
+           "XDDP_TEST_TORCH_PORT": str(free_port()), **(env or {})}
     spawn(_entry, args=(fn, world, backend, args), nprocs=world, env=env)

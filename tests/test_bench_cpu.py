@@ -11,12 +11,12 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(extra_env=None, args=()):
+def _run(extra_env=None, args=(), gpus=2):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
     env.update(extra_env or {})
-    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--device", "cpu",
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--device", "cpu",
                            "--model", "mlp", "--steps", "3", "--warmup", "2", *args],
                           capture_output=True, text=True, timeout=240, env=env, cwd="/tmp")
 
@@ -32,7 +32,16 @@ def test_self_launch_reports_one_json_line(tmp_path):
     assert d["n_gpus"] == 2 and d["nranks"] == 2 and d["config"]["parallelism"] == "dp2"
     assert d["steps"] == 3 and d["warmup"] == 2 and d["value"] > 0
     assert d["buckets"]["count"] >= 1 and sum(d["buckets"]["bytes"]) > 0
-    assert d["comm"]["avg_backward_comm_ms"] > 0 and d["comm"]["timed_iterations"] >= 2
+    c = d["comm"]
+    # comm is what the collectives themselves took (the CPU backend's worker clock), one sample per
+    # bucket all-reduce; overlap can never exceed it
+    assert c["collectives_launched"] >= d["buckets"]["count"] and c["timed_iterations"] >= 2
+    assert c["avg_backward_comm_ms"] > 0 and 0 <= c["avg_overlap_ms"] <= c["avg_backward_comm_ms"] + 1e-6
+    assert c["exposed_comm_ms"] >= 0 and 0 <= c["overlap_pct"] <= 100.0
+    assert len(c["per_bucket_comm_ms"]) >= d["buckets"]["count"]
+    assert abs(sum(c["per_bucket_comm_ms"]) - c["avg_backward_comm_ms"]) < 0.01 * c["avg_backward_comm_ms"] + 0.01
+    assert d["comm_info"]["backend"] == "cpu" and d["comm_info"]["rank_devices"] == [-1, -1]
+    assert d["buckets"]["tail"]["tail_bytes"] == d["buckets"]["bytes"][-1]
     assert d["allreduce_busbw"] and all(p["busbw_GBps"] > 0 for p in d["allreduce_busbw"])
     assert d["scaling_efficiency"] == pytest.approx(d["value"] / 2000.0, rel=1e-3)
 
@@ -42,3 +51,17 @@ def test_self_launch_fails_when_a_rank_fails():
     assert r.returncode != 0
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert "failed" in r.stderr
+
+
+def test_one_rank_reports_no_comm():
+    """At N=1 nothing crosses a link: the comm fields are null, not backward compute time."""
+    r = _run(gpus=1)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    c = d["comm"]
+    assert c["collectives_launched"] == 0
+    for k in ("avg_backward_comm_ms", "avg_overlap_ms", "exposed_comm_ms", "overlap_pct", "per_bucket_comm_ms"):
+        assert c[k] is None, (k, c)
+    assert c["avg_backward_compute_ms"] is not None and c["timed_iterations"] >= 2
+    assert "allreduce_busbw" not in d and "warning" not in d
+    assert d["buckets"]["tail"]["exposed_tail_us_model"] == 0.0

@@ -65,8 +65,24 @@ def test_llama3_8b_layout_pinned():
     ref = bp.assign(sizes, bp.reference_plan())
     assert plan.cap_bytes == 256 * MiB
     assert len(lay) == 50 and len(ref) == 162   # 3x fewer RCCL launches per step
-    # the embedding (1 GB) is produced last in backward and forms the tail bucket on its own
-    assert bp.bucket_bytes(sizes, lay)[-1] == sizes[-1]
+    # The embedding (1 GB) is produced last in backward: no cap can shrink a bucket below one
+    # tensor, so the tail is exposed (~5 ms at W=8) unless something hides it. The report must say
+    # so, and name the overlapped optimizer when it is on.
+    by = bp.bucket_bytes(sizes, lay)
+    assert by[-1] == sizes[-1] > plan.tail_bytes
+    rep = bp.tail_report(by, plan, 8, overlapped_optimizer=False)
+    assert rep["tail_is_one_tensor_over_cap"] and rep["mitigation"] == "none"
+    assert rep["exposed_tail_us_model"] > 4000
+    rep = bp.tail_report(by, plan, 8, overlapped_optimizer=True)
+    assert rep["mitigation"].startswith("overlapped optimizer")
+
+
+def test_tail_report_small_tail_uses_cap():
+    plan = bp.xgmi_plan(100 * MiB, 8, alpha_us=30, busbw_gbps=350)
+    rep = bp.tail_report([40 * MiB, 50 * MiB, plan.tail_bytes // 2], plan, 8, overlapped_optimizer=False)
+    assert not rep["tail_is_one_tensor_over_cap"] and rep["mitigation"].startswith("tail cap")
+    assert rep["exposed_tail_us_model"] < 60
+    assert bp.tail_report([1, 2], plan, 1, False)["exposed_tail_us_model"] == 0.0
 
 
 def test_native_rebuild_matches_python_planner():
@@ -106,11 +122,16 @@ def test_explicit_cap_keeps_reference_semantics():
     assert plan.policy == "xgmi" and not explicit
 
 
-def test_rccl_env_defaults_only_when_unset(monkeypatch):
+def test_rccl_env_defaults_force_nothing(monkeypatch):
     monkeypatch.delenv("NCCL_MAX_NCHANNELS", raising=False)
+    monkeypatch.delenv("XDDP_RCCL_MAX_CHANNELS", raising=False)
     assert bp.rccl_env_defaults(1, "rccl") == {}
-    got = bp.rccl_env_defaults(8, "rccl")
-    assert got == {"NCCL_MAX_NCHANNELS": "32"}
-    monkeypatch.setenv("NCCL_MAX_NCHANNELS", "64")
+    assert bp.rccl_env_defaults(8, "rccl") == {}          # no unmeasured channel cap by default
+    assert "NCCL_MAX_NCHANNELS" not in os.environ
+    monkeypatch.setenv("XDDP_RCCL_MAX_CHANNELS", "48")   # explicit opt-in
+    assert bp.rccl_env_defaults(8, "rccl") == {"NCCL_MAX_NCHANNELS": "48"}
+    monkeypatch.setenv("NCCL_MAX_NCHANNELS", "64")       # the user's own setting wins
+    monkeypatch.setenv("XDDP_RCCL_MAX_CHANNELS", "16")
     assert bp.rccl_env_defaults(8, "rccl") == {}
     assert os.environ["NCCL_MAX_NCHANNELS"] == "64"
+

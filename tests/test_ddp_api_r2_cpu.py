@@ -434,3 +434,38 @@ def test_overlapped_optimizer_matches_step_after_backward():
     """DDP.register_overlapped_optimizer: the per-bucket FusedAdamW.step_params inside backward
     trains exactly like the usual backward-then-step."""
     run_ranks(_w_overlapped_optimizer, world=2)
+
+
+def _w_join_buffer_hook(rank, world, location):
+    """Uneven inputs + a buffer comm hook: the joined rank must shadow the hook's collectives
+    (not a broadcast) at the same point of the iteration."""
+    import distributeddataparallel_amd as xddp
+    from distributeddataparallel_amd import distributed as xdist
+    from distributeddataparallel_amd.parallel.distributed import BufferCommHookLocation
+
+    m = _BufNet()
+    ddp = xddp.DDP(m)
+
+    def hook(state, named_buffers):
+        return [xdist.all_reduce(b, op=xdist.ReduceOp.AVG, async_op=True).get_future()
+                for b in named_buffers.values() if b.is_floating_point()]
+
+    ddp._register_buffer_comm_hook(None, hook, getattr(BufferCommHookLocation, location))
+    g = torch.Generator().manual_seed(rank)
+    n_inputs = 4 if rank == 0 else 1
+    with ddp.join():
+        for _ in range(n_inputs):
+            ddp(torch.randn(8, 6, generator=g) + rank).sum().backward()
+    # both ranks still agree afterwards: a healthy collective sequence
+    t = torch.tensor([float(rank + 1)])
+    xdist.all_reduce(t)
+    assert t.item() == 3.0
+    assert m.steps.item() == 4  # the final model sync copies the last joiner's buffers
+
+
+def test_join_with_buffer_comm_hook_post_forward():
+    run_ranks(_w_join_buffer_hook, world=2, args=("POST_FORWARD",))
+
+
+def test_join_with_buffer_comm_hook_pre_forward():
+    run_ranks(_w_join_buffer_hook, world=2, args=("PRE_FORWARD",))

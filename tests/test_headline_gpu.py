@@ -184,3 +184,47 @@ def test_resnet50_overfit_curve_tracks_fp32_reference():
         assert all(torch.isfinite(torch.tensor(la)))
     finally:
         dist.destroy_process_group()
+
+
+def test_config3_no_sync_accumulation_bf16_fused_vs_fp32():
+    """BASELINE config 3: bf16 channels_last ResNet-50 with FusedBatchNorm2d under the xddp DDP,
+    two micro-batches of 16 @ 224 — the first inside ``no_sync()`` (gradients accumulate locally,
+    nothing is launched), the second synced (the accumulated gradients go through the bucket copy
+    and the all-reduce path). Oracle: an fp32 torch model accumulating the same two backward passes;
+    yardstick: the same bf16 model through plain torch ops (SkipInit-conditioned, as above)."""
+    import distributeddataparallel_amd as xddp
+    from distributeddataparallel_amd import distributed as dist
+    from distributeddataparallel_amd.utils.spawn import free_port
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(free_port())
+    dist.init_process_group("rccl", rank=0, world_size=1, device_id=0)
+    try:
+        fused, ref32, ref16, xa, ya = _models(16, 224, seed=5, branch_gamma=0.2)
+        g = torch.Generator(device="cuda").manual_seed(77)
+        xb = torch.randn(16, 3, 224, 224, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        yb = torch.randint(0, 1000, (16,), device="cuda", generator=g)
+        ddp = xddp.DDP(fused, device_ids=[0], gradient_as_bucket_view=True)
+        for it in range(2):  # iteration 0 = one bucket; iteration 1 = the rebuilt layout
+            for m in (fused, ref32, ref16):
+                m.zero_grad(set_to_none=True)
+            launches0 = ddp.reducer.native_launches()
+            with ddp.no_sync():
+                F.cross_entropy(ddp(xa).float(), ya).backward()
+            assert ddp.reducer.native_launches() == launches0, "no_sync must not pack or launch buckets"
+            F.cross_entropy(ddp(xb).float(), yb).backward()
+            for m, conv in ((ref32, lambda t: t.float()), (ref16, lambda t: t)):
+                F.cross_entropy(m(conv(xa)).float(), ya).backward()
+                F.cross_entropy(m(conv(xb)).float(), yb).backward()
+            torch.cuda.synchronize()
+            sf, s16 = _grad_stats(fused, ref32), _grad_stats(ref16, ref32)
+            for n, (rel, cos) in sf.items():
+                assert rel <= 1.5 * s16[n][0] + 0.02, (it, n, rel, s16[n][0])
+                assert cos >= s16[n][1] - 0.05, (it, n, cos, s16[n][1])
+            mf = sorted(r for r, _ in sf.values())[len(sf) // 2]
+            m16 = sorted(r for r, _ in s16.values())[len(s16) // 2]
+            assert mf <= 1.1 * m16 + 0.01, (it, mf, m16)
+        print(f"\nconfig 3 (no_sync x2): median rel-L2 vs fp32 fused {mf:.4f} torch-bf16 {m16:.4f}")
+    finally:
+        dist.destroy_process_group()

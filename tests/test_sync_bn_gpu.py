@@ -14,7 +14,7 @@ from _dist_utils import run_ranks  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def _w_syncbn(rank, world):
+def _w_syncbn(rank, world, bounds=(0, 4, 8), eager_ranks=()):
     import torch.nn as nn
 
     from distributeddataparallel_amd.parallel.sync_batchnorm import SyncBatchNorm, _SyncBNNative
@@ -39,8 +39,10 @@ def _w_syncbn(rank, world):
     with torch.no_grad():
         sbn.weight.copy_(weight)
         sbn.bias.copy_(bias)
-    sl = slice(rank * N // world, (rank + 1) * N // world)
-    x = full[sl].contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    sl = slice(bounds[rank], bounds[rank + 1])
+    eager = rank in eager_ranks  # NCHW input: this rank takes the eager path, the others the native one
+    fmt = torch.contiguous_format if eager else torch.channels_last
+    x = full[sl].contiguous(memory_format=fmt).requires_grad_(True)
     calls = []
     orig = _SyncBNNative.forward
 
@@ -53,8 +55,8 @@ def _w_syncbn(rank, world):
         y = sbn(x)
     finally:
         _SyncBNNative.forward = staticmethod(orig)
-    assert calls, "native SyncBatchNorm path did not run"
-    y.backward(dy_full[sl].contiguous(memory_format=torch.channels_last))
+    assert bool(calls) != eager, "wrong SyncBatchNorm path"
+    y.backward(dy_full[sl].contiguous(memory_format=fmt))
 
     def close(a, b, tol):
         err = ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
@@ -75,3 +77,14 @@ def _w_syncbn(rank, world):
 
 def test_sync_batchnorm_native_two_ranks():
     run_ranks(_w_syncbn, world=2, backend="cpu")
+
+
+def test_sync_batchnorm_native_uneven_shards():
+    """5 + 3 rows: the statistics and the 1/M backward terms use the exact global count."""
+    run_ranks(_w_syncbn, world=2, backend="cpu", args=((0, 5, 8),))
+
+
+def test_sync_batchnorm_mixed_native_and_eager_ranks():
+    """Rank 1's input is NCHW (eager path) while rank 0 runs the native kernels: the all-gathered
+    [3, C] blocks and the all-reduced [C, 2] sums have the same layout on both paths."""
+    run_ranks(_w_syncbn, world=2, backend="cpu", args=((0, 3, 8), (1,)))
