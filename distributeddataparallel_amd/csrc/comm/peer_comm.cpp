@@ -286,8 +286,10 @@ class PeerComm : public Comm {
       }
       const bool timed_out = peer_->status() != 0;
       for (auto& w : done) flight_.finish(w->seq, timed_out ? "failed" : "completed");
-      if (timed_out && st_->err.load() == 0) {
-        st_->err.store(1);
+      if (timed_out && !reported_) {  // (a Work query may have set the error state first)
+        reported_ = true;
+        int z = 0;
+        st_->err.compare_exchange_strong(z, 1);
         const std::string reason = "a peer did not arrive within " + std::to_string((int64_t)peer_->timeout_ms()) +
                                    " ms (XDDP_PEER_TIMEOUT_MS)";
         std::cerr << "[xddp rank " << rank_ << "] peer watchdog: " << reason << "; communicator is in error state\n";
@@ -337,6 +339,7 @@ class PeerComm : public Comm {
   at::Tensor barrier_buf_;
   std::thread watchdog_;
   std::atomic<bool> wd_stop_{false};
+  bool reported_ = false;  // watchdog thread only
   std::mutex wd_mu_;
   std::condition_variable wd_cv_;
   std::list<std::shared_ptr<PeerWork>> inflight_;

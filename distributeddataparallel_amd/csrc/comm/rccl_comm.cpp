@@ -588,11 +588,13 @@ class RcclComm : public Comm {
         } catch (...) {
         }
       }
-      if (err_->load() == 0 && peer_ && peer_->status() != 0) {
+      if ((err_->load() == 0 || err_->load() == 4) && reason.empty() && peer_ && peer_->status() != 0) {
+        // (a Work query may have flagged it first; the watchdog still dumps, posts and aborts)
         reason = "peer-memory collective: a rank did not arrive within " +
                  std::to_string(static_cast<int64_t>(peer_->timeout_ms())) + " ms (XDDP_PEER_TIMEOUT_MS)";
         std::cerr << "[xddp rank " << rank_ << "] watchdog: " << reason << "; aborting communicator\n";
-        err_->store(4);
+        int z = 0;
+        err_->compare_exchange_strong(z, 4);
       }
       if (err_->load() == 0 && comm_ && !aborted_ && !destroyed_) {
         ncclResult_t ae = ncclSuccess;

@@ -1,0 +1,310 @@
+// Dense bf16 GEMM for the transformer linear layers (ViT-L/16, Llama-3-8B forward projections):
+//
+//   Y[M, N] = epilogue( A[M, K] · B[N, K]ᵀ )      (torch.nn.Linear: A = activations, B = weight)
+//
+// with the epilogues that otherwise cost an HBM pass each: + bias, + bias -> GELU (writing both
+// the pre-activation the backward needs and the activation), + residual (beta = 1 accumulate).
+//
+// Structure (gfx950, CDNA4): one 256 x BN block tile per CU (8 waves = 2 (M) x 4 (N), each wave a
+// 128 x BN/4 sub-tile = 8 x BN/64 MFMA accumulators of mfma_f32_16x16x32_bf16), BK = 64. Both
+// operands go global -> LDS with global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip); each
+// wave-instruction fills 8 full 128-B rows, the per-lane SOURCE address is pre-swizzled so the
+// lane-linear LDS image has the XOR-swizzled chunk order the ds_read_b128 fragment reads want
+// (conflict-free column-slice reads). Two LDS stages of 64 KB: the DMA of K-tile k+1 is issued
+// right after the barrier that retires tile k and has the whole 64-MFMA-per-wave compute of tile k
+// to land; one `s_waitcnt vmcnt(0)` + raw s_barrier per K-tile, nothing else drains the pipeline
+// (all LDS in one dynamic array, no other global loads in the loop). The MFMA computes the
+// transposed tile (B rows as the first operand), so a lane's four accumulators are four
+// consecutive output columns of one row: the C tile goes to LDS as 8-B writes and leaves as full
+// 16-B row chunks, where the epilogue math runs. Block ids are remapped XCD-contiguously: the
+// N tiles of one M panel (which share the A panel) and neighbouring panels sit in one XCD's L2.
+// Rows past M read a zero line and are not stored.
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include "common.h"
+#include "kernels/dev_utils.h"
+
+namespace xddp {
+namespace kernels {
+
+const uint16_t* zero_line(const at::Tensor& like);  // conv3x3.hip: 256 zero bytes per device
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+using dev::f32x4;
+using dev::u32x4;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int kBM = 256, kBK = 64, kWM = 2, kWN = 4, kThreads = 64 * kWM * kWN;
+
+enum Epi : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiResidual = 3 };
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ ((row >> 1) & 7)); }
+
+__device__ __forceinline__ float bf(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+template <int BN, int EPI>
+__global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A,
+                                                              const uint16_t* __restrict__ B,
+                                                              uint16_t* Y, uint16_t* __restrict__ Y2,
+                                                              const uint16_t* __restrict__ bias,
+                                                              const uint16_t* res, const uint16_t* __restrict__ zeros,
+                                                              int M, int N, int K, int ntiles, int64_t ldr) {
+  constexpr int NW = kThreads / 64;
+  constexpr int AI = kBM / 8 / NW, BI = BN / 8 / NW;  // DMA wave-instructions per stage (8 rows each)
+  static_assert(AI * NW * 8 == kBM && BI * NW * 8 == BN, "tile rows must split evenly over the waves");
+  constexpr int WTM = kBM / kWM, WTN = BN / kWN, TM = WTM / 16, TN = WTN / 16;
+  constexpr int STAGE = (kBM + BN) * 128;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / kWN, wn = wid % kWN;
+  const int wg = dev::xcd_remap(blockIdx.x, gridDim.x);
+  const int nt = wg % ntiles, mt = wg / ntiles;
+  const int n0 = nt * BN, m0 = mt * kBM;
+  const int pos = lane & 7;  // 16-B slot this lane fills in its 128-B LDS row
+  const int nk = K / kBK;
+
+  const uint16_t* asrc[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = (wid * AI + i) * 8 + (lane >> 3);
+    const int chunk = pos ^ ((row >> 1) & 7);
+    asrc[i] = m0 + row < M ? A + (int64_t)(m0 + row) * K + 8 * chunk : zeros + 8 * chunk;
+  }
+  const uint16_t* bsrc[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int row = (wid * BI + j) * 8 + (lane >> 3);
+    bsrc[j] = B + (int64_t)(n0 + row) * K + 8 * (pos ^ ((row >> 1) & 7));
+  }
+  // rows past M stay on the zero line (no advance)
+  bool a_live[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) a_live[i] = m0 + (wid * AI + i) * 8 + (lane >> 3) < M;
+
+  auto issue = [&](int kt, int buf) {
+    uint8_t* As = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const uint16_t* src = asrc[i] + (a_live[i] ? kt * kBK : 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + (wid * AI + i) * 1024), 16, 0, 0);
+    }
+    uint8_t* Bs = As + kBM * 128;
+#pragma unroll
+    for (int j = 0; j < BI; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[j] + kt * kBK), (lds_ptr_t)(Bs + (wid * BI + j) * 1024), 16,
+                                       0, 0);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt has landed for this wave; the barrier makes every wave's DMA visible and guarantees
+    // no wave still reads the stage the next DMA overwrites (it held tile kt - 1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    const uint8_t* As = smem + (kt & 1) * STAGE;
+    const uint8_t* Bs = As + kBM * 128;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ch = h * 4 + (lane >> 4);
+      bf16x8 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(As + swz(wm * WTM + i * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(Bs + swz(wn * WTN + j * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: fp32 -> bf16 C tile through LDS (rows padded 16 B), 16-B row chunks out ----
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave is done reading the stages
+  constexpr int CST = BN * 2 + 16;
+  uint8_t* Cs = smem;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wm * WTM + i * 16 + (lane & 15);
+      const int col = wn * WTN + j * 16 + (lane >> 4) * 4;
+      f32x4 v = acc[i][j];
+      if (EPI != kEpiNone && EPI != kEpiResidual) {  // bias in fp32 before the one rounding
+        const uint2 bb = *reinterpret_cast<const uint2*>(bias + n0 + col);
+        v[0] += bf(bb.x & 0xffffu);
+        v[1] += bf(bb.x >> 16);
+        v[2] += bf(bb.y & 0xffffu);
+        v[3] += bf(bb.y >> 16);
+      }
+      uint2 pk;
+      pk.x = dev::pack_bf16x2(v[0], v[1]);
+      pk.y = dev::pack_bf16x2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(Cs + row * CST + col * 2) = pk;
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  constexpr int CPR = BN / 8;
+  static_assert(kThreads % CPR == 0, "readout mapping needs a fixed chunk column per thread");
+  const int cc = tid % CPR;
+  const int rows_valid = min(kBM, M - m0);
+  u32x4 rb{};
+  if (EPI == kEpiResidual && bias) rb = *reinterpret_cast<const u32x4*>(bias + n0 + cc * 8);
+#pragma unroll 4
+  for (int q = tid; q < kBM * CPR; q += kThreads) {
+    const int row = q / CPR;
+    if (row >= rows_valid) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
+    const int64_t off = (int64_t)(m0 + row) * N + n0 + cc * 8;
+    if (EPI == kEpiBiasGelu) {
+      *reinterpret_cast<u32x4*>(Y + off) = v;  // pre-activation (the backward's dGELU input)
+      u32x4 g;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        g[e] = dev::pack_bf16x2(gelu_erf(bf(v[e] & 0xffffu)), gelu_erf(bf(v[e] >> 16)));
+      *reinterpret_cast<u32x4*>(Y2 + off) = g;
+    } else if (EPI == kEpiResidual) {
+      // y = res + (A·Bᵀ, already rounded to bf16 in the C tile) [+ bias]: one extra rounding of
+      // the product against addmm_'s single one (the residual term dominates the sum)
+      const u32x4 r = *reinterpret_cast<const u32x4*>(res + (int64_t)(m0 + row) * ldr + n0 + cc * 8);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float lo = bf(r[e] & 0xffffu) + bf(v[e] & 0xffffu), hi = bf(r[e] >> 16) + bf(v[e] >> 16);
+        if (bias) {
+          lo += bf(rb[e] & 0xffffu);
+          hi += bf(rb[e] >> 16);
+        }
+        v[e] = dev::pack_bf16x2(lo, hi);
+      }
+      *reinterpret_cast<u32x4*>(Y + off) = v;
+    } else {
+      *reinterpret_cast<u32x4*>(Y + off) = v;
+    }
+  }
+}
+
+template <int BN, int EPI>
+void launch_gemm(const at::Tensor& a, const at::Tensor& b, uint16_t* y, uint16_t* y2, const uint16_t* bias,
+                 const uint16_t* res, int64_t ldr, int M, int N, int K, hipStream_t stream) {
+  const int mtiles = (M + kBM - 1) / kBM, ntiles = N / BN;
+  const size_t lds = std::max<size_t>((size_t)2 * (kBM + BN) * 128, (size_t)kBM * (BN * 2 + 16));
+  static bool attr = false;
+  if (!attr) {
+    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI>), dim3(mtiles * ntiles), dim3(kThreads), lds, stream,
+                     reinterpret_cast<const uint16_t*>(a.data_ptr()), reinterpret_cast<const uint16_t*>(b.data_ptr()),
+                     y, y2, bias, res, zero_line(a), M, N, K, ntiles, ldr);
+  XDDP_HIP_CHECK(hipGetLastError());
+}
+
+// Tile width: 256 x 256 unless the 256 x 128 grid fills the CUs' last round better (one block
+// per CU: a 256 x 256 grid of 800 tiles on 256 CUs runs 4 rounds, the last 1/8 full).
+int pick_bn(int64_t M, int64_t N, int cus) {
+  if (const char* e = std::getenv("XDDP_GEMM_BN")) return std::atoi(e) == 128 || N % 256 ? 128 : 256;
+  if (N % 256) return 128;
+  const int64_t mt = (M + kBM - 1) / kBM;
+  const int64_t r256 = (mt * (N / 256) + cus - 1) / cus, r128 = (mt * (N / 128) + cus - 1) / cus;
+  // a 256 x 128 tile does half the work at ~1.15x the per-FLOP cost (more B traffic per MFMA)
+  return 2.0 * r256 <= 1.15 * r128 ? 256 : 128;
+}
+
+}  // namespace
+
+// a [M, K] bf16 (row-major, rows 16-B aligned), w [N, K] bf16 -> y [M, N] bf16 = a · wᵀ with
+// epilogue `epi`: 0 none, 1 + bias, 2 + bias then GELU (returns {pre-activation, activation}),
+// 3 + residual (y may be `out` = the residual itself: the in-place x += a·wᵀ of a pre-norm block;
+// + bias if given). K % 64 == 0, N % 128 == 0.
+std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                                int64_t epi, const c10::optional<at::Tensor>& residual,
+                                const c10::optional<at::Tensor>& out) {
+  TORCH_CHECK(a.is_cuda() && w.is_cuda() && a.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
+              "gemm_nt: bf16 CUDA operands expected");
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && a.size(1) == w.size(1) && a.stride(1) == 1 && a.stride(0) == a.size(1) &&
+                  w.is_contiguous(),
+              "gemm_nt: a [M, K] and w [N, K] must be contiguous with matching K");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(M > 0 && M < (int64_t(1) << 31) && K % 64 == 0 && K > 0 && N % 128 == 0 && N > 0,
+              "gemm_nt: needs K % 64 == 0 and N % 128 == 0");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "gemm_nt: 16-B aligned operands required");
+  TORCH_CHECK(epi >= 0 && epi <= 3, "gemm_nt: epi must be 0..3");
+  const bool has_bias = bias.has_value() && bias->defined();
+  if (has_bias)
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kBFloat16 && bias->numel() == N && bias->is_contiguous() &&
+                    reinterpret_cast<uintptr_t>(bias->data_ptr()) % 16 == 0,
+                "gemm_nt: bias must be a contiguous bf16 [N] vector");
+  TORCH_CHECK((epi != 1 && epi != 2) || has_bias, "gemm_nt: epilogues 1 and 2 need a bias");
+  at::Tensor res;
+  int64_t ldr = N;
+  if (epi == 3) {
+    TORCH_CHECK(residual.has_value() && residual->defined(), "gemm_nt: epilogue 3 needs a residual");
+    res = *residual;
+    TORCH_CHECK(res.scalar_type() == at::kBFloat16 && res.dim() == 2 && res.size(0) == M && res.size(1) == N &&
+                    res.stride(1) == 1 && res.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(res.data_ptr()) % 16 == 0,
+                "gemm_nt: residual must be bf16 [M, N] with unit column stride and 16-B aligned rows");
+    ldr = res.stride(0);
+  }
+  at::Tensor y;
+  if (out.has_value() && out->defined()) {
+    y = *out;
+    TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 2 && y.size(0) == M && y.size(1) == N && y.is_contiguous(),
+                "gemm_nt: out must be a contiguous bf16 [M, N] tensor");
+    TORCH_CHECK(epi != 3 || y.data_ptr() == res.data_ptr() || !(y.data_ptr() < (char*)res.data_ptr() + res.nbytes() &&
+                                                                  res.data_ptr() < (char*)y.data_ptr() + y.nbytes()),
+                "gemm_nt: out may alias the residual only exactly");
+  } else {
+    y = at::empty({M, N}, a.options());
+  }
+  at::Tensor y2 = epi == 2 ? at::empty({M, N}, a.options()) : at::Tensor();
+  auto stream = c10::hip::getCurrentHIPStream(a.device().index()).stream();
+  int cus = 256;
+  {
+    static int cached = 0;
+    if (!cached) {
+      int v = 0;
+      if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, a.device().index()) == hipSuccess && v > 0)
+        cached = v;
+      else
+        cached = 256;
+    }
+    cus = cached;
+  }
+  const int BN = pick_bn(M, N, cus);
+  auto* yp = reinterpret_cast<uint16_t*>(y.data_ptr());
+  auto* y2p = epi == 2 ? reinterpret_cast<uint16_t*>(y2.data_ptr()) : nullptr;
+  const auto* bp = has_bias ? reinterpret_cast<const uint16_t*>(bias->data_ptr()) : nullptr;
+  const auto* rp = epi == 3 ? reinterpret_cast<const uint16_t*>(res.data_ptr()) : nullptr;
+#define XDDP_GEMM(BN_)                                                                                 \
+  switch (epi) {                                                                                       \
+    case 0: launch_gemm<BN_, kEpiNone>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break;     \
+    case 1: launch_gemm<BN_, kEpiBias>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break;     \
+    case 2: launch_gemm<BN_, kEpiBiasGelu>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break; \
+    default: launch_gemm<BN_, kEpiResidual>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break; \
+  }
+  if (BN == 256) {
+    XDDP_GEMM(256)
+  } else {
+    XDDP_GEMM(128)
+  }
+#undef XDDP_GEMM
+  if (epi == 2) return {y, y2};
+  return {y};
+}
+
+}  // namespace kernels
+}  // namespace xddp

@@ -42,6 +42,9 @@ void bind_norm_kernels(py::module_& m) {
         py::arg("momentum"), py::arg("cumulative"), py::arg("eps"), py::arg("group_minor") = false);
   m.def("conv1x1_dma_forward", &conv1x1_dma_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"),
         py::arg("tile") = -1);
+  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,
+        py::arg("residual") = py::none(), py::arg("out") = py::none(),
+        "y = a @ w.T (bf16, MFMA LDS-DMA GEMM) with epilogue 0 none | 1 +bias | 2 +bias->GELU | 3 +residual");
   m.def("flash_attn_forward", &flash_attn_forward, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
         py::arg("scale"));
   m.def("flash_attn_backward", &flash_attn_backward, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),

@@ -1,0 +1,93 @@
+"""Workload for rocprofv3 --pmc passes over the round-2 kernels (VERDICT r2 "Next round" #7):
+3x3 implicit-GEMM forward / stride-1 dgrad, 3x3 patch weight gradient, stem conv forward / weight
+gradient, flash attention forward / backward (dK/dV with fused dQ), and the conv1 input-gradient
+GEMM with the BN-reduce epilogue (EPI). ResNet-50 / ViT-L/16 shapes at the bench batch.
+
+Each op runs CALLS times back to back between two marker kernels (an int16 add, a name nothing else
+in the workload launches); ``gpurun_out/pmc_r3_plan.json`` records, in launch order, the kernel-name
+pattern, the call count and the analytic FLOPs / unique HBM bytes of one call, so
+``scripts/pmc_summary.py`` can put each op's dispatches on the roofline.
+
+usage: python scripts/pmc_r3.py [--plan-out PATH]
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from distributeddataparallel_amd._native import load  # noqa: E402
+
+C = load()
+CALLS = 3
+cl = torch.channels_last
+plan = []
+_marker = torch.zeros(7, dtype=torch.int16, device="cuda")
+
+
+def bf(*shape, scale=1.0, fmt=cl):
+    t = (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16)
+    return t.contiguous(memory_format=fmt) if len(shape) == 4 else t.contiguous()
+
+
+def run(label, pattern, flops, nbytes, fn):
+    fn()  # warm (first-call allocations, tuning) — not part of the plan
+    torch.cuda.synchronize()
+    plan.append({"label": label, "pattern": pattern, "calls": CALLS, "flops": float(flops), "bytes": float(nbytes)})
+    _marker.add_(1)
+    for _ in range(CALLS):
+        fn()
+    _marker.add_(1)
+    torch.cuda.synchronize()
+
+
+B = 256
+# 3x3 forward (+ BN statistics epilogue) and the stride-1 input gradient (same kernel, rotated W)
+for cin, hw in ((64, 56), (128, 28), (256, 14)):
+    x, w = bf(B, cin, hw, hw), bf(cin, cin, 3, 3, scale=(9 * cin) ** -0.5)
+    m = B * hw * hw
+    fl, by = 2.0 * m * cin * 9 * cin, 2.0 * (2 * x.numel() + w.numel())
+    run(f"conv3x3 fwd C{cin} {hw}x{hw}", "conv3x3_fwd_kernel", fl, by, lambda: C.conv3x3_forward(x, w, 1, True))
+    wr = C.conv3x3_rot_weight(w)
+    run(f"conv3x3 dgrad C{cin} {hw}x{hw}", "conv3x3_fwd_kernel", fl, by, lambda: C.conv3x3_forward(x, wr, 1, False))
+    run(f"conv3x3 wgrad(patch) C{cin} {hw}x{hw}", "conv3x3_wgrad_kernel", fl, 2.0 * 2 * x.numel() + 4 * w.numel(),
+        lambda: C.conv3x3_wgrad_patch(x, x, 1, w))
+# stem 7x7/s2 (3 -> 64, 224 -> 112): forward with BN statistics, weight gradient
+xs = bf(B, 3, 224, 224)
+ws = bf(64, 3, 7, 7, scale=147 ** -0.5)
+ys, _ = C.stem_conv_forward(xs, ws)
+m = B * 112 * 112
+run("stem conv fwd", "stem_conv_fwd_kernel", 2.0 * m * 64 * 147, 2.0 * (xs.numel() + ys.numel()),
+    lambda: C.stem_conv_forward(xs, ws))
+run("stem conv wgrad", "stem_conv_wgrad_kernel", 2.0 * m * 64 * 147, 2.0 * (xs.numel() + ys.numel()),
+    lambda: C.stem_conv_wgrad(ys, xs, ws))
+# EPI: conv1 input gradient + identity gradient + ReLU mask + BN-backward reduce in the epilogue
+for hw, n, k in ((56, 256, 64), (28, 512, 128), (14, 1024, 256)):
+    dy = bf(B, k, hw, hw)
+    w = bf(k, n, 1, 1, scale=k ** -0.5)
+    add, y = bf(B, n, hw, hw), bf(B, n, hw, hw)
+    bits = torch.randint(0, 256, (y.numel() // 8,), device="cuda", dtype=torch.uint8)
+    mean = torch.zeros(n, device="cuda")
+    run(f"EPI dgrad N{n} K{k} {hw}x{hw}", "conv1x1_gemm_kernel", 2.0 * y.numel() * k,
+        2.0 * (dy.numel() + 3 * y.numel()) + bits.numel(),
+        lambda: C.conv1x1_gemm(dy, w, 1, None, False, None, True, add, y, bits, mean))
+# flash attention, ViT-L/16 (197 tokens, 16 heads x 64) at 64 images, and a Llama-like causal shape
+for (b, s, h, d, causal) in ((64, 197, 16, 64, False), (2, 4096, 32, 128, True)):
+    q, k, v = bf(b, s, h, d), bf(b, s, h, d), bf(b, s, h, d)
+    o, lse = C.flash_attn_forward(q, k, v, causal, d ** -0.5)
+    do = bf(b, s, h, d)
+    f = 0.5 if causal else 1.0
+    fl = 4.0 * b * h * s * s * d * f
+    run(f"flash fwd B{b} S{s} H{h} D{d}{' causal' if causal else ''}", "fa_fwd_kernel", fl, 2.0 * 4 * q.numel(),
+        lambda: C.flash_attn_forward(q, k, v, causal, d ** -0.5))
+    run(f"flash bwd B{b} S{s} H{h} D{d}{' causal' if causal else ''}", "fa_bwd_(dkdv|dq)_kernel", 2.5 * fl,
+        2.0 * 8 * q.numel(), lambda: C.flash_attn_backward(do, q, k, v, o, lse, causal, d ** -0.5))
+
+out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "pmc_r3_plan.json")
+if len(sys.argv) > 2 and sys.argv[1] == "--plan-out":
+    out = sys.argv[2]
+os.makedirs(os.path.dirname(out), exist_ok=True)
+with open(out, "w") as fh:
+    json.dump(plan, fh, indent=1)
+print(f"pmc workload done: {len(plan)} ops x {CALLS} calls", flush=True)

@@ -1,0 +1,67 @@
+"""Own transformer GEMM (csrc/kernels/gemm.hip: y = a · wᵀ on the LDS-DMA MFMA pipeline) against
+an fp32 torch reference of the same op: plain, + bias, + bias -> GELU (pre-activation and
+activation), + residual (in place, the pre-norm block's x += o · Woᵀ); M tails (rows past M read
+a zero line and are not stored), both tile widths (N % 256 and N % 128 only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _C():
+    from distributeddataparallel_amd._native import load
+
+    return load()
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("M,K,N", [(1, 64, 128), (100, 128, 256), (300, 192, 384), (513, 1024, 1024),
+                                   (12608 // 4, 1024, 3072), (2048, 4096, 1024)])
+def test_gemm_nt_plain_and_bias(M, K, N):
+    C = _C()
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
+    ref = a.float() @ w.float().t()
+    y = C.gemm_nt(a, w)[0]
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    assert _rel(y, ref) < 5e-3
+    yb = C.gemm_nt(a, w, b, 1)[0]
+    assert _rel(yb, ref + b.float()) < 5e-3
+
+
+@pytest.mark.parametrize("bn", ["128", "256"])
+def test_gemm_nt_gelu_and_residual(bn, monkeypatch):
+    monkeypatch.setenv("XDDP_GEMM_BN", bn)  # read per call: both tile widths on one shape
+    C = _C()
+    g = torch.Generator(device="cuda").manual_seed(7)
+    M, K, N = 777, 512, 1024
+    a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
+    h, act = C.gemm_nt(a, w, b, 2)
+    href = a.float() @ w.float().t() + b.float()
+    assert _rel(h, href) < 5e-3
+    # the activation is GELU of the stored (bf16) pre-activation
+    assert _rel(act, F.gelu(h.float())) < 5e-3
+    # residual: in place into x (x is the residual and the output), with and without a bias
+    x = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+    for bias in (None, b):
+        xr = x.float() + a.float() @ w.float().t() + (0 if bias is None else bias.float())
+        xx = x.clone()
+        out = C.gemm_nt(a, w, bias, 3, xx, xx)[0]
+        assert out.data_ptr() == xx.data_ptr()
+        assert _rel(xx, xr) < 5e-3
+
+
+def test_gemm_nt_rejects_bad_shapes():
+    C = _C()
+    a = torch.zeros(8, 100, device="cuda", dtype=torch.bfloat16)
+    w = torch.zeros(128, 100, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="K % 64"):
+        C.gemm_nt(a, w)
