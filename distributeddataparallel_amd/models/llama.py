@@ -18,6 +18,7 @@ import torch.nn.functional as F
 
 from ..ops.attention import flash_attention
 from ..ops.layer_norm import FusedRMSNorm
+from ..ops.linear import linear
 from ..ops.transformer import rope, rope_reference, swiglu
 
 __all__ = ["LlamaConfig", "Llama", "llama3_8b", "llama_tiny"]
@@ -58,25 +59,32 @@ class Attention(nn.Module):
         self.wv = nn.Linear(cfg.dim, self.kvh * self.hd, bias=False)
         self.wo = nn.Linear(self.h * self.hd, cfg.dim, bias=False)
 
-    def forward(self, x, cos, sin):
+    def forward(self, x, cos, sin, residual=None):
+        """Attention output; with ``residual`` (fused path) ``residual + attention`` (the skip
+        connection added in the o-projection GEMM's epilogue)."""
         B, S, _ = x.shape
         rot = rope if _fused() else rope_reference
         # rotate in the projection's [B, S, H, Dh] layout, then move heads forward for attention
+        if _fused():
+            # projections on the own GEMM (ops/linear.py); gfx950 flash attention in their
+            # [B, S, H, Dh] layout (GQA without materialised K/V repeats; output already in the
+            # o-projection's layout)
+            q = rot(linear(x, self.wq.weight).view(B, S, self.h, self.hd), cos, sin)
+            k = rot(linear(x, self.wk.weight).view(B, S, self.kvh, self.hd), cos, sin)
+            v = linear(x, self.wv.weight).view(B, S, self.kvh, self.hd)
+            o = flash_attention(q, k, v, causal=True)
+            return linear(o.reshape(B, S, -1), self.wo.weight, residual)
         q = rot(self.wq(x).view(B, S, self.h, self.hd), cos, sin)
         k = rot(self.wk(x).view(B, S, self.kvh, self.hd), cos, sin)
         v = self.wv(x).view(B, S, self.kvh, self.hd)
-        if _fused():
-            # gfx950 flash attention in the projections' [B, S, H, Dh] layout (GQA without
-            # materialised K/V repeats; output already in the o-projection's layout)
-            o = flash_attention(q, k, v, causal=True)
-            return self.wo(o.reshape(B, S, -1))
         q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
         if self.kvh != self.h:
             rep = self.h // self.kvh
             k = k.repeat_interleave(rep, dim=1)
             v = v.repeat_interleave(rep, dim=1)
         o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-        return self.wo(o.transpose(1, 2).reshape(B, S, -1))
+        out = self.wo(o.transpose(1, 2).reshape(B, S, -1))
+        return out if residual is None else residual + out
 
 
 class FeedForward(nn.Module):
@@ -86,10 +94,11 @@ class FeedForward(nn.Module):
         self.w2 = nn.Linear(cfg.ffn_dim, cfg.dim, bias=False)
         self.w3 = nn.Linear(cfg.dim, cfg.ffn_dim, bias=False)
 
-    def forward(self, x):
+    def forward(self, x, residual=None):
         if _fused():
-            return self.w2(swiglu(self.w1(x), self.w3(x)))
-        return self.w2(F.silu(self.w1(x)) * self.w3(x))
+            return linear(swiglu(linear(x, self.w1.weight), linear(x, self.w3.weight)), self.w2.weight, residual)
+        out = self.w2(F.silu(self.w1(x)) * self.w3(x))
+        return out if residual is None else residual + out
 
 
 class Block(nn.Module):
@@ -101,8 +110,8 @@ class Block(nn.Module):
         self.feed_forward = FeedForward(cfg)
 
     def forward(self, x, cos, sin):
-        x = x + self.attention(self.attention_norm(x), cos, sin)
-        return x + self.feed_forward(self.ffn_norm(x))
+        x = self.attention(self.attention_norm(x), cos, sin, residual=x)
+        return self.feed_forward(self.ffn_norm(x), residual=x)
 
 
 class Llama(nn.Module):
@@ -137,7 +146,7 @@ class Llama(nn.Module):
                 h = torch.utils.checkpoint.checkpoint(blk, h, cos, sin, use_reentrant=False)
             else:
                 h = blk(h, cos, sin)
-        return self.output(self.norm(h))
+        return linear(self.norm(h), self.output.weight) if _fused() else self.output(self.norm(h))
 
 
 def llama3_8b(**kw):

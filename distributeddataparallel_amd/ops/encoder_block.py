@@ -59,16 +59,24 @@ class _EncoderBlockFn(torch.autograd.Function):
         dh = D // heads
         scale = 1.0 / math.sqrt(dh)
         x2 = x.reshape(-1, D).contiguous()
+        own = _own_gemm(D, w_1.shape[0])
         y1, mean1, rstd1, xb = C.ln_forward(x2, ln1_w, ln1_b, eps1, False, b_o)
-        qkv = torch.addmm(b_qkv, y1, w_qkv.t())
+        qkv = C.gemm_nt(y1, w_qkv, b_qkv, 1)[0] if own else torch.addmm(b_qkv, y1, w_qkv.t())
         q5 = qkv.view(B, S, 3, heads, dh)
         o, lse = C.flash_attn_forward(q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], False, scale)
         o2 = o.view(-1, D)
-        x1 = xb.addmm_(o2, w_o.t())                      # x + b_o + o·W_oᵀ
+        if own:  # x + b_o + o·W_oᵀ, the residual added in the GEMM epilogue, in place
+            x1 = C.gemm_nt(o2, w_o, None, 3, xb, xb)[0]
+        else:
+            x1 = xb.addmm_(o2, w_o.t())
         y2, mean2, rstd2, x1b = C.ln_forward(x1, ln2_w, ln2_b, eps2, False, b_2)
-        h = torch.addmm(b_1, y2, w_1.t())
-        a = C.gelu_forward(h)
-        out = x1b.addmm_(a, w_2.t())                     # x1 + b_2 + a·W_2ᵀ
+        if own:  # fc1 + bias + GELU in one GEMM epilogue: h (for dGELU) and a = gelu(h)
+            h, a = C.gemm_nt(y2, w_1, b_1, 2)
+            out = C.gemm_nt(a, w_2, None, 3, x1b, x1b)[0]  # x1 + b_2 + a·W_2ᵀ
+        else:
+            h = torch.addmm(b_1, y2, w_1.t())
+            a = C.gelu_forward(h)
+            out = x1b.addmm_(a, w_2.t())
         ctx.save_for_backward(x2, ln1_w, mean1, rstd1, y1, w_qkv, b_qkv, qkv, o, lse, w_o, b_o, x1, ln2_w, mean2,
                               rstd2, y2, w_1, b_1, h, a, w_2, b_2)
         ctx.shape, ctx.heads, ctx.scale = (B, S, D), heads, scale
@@ -104,6 +112,14 @@ class _EncoderBlockFn(torch.autograd.Function):
         dx, dln1_w, dln1_b, _, _ = C.ln_backward(dy1, x2, ln1_w, mean1, rstd1, False, True, True, g1)
         return (dx.view(B, S, D), dln1_w, dln1_b, dw_qkv, db_qkv, dw_o, db_o, dln2_w, dln2_b, dw_1, db_1, dw_2, db_2,
                 None, None, None)
+
+
+def _own_gemm(D: int, hidden: int) -> bool:
+    """Forward projections on the own LDS-DMA MFMA GEMM (csrc/kernels/gemm.hip) with the bias,
+    bias+GELU and residual epilogues fused; XDDP_OWN_GEMM=0 keeps hipBLASLt (addmm) + the
+    separate GELU pass (A/B switch)."""
+    return (os.environ.get("XDDP_OWN_GEMM", "1") != "0" and D % 128 == 0 and hidden % 128 == 0
+            and (3 * D) % 128 == 0)
 
 
 def encoder_block(x: torch.Tensor, blk) -> torch.Tensor:

@@ -65,3 +65,22 @@ def test_gemm_nt_rejects_bad_shapes():
     w = torch.zeros(128, 100, device="cuda", dtype=torch.bfloat16)
     with pytest.raises(RuntimeError, match="K % 64"):
         C.gemm_nt(a, w)
+
+
+def test_own_linear_autograd_matches_fp32():
+    """ops/linear.py: forward on gemm_nt (with the residual epilogue), backward on hipBLASLt."""
+    from distributeddataparallel_amd.ops.linear import linear
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(2, 200, 512, device="cuda", generator=g).to(torch.bfloat16).requires_grad_(True)
+    w = (torch.randn(768, 512, device="cuda", generator=g) * 512 ** -0.5).to(torch.bfloat16).requires_grad_(True)
+    r = torch.randn(2, 200, 768, device="cuda", generator=g).to(torch.bfloat16).requires_grad_(True)
+    y = linear(x, w, r)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xf, wf, rf = (t.detach().float().requires_grad_(True) for t in (x, w, r))
+    yf = rf + xf @ wf.t()
+    yf.backward(dy.float())
+    assert _rel(y, yf) < 5e-3
+    for a, b in ((x.grad, xf.grad), (w.grad, wf.grad), (r.grad, rf.grad)):
+        assert _rel(a, b) < 1e-2
