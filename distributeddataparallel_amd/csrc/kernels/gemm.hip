@@ -28,9 +28,17 @@
 namespace xddp {
 namespace kernels {
 
-const uint16_t* zero_line(const at::Tensor& like);  // conv3x3.hip: 256 zero bytes per device
-
 namespace {
+
+// 256 zero bytes per device that rows past M read instead of branching; never freed (a static
+// tensor would be destroyed after the HIP runtime at exit)
+const uint16_t* gemm_zero_line(const at::Tensor& like) {
+  static at::Tensor* z[64] = {};
+  const int d = like.device().index();
+  TORCH_CHECK(d >= 0 && d < 64, "gemm_nt: device index out of range");
+  if (!z[d]) z[d] = new at::Tensor(at::zeros({128}, like.options().dtype(at::kBFloat16)));
+  return reinterpret_cast<const uint16_t*>(z[d]->data_ptr());
+}
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 using dev::f32x4;
@@ -208,7 +216,7 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, uint16_t* y, uint16_t
   }
   hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI>), dim3(mtiles * ntiles), dim3(kThreads), lds, stream,
                      reinterpret_cast<const uint16_t*>(a.data_ptr()), reinterpret_cast<const uint16_t*>(b.data_ptr()),
-                     y, y2, bias, res, zero_line(a), M, N, K, ntiles, ldr);
+                     y, y2, bias, res, gemm_zero_line(a), M, N, K, ntiles, ldr);
   XDDP_HIP_CHECK(hipGetLastError());
 }
 
