@@ -18,9 +18,11 @@
 // consecutive output columns of one row: the C tile goes to LDS as 8-B writes and leaves as full
 // 16-B row chunks, where the epilogue math runs. Block ids are remapped XCD-contiguously: the
 // N tiles of one M panel (which share the A panel) and neighbouring panels sit in one XCD's L2.
-// Rows past M read a zero line and are not stored.
+// Rows past M re-read row M - 1 and are not stored.
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
+
+#include <type_traits>
 
 #include "common.h"
 #include "kernels/dev_utils.h"
@@ -29,16 +31,6 @@ namespace xddp {
 namespace kernels {
 
 namespace {
-
-// 256 zero bytes per device that rows past M read instead of branching; never freed (a static
-// tensor would be destroyed after the HIP runtime at exit)
-const uint16_t* gemm_zero_line(const at::Tensor& like) {
-  static at::Tensor* z[64] = {};
-  const int d = like.device().index();
-  TORCH_CHECK(d >= 0 && d < 64, "gemm_nt: device index out of range");
-  if (!z[d]) z[d] = new at::Tensor(at::zeros({128}, like.options().dtype(at::kBFloat16)));
-  return reinterpret_cast<const uint16_t*>(z[d]->data_ptr());
-}
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 using dev::f32x4;
@@ -54,15 +46,16 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 *
 __device__ __forceinline__ float bf(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
-template <int BN, int EPI>
+template <int BN, int EPI, int PH>
 __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A,
                                                               const uint16_t* __restrict__ B,
                                                               uint16_t* Y, uint16_t* __restrict__ Y2,
                                                               const uint16_t* __restrict__ bias,
-                                                              const uint16_t* res, const uint16_t* __restrict__ zeros,
+                                                              const uint16_t* res,
                                                               int M, int N, int K, int ntiles, int64_t ldr) {
   constexpr int NW = kThreads / 64;
   constexpr int AI = kBM / 8 / NW, BI = BN / 8 / NW;  // DMA wave-instructions per stage (8 rows each)
+  static_assert(NW == 8, "the DMA row mapping assumes 8 waves (row = (w + 8 i) * 8 + lane / 8)");
   static_assert(AI * NW * 8 == kBM && BI * NW * 8 == BN, "tile rows must split evenly over the waves");
   constexpr int WTM = kBM / kWM, WTN = BN / kWN, TM = WTM / 16, TN = WTN / 16;
   constexpr int STAGE = (kBM + BN) * 128;
@@ -75,36 +68,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   const int pos = lane & 7;  // 16-B slot this lane fills in its 128-B LDS row
   const int nk = K / kBK;
 
-  const uint16_t* asrc[AI];
-#pragma unroll
-  for (int i = 0; i < AI; ++i) {
-    const int row = (wid * AI + i) * 8 + (lane >> 3);
-    const int chunk = pos ^ ((row >> 1) & 7);
-    asrc[i] = m0 + row < M ? A + (int64_t)(m0 + row) * K + 8 * chunk : zeros + 8 * chunk;
-  }
-  const uint16_t* bsrc[BI];
-#pragma unroll
-  for (int j = 0; j < BI; ++j) {
-    const int row = (wid * BI + j) * 8 + (lane >> 3);
-    bsrc[j] = B + (int64_t)(n0 + row) * K + 8 * (pos ^ ((row >> 1) & 7));
-  }
-  // rows past M stay on the zero line (no advance)
-  bool a_live[AI];
-#pragma unroll
-  for (int i = 0; i < AI; ++i) a_live[i] = m0 + (wid * AI + i) * 8 + (lane >> 3) < M;
-
+  // DMA sources: lane l of wave w fills 16-B slot (l & 7) of rows (w*AI + i)*8 + (l >> 3); the
+  // offsets are recomputed per issue from two per-lane values (few live VGPRs: the 4-phase loop
+  // needs ~224 for accumulators and fragments). Rows past M re-read row M - 1 (never stored).
+  const int drow = wid * 8 + (lane >> 3);                    // + i * 64 (A, i < AI) / j * 64 (B)
+  const int dchunk = 8 * (pos ^ ((drow >> 1) & 7));          // (row >> 1) & 7 is the same for row + 64 i
   auto issue = [&](int kt, int buf) {
     uint8_t* As = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
-      const uint16_t* src = asrc[i] + (a_live[i] ? kt * kBK : 0);
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + (wid * AI + i) * 1024), 16, 0, 0);
+      const int row = min(m0 + drow + i * 64, M - 1);
+      const uint16_t* src = A + (uint32_t)row * (uint32_t)K + (uint32_t)(dchunk + kt * kBK);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + (wid * 8 + i * 64) * 128), 16, 0, 0);
     }
     uint8_t* Bs = As + kBM * 128;
 #pragma unroll
-    for (int j = 0; j < BI; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(bsrc[j] + kt * kBK), (lds_ptr_t)(Bs + (wid * BI + j) * 1024), 16,
-                                       0, 0);
+    for (int j = 0; j < BI; ++j) {
+      const uint16_t* src = B + (uint32_t)(n0 + drow + j * 64) * (uint32_t)K + (uint32_t)(dchunk + kt * kBK);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(Bs + (wid * 8 + j * 64) * 128), 16, 0, 0);
+    }
   };
 
   f32x4 acc[TM][TN];
@@ -113,30 +95,145 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue(0, 0);
-  for (int kt = 0; kt < nk; ++kt) {
-    // tile kt has landed for this wave; the barrier makes every wave's DMA visible and guarantees
-    // no wave still reads the stage the next DMA overwrites (it held tile kt - 1)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-    const uint8_t* As = smem + (kt & 1) * STAGE;
-    const uint8_t* Bs = As + kBM * 128;
+  if (PH == 0) {
+    // 2-phase: one barrier per K-tile, all fragments of the tile read after it
+    issue(0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      // tile kt has landed for this wave; the barrier makes every wave's DMA visible and
+      // guarantees no wave still reads the stage the next DMA overwrites (it held tile kt - 1)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+      const uint8_t* As = smem + (kt & 1) * STAGE;
+      const uint8_t* Bs = As + kBM * 128;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int ch = h * 4 + (lane >> 4);
-      bf16x8 a[TM], b[TN];
+      for (int h = 0; h < 2; ++h) {
+        const int ch = h * 4 + (lane >> 4);
+        bf16x8 a[TM], b[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        a[i] = *reinterpret_cast<const bf16x8*>(As + swz(wm * WTM + i * 16 + (lane & 15), ch));
+        for (int i = 0; i < TM; ++i)
+          a[i] = *reinterpret_cast<const bf16x8*>(As + swz(wm * WTM + i * 16 + (lane & 15), ch));
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(Bs + swz(wn * WTN + j * 16 + (lane & 15), ch));
+        for (int j = 0; j < TN; ++j)
+          b[j] = *reinterpret_cast<const bf16x8*>(Bs + swz(wn * WTN + j * 16 + (lane & 15), ch));
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      }
     }
+  } else {
+    // 4-phase: each K-tile is 4 phases, one per quadrant (A half x B half) of the wave's output,
+    // 16 MFMAs each; the fragments of the next phase are read while the current phase's MFMAs
+    // run, so the MFMA pipe never waits on LDS. The phase order alternates between even and odd
+    // K-tiles so the last phase of a tile and the first of the next use different fragment
+    // registers: even (A0,B0) (A0,B1) (A1,B1) (A1,B0), odd (A0,B1) (A0,B0) (A1,B0) (A1,B1).
+    // One barrier per K-tile, between phases 1 and 2: by then this wave's reads of the tile's
+    // stage are done (lgkmcnt(0)) and its DMA of tile t+1 (issued after the previous tile's
+    // barrier, four phases ago) has landed (vmcnt(0) - nothing else is in flight); after it the
+    // DMA of tile t+2 goes into this tile's stage and phases 2-3 read the first fragments of t+1.
+    constexpr int HA = TM / 2, HB = TN / 2;
+    static_assert(HB >= 1, "B halves need at least one 16-column fragment");
+    bf16x8 fa0[2][HA], fa1[2][HA], fb0[2][HB], fb1[2][HB];  // [k-half][fragment]
+    // fragment rows of a wave are row0 + 16 i: the XOR term ((row >> 1) & 7) is the same for all
+    // of them, so each k-half needs ONE per-lane byte offset; the rest is an immediate
+    const int ra = wm * WTM + (lane & 15), rb = wn * WTN + (lane & 15);
+    uint32_t a_lds[2], b_lds[2];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      a_lds[kh] = ra * 128 + 16 * ((kh * 4 + (lane >> 4)) ^ ((ra >> 1) & 7));
+      b_lds[kh] = kBM * 128 + rb * 128 + 16 * ((kh * 4 + (lane >> 4)) ^ ((rb >> 1) & 7));
+    }
+    auto ldA = [&](bf16x8 (&f)[2][HA], int half, int buf) {
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < HA; ++i)
+          f[kh][i] = *reinterpret_cast<const bf16x8*>(smem + buf * STAGE + a_lds[kh] + (half * HA + i) * 16 * 128);
+    };
+    auto ldB = [&](bf16x8 (&f)[2][HB], int half, int buf) {
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int j = 0; j < HB; ++j)
+          f[kh][j] = *reinterpret_cast<const bf16x8*>(smem + buf * STAGE + b_lds[kh] + (half * HB + j) * 16 * 128);
+    };
+    auto mma = [&](const bf16x8 (&a)[2][HA], auto ah, const bf16x8 (&b)[2][HB], auto bh) {
+      constexpr int AH = decltype(ah)::value, BHV = decltype(bh)::value;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < HA; ++i)
+#pragma unroll
+          for (int j = 0; j < HB; ++j)
+            acc[AH * HA + i][BHV * HB + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[kh][j], a[kh][i], acc[AH * HA + i][BHV * HB + j], 0, 0, 0);
+    };
+    // One phase = the fragment reads for the NEXT phase interleaved into this phase's MFMAs,
+    // MFMA first: the wait the compiler puts before the first MFMA then covers only the reads of
+    // the previous phase (whose MFMAs hid them), never the ones just issued. sched_barrier(0)
+    // keeps every instruction inside its phase.
+    auto interleave = [&](auto nld) {
+      constexpr int NLD = decltype(nld)::value, NM = 2 * HA * HB;
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // one MFMA (waits for this phase's fragments)
+      __builtin_amdgcn_sched_group_barrier(0x100, NLD, 0);     // the next phase's reads
+      __builtin_amdgcn_sched_group_barrier(0x008, NM - 1, 0);  // the rest of the MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    using LA = std::integral_constant<int, 2 * HA>;  // reads of an A half (both k-halves)
+    using LB = std::integral_constant<int, 2 * HB>;
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    // Branch-free (nk is even: the host sends odd K-tile counts to the 2-phase loop): a wait
+    // counter cannot be tracked through a conditional load (the compiler then waits for
+    // everything), so the last tiles re-read a valid stage and re-stage the last K-tile instead of
+    // skipping; those values are never used.
+    auto sync = [&](int t) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      issue(min(t + 2, nk - 1), t & 1);
+    };
+    issue(0, 0);
+    issue(min(1, nk - 1), 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AI + BI) : "memory");  // tile 0 landed, tile 1 in flight
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    ldA(fa0, 0, 0);
+    ldB(fb0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    for (int t = 0; t < nk; t += 2) {
+      // even tile t (stage 0): enters with A0, B0 of t
+      ldB(fb1, 1, 0);
+      mma(fa0, I0{}, fb0, I0{});
+      interleave(LB{});
+      ldA(fa1, 1, 0);
+      mma(fa0, I0{}, fb1, I1{});
+      interleave(LA{});
+      sync(t);
+      __builtin_amdgcn_sched_barrier(0);
+      ldA(fa0, 0, 1);  // A0 of t + 1
+      mma(fa1, I1{}, fb1, I1{});
+      interleave(LA{});
+      ldB(fb1, 1, 1);  // B1 of t + 1
+      mma(fa1, I1{}, fb0, I0{});
+      interleave(LB{});
+      // odd tile t + 1 (stage 1): enters with A0, B1 of t + 1
+      ldB(fb0, 0, 1);
+      mma(fa0, I0{}, fb1, I1{});
+      interleave(LB{});
+      ldA(fa1, 1, 1);
+      mma(fa0, I0{}, fb0, I0{});
+      interleave(LA{});
+      sync(t + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      ldA(fa0, 0, 0);  // A0 of t + 2
+      mma(fa1, I1{}, fb0, I0{});
+      interleave(LA{});
+      ldB(fb0, 0, 0);  // B0 of t + 2
+      mma(fa1, I1{}, fb1, I1{});
+      interleave(LB{});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-stage DMAs land before the C tile reuses LDS
   }
 
   // ---- epilogue: fp32 -> bf16 C tile through LDS (rows padded 16 B), 16-B row chunks out ----
@@ -203,20 +300,20 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   }
 }
 
-template <int BN, int EPI>
+template <int BN, int EPI, int PH = 1>
 void launch_gemm(const at::Tensor& a, const at::Tensor& b, uint16_t* y, uint16_t* y2, const uint16_t* bias,
                  const uint16_t* res, int64_t ldr, int M, int N, int K, hipStream_t stream) {
   const int mtiles = (M + kBM - 1) / kBM, ntiles = N / BN;
   const size_t lds = std::max<size_t>((size_t)2 * (kBM + BN) * 128, (size_t)kBM * (BN * 2 + 16));
   static bool attr = false;
   if (!attr) {
-    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI>,
+    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI, PH>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI>), dim3(mtiles * ntiles), dim3(kThreads), lds, stream,
+  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI, PH>), dim3(mtiles * ntiles), dim3(kThreads), lds, stream,
                      reinterpret_cast<const uint16_t*>(a.data_ptr()), reinterpret_cast<const uint16_t*>(b.data_ptr()),
-                     y, y2, bias, res, gemm_zero_line(a), M, N, K, ntiles, ldr);
+                     y, y2, bias, res, M, N, K, ntiles, ldr);
   XDDP_HIP_CHECK(hipGetLastError());
 }
 
@@ -303,6 +400,13 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
     case 1: launch_gemm<BN_, kEpiBias>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break;     \
     case 2: launch_gemm<BN_, kEpiBiasGelu>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break; \
     default: launch_gemm<BN_, kEpiResidual>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break; \
+  }
+  const char* pe = std::getenv("XDDP_GEMM_PIPE");
+  if ((pe && std::atoi(pe) == 0) || (K / 64) % 2) {
+    if (BN == 256) launch_gemm<256, kEpiNone, 0>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream);
+    else launch_gemm<128, kEpiNone, 0>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream);
+    TORCH_CHECK(epi == 0, "gemm_nt: the 2-phase loop (odd K/64, or XDDP_GEMM_PIPE=0) supports the plain epilogue only");
+    return {y};
   }
   if (BN == 256) {
     XDDP_GEMM(256)

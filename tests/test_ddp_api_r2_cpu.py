@@ -421,13 +421,31 @@ def _w_overlapped_optimizer(rank, world):
     d2 = xddp.DDP(m2)
     d1.register_overlapped_optimizer(o1 := FusedAdamW(m1.parameters(), lr=1e-2, weight_decay=0.1))
     o2 = FusedAdamW(m2.parameters(), lr=1e-2, weight_decay=0.1)
+    # event log: every bucket's update is issued right after its own all-reduce, so the updates of
+    # all earlier buckets are already issued (on GPU: running on the side stream) while the LAST
+    # bucket's all-reduce — the exposed tail — is in flight
+    log = []
+    pg = d1.process_group
+    orig_ar, orig_step = pg.allreduce, o1.step_params
+    pg.allreduce = lambda t, *a, **k: (log.append(("ar", t.numel())), orig_ar(t, *a, **k))[1]
+    o1.step_params = lambda ps, gs: (log.append(("step", sum(p.numel() for p in ps))), orig_step(ps, gs))[1]
     for x, y in _batches(1, 4, per_rank=4, seed=90 + rank):
         o1.zero_grad()
+        log.clear()
         F.cross_entropy(d1(x), y).backward()  # stepped per bucket inside backward
         o2.zero_grad()
         F.cross_entropy(d2(x), y).backward()
         o2.step()
+    pg.allreduce, o1.step_params = orig_ar, orig_step
     _assert_params_equal(m1, m2)
+    nb = len(d1.reducer.bucket_sizes_bytes())
+    assert nb >= 2
+    ars = [i for i, e in enumerate(log) if e[0] == "ar"]
+    steps = [i for i, e in enumerate(log) if e[0] == "step"]
+    assert len(ars) == nb and len(steps) == nb, log
+    for b in range(nb):  # bucket b steps after its all-reduce, before the next bucket's
+        assert ars[b] < steps[b] and (b + 1 == nb or steps[b] < ars[b + 1]), log
+    assert all(s < ars[-1] for s in steps[:-1])  # every other update precedes the tail all-reduce
 
 
 def test_overlapped_optimizer_matches_step_after_backward():

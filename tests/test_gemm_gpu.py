@@ -84,3 +84,19 @@ def test_own_linear_autograd_matches_fp32():
     assert _rel(y, yf) < 5e-3
     for a, b in ((x.grad, xf.grad), (w.grad, wf.grad), (r.grad, rf.grad)):
         assert _rel(a, b) < 1e-2
+
+
+@pytest.mark.parametrize("K", [128, 1024])
+def test_gemm_nt_pipelines_agree(K, monkeypatch):
+    """The 4-phase K loop (even K/64) and the 2-phase loop (XDDP_GEMM_PIPE=0, and every odd K/64)
+    compute the same product (bitwise: same MFMA order per accumulator)."""
+    C = _C()
+    g = torch.Generator(device="cuda").manual_seed(K)
+    M, N = 1000, 512
+    a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    y4 = C.gemm_nt(a, w)[0]
+    monkeypatch.setenv("XDDP_GEMM_PIPE", "0")
+    y2 = C.gemm_nt(a, w)[0]
+    assert _rel(y4, a.float() @ w.float().t()) < 5e-3
+    assert torch.equal(y4, y2)
