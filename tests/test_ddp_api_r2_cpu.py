@@ -417,7 +417,7 @@ def _w_overlapped_optimizer(rank, world):
     from distributeddataparallel_amd.optim import FusedAdamW
 
     m1, m2 = _mlp(), _mlp()
-    d1 = xddp.DDP(m1, bucket_cap_mb=0.001)  # several buckets
+    d1 = xddp.DDP(m1, bucket_cap_mb=0.001, first_bucket_cap_mb=0.001)  # several buckets
     d2 = xddp.DDP(m2)
     d1.register_overlapped_optimizer(o1 := FusedAdamW(m1.parameters(), lr=1e-2, weight_decay=0.1))
     o2 = FusedAdamW(m2.parameters(), lr=1e-2, weight_decay=0.1)
