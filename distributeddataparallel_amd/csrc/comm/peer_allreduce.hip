@@ -35,6 +35,8 @@
 #include <hip/hip_fp16.h>
 #include <torch/extension.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -336,7 +338,13 @@ PeerAllReduce::PeerAllReduce(std::shared_ptr<Store> store, int rank, int size, i
   *impl_->status_host = 0;
   XDDP_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&impl_->status_dev), impl_->status_host, 0));
   impl_->one.open(store, "1", rank, size, kPeerMaxBlocks, capacity);
-  if (two_shot_capacity > 0) impl_->two.open(store, "2", rank, size, kPeerTwoShotBlocks, two_shot_capacity);
+  if (two_shot_capacity > 0) {
+    // XDDP_PEER_TWO_SHOT_BLOCKS: workgroups of the two-shot grid (8..256; fewer = fewer waves
+    // resident while a launch waits for its peers)
+    int nb = kPeerTwoShotBlocks;
+    if (const char* e = std::getenv("XDDP_PEER_TWO_SHOT_BLOCKS")) nb = std::max(8, std::min(kPeerTwoShotBlocks, std::atoi(e)));
+    impl_->two.open(store, "2", rank, size, nb, two_shot_capacity);
+  }
   int khz = 0;
   XDDP_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
   const char* t = std::getenv("XDDP_PEER_TIMEOUT_MS");

@@ -10,10 +10,11 @@
 // operands go global -> LDS with global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip); each
 // wave-instruction fills 8 full 128-B rows, the per-lane SOURCE address is pre-swizzled so the
 // lane-linear LDS image has the XOR-swizzled chunk order the ds_read_b128 fragment reads want
-// (conflict-free column-slice reads). Two LDS stages of 64 KB: the DMA of K-tile k+1 is issued
-// right after the barrier that retires tile k and has the whole 64-MFMA-per-wave compute of tile k
-// to land; one `s_waitcnt vmcnt(0)` + raw s_barrier per K-tile, nothing else drains the pipeline
-// (all LDS in one dynamic array, no other global loads in the loop). The MFMA computes the
+// (conflict-free column-slice reads). Two LDS stages of 64 KB; each K-tile runs as four
+// 16-MFMA phases whose fragment reads are issued one phase ahead, and the DMA of tile k+2 goes
+// out at the one `s_waitcnt vmcnt(0)` + raw s_barrier of tile k, halfway through it (details at
+// the loop); nothing else drains the pipeline (all LDS in one dynamic array, no other global
+// loads in the loop). The MFMA computes the
 // transposed tile (B rows as the first operand), so a lane's four accumulators are four
 // consecutive output columns of one row: the C tile goes to LDS as 8-B writes and leaves as full
 // 16-B row chunks, where the epilogue math runs. Block ids are remapped XCD-contiguously: the
@@ -41,12 +42,11 @@ constexpr int kBM = 256, kBK = 64, kWM = 2, kWN = 4, kThreads = 64 * kWM * kWN;
 
 enum Epi : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiResidual = 3 };
 
-__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ ((row >> 1) & 7)); }
 
 __device__ __forceinline__ float bf(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
-template <int BN, int EPI, int PH>
+template <int BN, int EPI>
 __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A,
                                                               const uint16_t* __restrict__ B,
                                                               uint16_t* Y, uint16_t* __restrict__ Y2,
@@ -95,35 +95,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (PH == 0) {
-    // 2-phase: one barrier per K-tile, all fragments of the tile read after it
-    issue(0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-      // tile kt has landed for this wave; the barrier makes every wave's DMA visible and
-      // guarantees no wave still reads the stage the next DMA overwrites (it held tile kt - 1)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-      const uint8_t* As = smem + (kt & 1) * STAGE;
-      const uint8_t* Bs = As + kBM * 128;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int ch = h * 4 + (lane >> 4);
-        bf16x8 a[TM], b[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          a[i] = *reinterpret_cast<const bf16x8*>(As + swz(wm * WTM + i * 16 + (lane & 15), ch));
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          b[j] = *reinterpret_cast<const bf16x8*>(Bs + swz(wn * WTN + j * 16 + (lane & 15), ch));
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-      }
-    }
-  } else {
+  {
     // 4-phase: each K-tile is 4 phases, one per quadrant (A half x B half) of the wave's output,
     // 16 MFMAs each; the fragments of the next phase are read while the current phase's MFMAs
     // run, so the MFMA pipe never waits on LDS. The phase order alternates between even and odd
@@ -185,23 +157,30 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
     using LB = std::integral_constant<int, 2 * HB>;
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
-    // Branch-free (nk is even: the host sends odd K-tile counts to the 2-phase loop): a wait
-    // counter cannot be tracked through a conditional load (the compiler then waits for
-    // everything), so the last tiles re-read a valid stage and re-stage the last K-tile instead of
-    // skipping; those values are never used.
+    // The loop runs tile PAIRS and is branch-free: a wait counter cannot be tracked through a
+    // conditional load (the compiler then waits for everything), so the last tiles re-read a
+    // valid stage and re-stage the last K-tile instead of skipping; those values are never used.
+    // An odd tile count gets a zero tile in front (virtual tile 0 = zeros written to stage 0, real
+    // tile k = virtual k + 1): its MFMAs add exact zeros, and no tail code raises the register
+    // pressure of the loop.
+    const int odd = nk & 1, nv = nk + odd;
     auto sync = [&](int t) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      issue(min(t + 2, nk - 1), t & 1);
+      issue(min(t + 2, nv - 1) - odd, t & 1);
     };
-    issue(0, 0);
-    issue(min(1, nk - 1), 1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AI + BI) : "memory");  // tile 0 landed, tile 1 in flight
+    if (odd) {
+      for (int q = tid; q < STAGE / 16; q += kThreads) reinterpret_cast<u32x4*>(smem)[q] = u32x4{0u, 0u, 0u, 0u};
+    } else {
+      issue(0, 0);
+    }
+    issue(1 - odd, 1);  // virtual tile 1: real tile 1 (even count) / 0 (odd count)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AI + BI) : "memory");  // stage 0 ready, stage 1 in flight
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     ldA(fa0, 0, 0);
     ldB(fb0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
-    for (int t = 0; t < nk; t += 2) {
+    for (int t = 0; t < nv; t += 2) {
       // even tile t (stage 0): enters with A0, B0 of t
       ldB(fb1, 1, 0);
       mma(fa0, I0{}, fb0, I0{});
@@ -300,18 +279,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   }
 }
 
-template <int BN, int EPI, int PH = 1>
+template <int BN, int EPI>
 void launch_gemm(const at::Tensor& a, const at::Tensor& b, uint16_t* y, uint16_t* y2, const uint16_t* bias,
                  const uint16_t* res, int64_t ldr, int M, int N, int K, hipStream_t stream) {
   const int mtiles = (M + kBM - 1) / kBM, ntiles = N / BN;
   const size_t lds = std::max<size_t>((size_t)2 * (kBM + BN) * 128, (size_t)kBM * (BN * 2 + 16));
   static bool attr = false;
   if (!attr) {
-    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI, PH>,
+    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI, PH>), dim3(mtiles * ntiles), dim3(kThreads), lds, stream,
+  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI>), dim3(mtiles * ntiles), dim3(kThreads), lds, stream,
                      reinterpret_cast<const uint16_t*>(a.data_ptr()), reinterpret_cast<const uint16_t*>(b.data_ptr()),
                      y, y2, bias, res, M, N, K, ntiles, ldr);
   XDDP_HIP_CHECK(hipGetLastError());
@@ -400,13 +379,6 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
     case 1: launch_gemm<BN_, kEpiBias>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break;     \
     case 2: launch_gemm<BN_, kEpiBiasGelu>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break; \
     default: launch_gemm<BN_, kEpiResidual>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break; \
-  }
-  const char* pe = std::getenv("XDDP_GEMM_PIPE");
-  if ((pe && std::atoi(pe) == 0) || (K / 64) % 2) {
-    if (BN == 256) launch_gemm<256, kEpiNone, 0>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream);
-    else launch_gemm<128, kEpiNone, 0>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream);
-    TORCH_CHECK(epi == 0, "gemm_nt: the 2-phase loop (odd K/64, or XDDP_GEMM_PIPE=0) supports the plain epilogue only");
-    return {y};
   }
   if (BN == 256) {
     XDDP_GEMM(256)

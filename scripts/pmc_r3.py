@@ -1,7 +1,8 @@
 """Workload for rocprofv3 --pmc passes over the round-2 kernels (VERDICT r2 "Next round" #7):
 3x3 implicit-GEMM forward / stride-1 dgrad, 3x3 patch weight gradient, stem conv forward / weight
 gradient, flash attention forward / backward (dK/dV with fused dQ), and the conv1 input-gradient
-GEMM with the BN-reduce epilogue (EPI). ResNet-50 / ViT-L/16 shapes at the bench batch.
+GEMM with the BN-reduce epilogue (EPI), and the transformer GEMM (gemm_nt) beside hipBLASLt.
+ResNet-50 / ViT-L/16 / Llama-3-8B shapes at the bench batch.
 
 Each op runs CALLS times back to back between two marker kernels (an int16 add, a name nothing else
 in the workload launches); ``gpurun_out/pmc_r3_plan.json`` records, in launch order, the kernel-name
@@ -74,15 +75,28 @@ for hw, n, k in ((56, 256, 64), (28, 512, 128), (14, 1024, 256)):
         lambda: C.conv1x1_gemm(dy, w, 1, None, False, None, True, add, y, bits, mean))
 # flash attention, ViT-L/16 (197 tokens, 16 heads x 64) at 64 images, and a Llama-like causal shape
 for (b, s, h, d, causal) in ((64, 197, 16, 64, False), (2, 4096, 32, 128, True)):
-    q, k, v = bf(b, s, h, d), bf(b, s, h, d), bf(b, s, h, d)
+    nc = torch.contiguous_format  # [B, S, H, D] row-major (channels_last would move D)
+    q, k, v = bf(b, s, h, d, fmt=nc), bf(b, s, h, d, fmt=nc), bf(b, s, h, d, fmt=nc)
     o, lse = C.flash_attn_forward(q, k, v, causal, d ** -0.5)
-    do = bf(b, s, h, d)
+    do = bf(b, s, h, d, fmt=nc)
     f = 0.5 if causal else 1.0
     fl = 4.0 * b * h * s * s * d * f
     run(f"flash fwd B{b} S{s} H{h} D{d}{' causal' if causal else ''}", "fa_fwd_kernel", fl, 2.0 * 4 * q.numel(),
         lambda: C.flash_attn_forward(q, k, v, causal, d ** -0.5))
     run(f"flash bwd B{b} S{s} H{h} D{d}{' causal' if causal else ''}", "fa_bwd_(dkdv|dq)_kernel", 2.5 * fl,
         2.0 * 8 * q.numel(), lambda: C.flash_attn_backward(do, q, k, v, o, lse, causal, d ** -0.5))
+
+# the transformer GEMM (own LDS-DMA MFMA kernel) next to hipBLASLt on the same operands
+for name, M, K, N in (("8192^3", 8192, 8192, 8192), ("vit fc1", 12608, 1024, 4096), ("llama down", 4096, 14336, 4096)):
+    a, w = bf(M, K), bf(N, K, scale=K ** -0.5)
+    fl, by = 2.0 * M * N * K, 2.0 * (M * K + N * K + M * N)
+    run(f"gemm_nt {name}", "gemm_nt_kernel", fl, by, lambda: C.gemm_nt(a, w))
+    run(f"hipBLASLt {name}", "Cijk", fl, by, lambda: torch.mm(a, w.t()))
+    if name == "vit fc1":
+        bias = bf(N)
+        run(f"gemm_nt {name} +bias+GELU", "gemm_nt_kernel", fl, by + 2.0 * M * N,
+            lambda: C.gemm_nt(a, w, bias, 2))
+    del a, w
 
 out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "pmc_r3_plan.json")
 if len(sys.argv) > 2 and sys.argv[1] == "--plan-out":

@@ -12,7 +12,8 @@ Columns: time per call; achieved TF/s from the analytic FLOPs; MFMA FLOPs issued
 (SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512) vs analytic; LDS bank-conflict cycles / LDS-active cycles;
 HBM traffic (2 x FETCH_SIZE + WRITE_SIZE, KB counters; gfx950 FETCH_SIZE counts half the bytes
 of wide reads) and its rate; arithmetic intensity and the
-fraction of the roofline bound min(peak, AI x HBM) reached.
+fraction of the roofline bound min(peak, AI x HBM) reached; MFMA-busy and LDS-busy cycles per
+CU-cycle (GRBM_GUI_ACTIVE x 32 CUs per XCD; raw hardware ratios, not calibrated against a peak).
 """
 import argparse
 import csv
@@ -86,7 +87,7 @@ def main():
     lines = ["# r3 PMC roofline (1x MI355X, rocprofv3; per call = op total over its dispatches / calls)",
              f"# peaks: {PEAK_TF:.0f} TF/s dense bf16 MFMA, {HBM_TBS} TB/s HBM streaming",
              f"{'op':38s} {'us':>8s} {'TF/s':>7s} {'%pk':>5s} {'mfmaF/anl':>9s} {'ldsConf':>7s} "
-             f"{'HBM MB':>8s} {'TB/s':>5s} {'AI':>6s} {'%roof':>6s}  bound"]
+             f"{'HBM MB':>8s} {'TB/s':>5s} {'AI':>6s} {'%roof':>6s} {'mfmaBusy':>8s} {'ldsBusy':>7s}  bound"]
     for i, e in enumerate(plan):
         pat = re.compile(e["pattern"])
         us = sum(t for n, t in tsegs[i] if pat.search(n)) / e["calls"] if i < len(tsegs) else float("nan")
@@ -108,8 +109,13 @@ def main():
         ai = e["flops"] / hbm
         roof = min(PEAK_TF, ai * HBM_TBS)
         bound = "MFMA" if ai * HBM_TBS >= PEAK_TF else "HBM"
+        # busy fractions per CU-cycle: GRBM_GUI_ACTIVE counts GPU-active cycles per XCD (summed
+        # over the 8), so x 32 CUs per XCD gives CU-cycles
+        cu_cyc = c.get("GRBM_GUI_ACTIVE", 0) * 32
+        mb = f"{c['SQ_VALU_MFMA_BUSY_CYCLES'] / cu_cyc:8.3f}" if cu_cyc and "SQ_VALU_MFMA_BUSY_CYCLES" in c else f"{'-':>8s}"
+        lb = f"{c['SQ_LDS_IDX_ACTIVE'] / cu_cyc:7.3f}" if cu_cyc and "SQ_LDS_IDX_ACTIVE" in c else f"{'-':>7s}"
         lines.append(f"{e['label']:38s} {us:8.1f} {tf:7.1f} {100 * tf / PEAK_TF:5.1f} {mf} {ldss} "
-                     f"{hbm / 1e6:8.1f} {tbs:5.2f} {ai:6.0f} {100 * tf / roof:6.1f}  {bound} ({src} bytes)")
+                     f"{hbm / 1e6:8.1f} {tbs:5.2f} {ai:6.0f} {100 * tf / roof:6.1f} {mb} {lb}  {bound} ({src} bytes)")
     text = "\n".join(lines) + "\n"
     print(text)
     if a.out:

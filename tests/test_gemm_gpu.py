@@ -1,7 +1,8 @@
 """Own transformer GEMM (csrc/kernels/gemm.hip: y = a · wᵀ on the LDS-DMA MFMA pipeline) against
 an fp32 torch reference of the same op: plain, + bias, + bias -> GELU (pre-activation and
-activation), + residual (in place, the pre-norm block's x += o · Woᵀ); M tails (rows past M read
-a zero line and are not stored), both tile widths (N % 256 and N % 128 only)."""
+activation), + residual (in place, the pre-norm block's x += o · Woᵀ); M tails (rows past M
+re-read row M - 1 and are not stored), both tile widths (N % 256 and N % 128 only), even and odd
+K-tile counts (an odd count runs behind a zero tile)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -35,12 +36,12 @@ def test_gemm_nt_plain_and_bias(M, K, N):
     assert _rel(yb, ref + b.float()) < 5e-3
 
 
-@pytest.mark.parametrize("bn", ["128", "256"])
-def test_gemm_nt_gelu_and_residual(bn, monkeypatch):
+@pytest.mark.parametrize("bn,K", [("128", 512), ("256", 512), ("256", 576)])
+def test_gemm_nt_gelu_and_residual(bn, K, monkeypatch):
     monkeypatch.setenv("XDDP_GEMM_BN", bn)  # read per call: both tile widths on one shape
     C = _C()
     g = torch.Generator(device="cuda").manual_seed(7)
-    M, K, N = 777, 512, 1024
+    M, N = 777, 1024
     a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
     w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
     b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
@@ -85,18 +86,3 @@ def test_own_linear_autograd_matches_fp32():
     for a, b in ((x.grad, xf.grad), (w.grad, wf.grad), (r.grad, rf.grad)):
         assert _rel(a, b) < 1e-2
 
-
-@pytest.mark.parametrize("K", [128, 1024])
-def test_gemm_nt_pipelines_agree(K, monkeypatch):
-    """The 4-phase K loop (even K/64) and the 2-phase loop (XDDP_GEMM_PIPE=0, and every odd K/64)
-    compute the same product (bitwise: same MFMA order per accumulator)."""
-    C = _C()
-    g = torch.Generator(device="cuda").manual_seed(K)
-    M, N = 1000, 512
-    a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
-    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
-    y4 = C.gemm_nt(a, w)[0]
-    monkeypatch.setenv("XDDP_GEMM_PIPE", "0")
-    y2 = C.gemm_nt(a, w)[0]
-    assert _rel(y4, a.float() @ w.float().t()) < 5e-3
-    assert torch.equal(y4, y2)
