@@ -38,7 +38,7 @@ using dev::f32x4;
 using dev::u32x4;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-constexpr int kBM = 256, kBK = 64, kWM = 2, kWN = 4, kThreads = 64 * kWM * kWN;
+constexpr int kBM = 256, kBK = 64, kWM = 2;  // waves along M; NW / kWM along N
 
 enum Epi : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiResidual = 3 };
 
@@ -46,16 +46,16 @@ enum Epi : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiResidual = 3 
 __device__ __forceinline__ float bf(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
-template <int BN, int EPI>
-__global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A,
+template <int BN, int EPI, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A,
                                                               const uint16_t* __restrict__ B,
                                                               uint16_t* Y, uint16_t* __restrict__ Y2,
                                                               const uint16_t* __restrict__ bias,
                                                               const uint16_t* res,
                                                               int M, int N, int K, int ntiles, int64_t ldr) {
-  constexpr int NW = kThreads / 64;
+  constexpr int kThreads = 64 * NW, kWN = NW / kWM;
   constexpr int AI = kBM / 8 / NW, BI = BN / 8 / NW;  // DMA wave-instructions per stage (8 rows each)
-  static_assert(NW == 8, "the DMA row mapping assumes 8 waves (row = (w + 8 i) * 8 + lane / 8)");
+  static_assert(NW == 4 || NW == 8, "4 waves (128 x BN/2 each, one per SIMD) or 8 (128 x BN/4, two per SIMD)");
   static_assert(AI * NW * 8 == kBM && BI * NW * 8 == BN, "tile rows must split evenly over the waves");
   constexpr int WTM = kBM / kWM, WTN = BN / kWN, TM = WTM / 16, TN = WTN / 16;
   constexpr int STAGE = (kBM + BN) * 128;
@@ -71,21 +71,21 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   // DMA sources: lane l of wave w fills 16-B slot (l & 7) of rows (w*AI + i)*8 + (l >> 3); the
   // offsets are recomputed per issue from two per-lane values (few live VGPRs: the 4-phase loop
   // needs ~224 for accumulators and fragments). Rows past M re-read row M - 1 (never stored).
-  const int drow = wid * 8 + (lane >> 3);                    // + i * 64 (A, i < AI) / j * 64 (B)
-  const int dchunk = 8 * (pos ^ ((drow >> 1) & 7));          // (row >> 1) & 7 is the same for row + 64 i
+  const int drow = wid * 8 + (lane >> 3);                    // + i * 8 NW (A, i < AI) / j * 8 NW (B)
+  const int dchunk = 8 * (pos ^ ((drow >> 1) & 7));          // (row >> 1) & 7 is the same for row + 32 i
   auto issue = [&](int kt, int buf) {
     uint8_t* As = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
-      const int row = min(m0 + drow + i * 64, M - 1);
+      const int row = min(m0 + drow + i * 8 * NW, M - 1);
       const uint16_t* src = A + (uint32_t)row * (uint32_t)K + (uint32_t)(dchunk + kt * kBK);
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + (wid * 8 + i * 64) * 128), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + (wid * 8 + i * 8 * NW) * 128), 16, 0, 0);
     }
     uint8_t* Bs = As + kBM * 128;
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
-      const uint16_t* src = B + (uint32_t)(n0 + drow + j * 64) * (uint32_t)K + (uint32_t)(dchunk + kt * kBK);
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(Bs + (wid * 8 + j * 64) * 128), 16, 0, 0);
+      const uint16_t* src = B + (uint32_t)(n0 + drow + j * 8 * NW) * (uint32_t)K + (uint32_t)(dchunk + kt * kBK);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(Bs + (wid * 8 + j * 8 * NW) * 128), 16, 0, 0);
     }
   };
 
@@ -279,18 +279,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   }
 }
 
-template <int BN, int EPI>
+template <int BN, int EPI, int NW>
 void launch_gemm(const at::Tensor& a, const at::Tensor& b, uint16_t* y, uint16_t* y2, const uint16_t* bias,
                  const uint16_t* res, int64_t ldr, int M, int N, int K, hipStream_t stream) {
   const int mtiles = (M + kBM - 1) / kBM, ntiles = N / BN;
   const size_t lds = std::max<size_t>((size_t)2 * (kBM + BN) * 128, (size_t)kBM * (BN * 2 + 16));
   static bool attr = false;
   if (!attr) {
-    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI>,
+    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI, NW>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI>), dim3(mtiles * ntiles), dim3(kThreads), lds, stream,
+  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI, NW>), dim3(mtiles * ntiles), dim3(64 * NW), lds, stream,
                      reinterpret_cast<const uint16_t*>(a.data_ptr()), reinterpret_cast<const uint16_t*>(b.data_ptr()),
                      y, y2, bias, res, M, N, K, ntiles, ldr);
   XDDP_HIP_CHECK(hipGetLastError());
@@ -373,17 +373,25 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
   auto* y2p = epi == 2 ? reinterpret_cast<uint16_t*>(y2.data_ptr()) : nullptr;
   const auto* bp = has_bias ? reinterpret_cast<const uint16_t*>(bias->data_ptr()) : nullptr;
   const auto* rp = epi == 3 ? reinterpret_cast<const uint16_t*>(res.data_ptr()) : nullptr;
-#define XDDP_GEMM(BN_)                                                                                 \
-  switch (epi) {                                                                                       \
-    case 0: launch_gemm<BN_, kEpiNone>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break;     \
-    case 1: launch_gemm<BN_, kEpiBias>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break;     \
-    case 2: launch_gemm<BN_, kEpiBiasGelu>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break; \
-    default: launch_gemm<BN_, kEpiResidual>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break; \
+#define XDDP_GEMM(BN_, NW_)                                                                                  \
+  switch (epi) {                                                                                             \
+    case 0: launch_gemm<BN_, kEpiNone, NW_>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break;     \
+    case 1: launch_gemm<BN_, kEpiBias, NW_>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break;     \
+    case 2: launch_gemm<BN_, kEpiBiasGelu, NW_>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break; \
+    default: launch_gemm<BN_, kEpiResidual, NW_>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break; \
   }
-  if (BN == 256) {
-    XDDP_GEMM(256)
+  const char* we = std::getenv("XDDP_GEMM_WAVES");  // A/B: 4 waves (one per SIMD) or 8
+  const int waves = we && std::atoi(we) == 4 ? 4 : 8;
+  if (waves == 4) {
+    if (BN == 256) {
+      XDDP_GEMM(256, 4)
+    } else {
+      XDDP_GEMM(128, 4)
+    }
+  } else if (BN == 256) {
+    XDDP_GEMM(256, 8)
   } else {
-    XDDP_GEMM(128)
+    XDDP_GEMM(128, 8)
   }
 #undef XDDP_GEMM
   if (epi == 2) return {y, y2};

@@ -8,6 +8,8 @@ export XDDP_NO_AUTOBUILD=1
 step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "$ROOT/gpurun_out/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -4 "$ROOT/gpurun_out/$name.log"; if [ $rc -ge 124 ]; then exit $rc; fi; }
 PYT="python -u -m pytest -x -v --timeout 240 --timeout-method thread"
 step pytest_gemm 300 $PYT tests/test_gemm_gpu.py
+XDDP_GEMM_WAVES=4 step pytest_gemm_w4 300 $PYT tests/test_gemm_gpu.py
+step gemm_bench 400 python -u scripts/gemm_nt_bench.py --out gpurun_out/r3_gemm_nt_vs_hipblaslt_v3.txt
 step stress_nocompute 100 python -u scripts/peer_stress.py --compute 0 --iters 4
 step stress_default 100 python -u scripts/peer_stress.py --iters 4
 step stress_b64 100 python -u scripts/peer_stress.py --blocks 64 --iters 4
