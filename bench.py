@@ -86,7 +86,8 @@ def parse(argv=None):
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     if a.batch_size is None:
-        a.batch_size = {"mlp": 64, "simplecnn": 32}.get(a.model, 256)
+        # LM configs: one 4096-token sequence per rank (Llama-3-8B pure DDP sizing on 288 GB)
+        a.batch_size = 1 if a.model.startswith("llama") else {"mlp": 64, "simplecnn": 32}.get(a.model, 256)
     if a.backend is None:
         a.backend = "rccl" if a.device == "cuda" else "cpu"
     return a

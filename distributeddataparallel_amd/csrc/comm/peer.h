@@ -19,9 +19,11 @@ constexpr int kPeerMaxRanks = 8;
 // only take part in the flag barrier), so each workgroup's call counter — which picks the
 // double-buffer slot — advances in lockstep with every other workgroup's.
 constexpr int kPeerMaxBlocks = 64;
-// Workgroups of a two-shot launch: 8 XCDs x 32 CUs; each rank pulls its slice from W - 1 peers
-// concurrently, so the xGMI reads of one launch are spread over every link.
+// Workgroups of a two-shot launch (at most kPeerTwoShotBlocks, XDDP_PEER_TWO_SHOT_BLOCKS; default
+// 64 = 8 per XCD): each rank pulls its slice from W - 1 peers concurrently, so the xGMI reads of
+// one launch are spread over every link.
 constexpr int kPeerTwoShotBlocks = 256;
+constexpr int kPeerTwoShotDefaultBlocks = 64;
 
 class PeerAllReduce {
  public:

@@ -63,27 +63,33 @@ __device__ __forceinline__ void st_release_sys(uint32_t* p, uint32_t v) {
 }
 
 // Cross-rank barrier of workgroup b at value `val`. Returns false (and raises the status word)
-// when a peer did not arrive within the timeout.
+// when a peer did not arrive within the timeout. Uses no LDS: wave 0 raises this rank's flags and
+// EVERY wave polls the peers' flags itself. A spinning workgroup that held LDS (or many registers)
+// would keep LDS-heavy compute kernels — the GEMMs and convolutions running concurrently on the
+// compute stream — off its CU until the peers arrive; when the peers share the GPU (2 processes
+// on one device) that is a deadlock broken only by the timeout.
 __device__ __forceinline__ bool flag_barrier(const PeerPtrs& pp, int b, int rank, int size, uint32_t val,
-                                             int* status, uint64_t timeout_ticks, int* s_ok) {
+                                             int* status, uint64_t timeout_ticks) {
   __threadfence_system();  // every thread's staging stores are visible system-wide before the flags go out
   __syncthreads();
-  if (threadIdx.x < size) {
-    st_release_sys(pp.flags[threadIdx.x] + b * kPeerMaxRanks + rank, val);
-    const uint32_t* f = pp.flags[rank] + b * kPeerMaxRanks + threadIdx.x;
+  if (threadIdx.x < size) st_release_sys(pp.flags[threadIdx.x] + b * kPeerMaxRanks + rank, val);
+  const int lane = threadIdx.x & 63;
+  bool ok = true;
+  if (lane < size) {
+    const uint32_t* f = pp.flags[rank] + b * kPeerMaxRanks + lane;
     const uint64_t t0 = wall_clock64();
     while (ld_acquire_sys(f) < val) {
       if (wall_clock64() - t0 > timeout_ticks) {
-        *s_ok = 0;
+        ok = false;
         __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  __syncthreads();
-  __threadfence_system();  // acquire side for the threads that did not poll
-  return *s_ok != 0;
+  ok = __all(ok);
+  __threadfence_system();  // acquire side for the lanes that did not poll
+  return ok;
 }
 
 // element <-> accumulator conversions (bf16 and fp16 reduce in fp32, integers in their own type)
@@ -135,14 +141,7 @@ __global__ __launch_bounds__(kThreads) void peer_kernel(T* __restrict__ io, int6
     T e[V];
   };
   const int b = blockIdx.x;
-  __shared__ uint32_t s_gen;
-  __shared__ int s_ok;
-  if (threadIdx.x == 0) {
-    s_gen = gen_dev[b] + 1u;
-    s_ok = 1;
-  }
-  __syncthreads();
-  const uint32_t gen = s_gen;
+  const uint32_t gen = gen_dev[b] + 1u;  // every thread reads it (no LDS); thread 0 writes it back last
   const int64_t lo = min(n, (int64_t)b * chunk), hi = min(n, lo + chunk);  // chunk is a multiple of V
   const int64_t off = (int64_t)(gen & 1u) * slot_bytes;
   T* mine = reinterpret_cast<T*>(pp.data[rank] + off);
@@ -150,7 +149,7 @@ __global__ __launch_bounds__(kThreads) void peer_kernel(T* __restrict__ io, int6
   // 1. stage this workgroup's chunk (empty for the workgroups past the end of the message)
   if (!BCAST || rank == root) copy_range(mine, io, lo, hi);
   // 2. cross-rank barrier on this workgroup's flags
-  if (flag_barrier(pp, b, rank, size, 2u * gen, status, timeout_ticks, &s_ok)) {
+  if (flag_barrier(pp, b, rank, size, 2u * gen, status, timeout_ticks)) {
     // 3. reduce (or read the root's copy) straight from the peers' slots
     const int64_t nv = (hi - lo) / V;
     if (MODE == 2) {
@@ -205,14 +204,7 @@ __global__ __launch_bounds__(kThreads) void two_shot_kernel(T* __restrict__ io, 
     T e[V];
   };
   const int b = blockIdx.x;
-  __shared__ uint32_t s_gen;
-  __shared__ int s_ok;
-  if (threadIdx.x == 0) {
-    s_gen = gen_dev[b] + 1u;
-    s_ok = 1;
-  }
-  __syncthreads();
-  const uint32_t gen = s_gen;
+  const uint32_t gen = gen_dev[b] + 1u;
   const int64_t off = (int64_t)(gen & 1u) * slot_bytes;
   const int64_t cs = chunk / W;
   const int64_t lo = min(n, (int64_t)b * chunk), hi = min(n, lo + chunk);
@@ -222,7 +214,7 @@ __global__ __launch_bounds__(kThreads) void two_shot_kernel(T* __restrict__ io, 
   // 1. stage the slices the peers will reduce (not my own: I reduce it from io directly)
   copy_range(mine, io, lo, my_lo);
   copy_range(mine, io, my_hi, hi);
-  if (flag_barrier(pp, b, rank, W, 2u * gen - 1u, status, timeout_ticks, &s_ok)) {
+  if (flag_barrier(pp, b, rank, W, 2u * gen - 1u, status, timeout_ticks)) {
     // 2. reduce my slice from every rank, in rank order (every rank gets bitwise the same sum);
     // the result goes to io and to my staging slot, where the peers gather it from
     const T* src[W];
@@ -253,7 +245,7 @@ __global__ __launch_bounds__(kThreads) void two_shot_kernel(T* __restrict__ io, 
       mine[i] = o;
     }
     // 3. gather the other ranks' reduced slices
-    if (flag_barrier(pp, b, rank, W, 2u * gen, status, timeout_ticks, &s_ok)) {
+    if (flag_barrier(pp, b, rank, W, 2u * gen, status, timeout_ticks)) {
 #pragma unroll
       for (int r = 0; r < W; ++r) {
         if (r == rank) continue;
@@ -339,9 +331,12 @@ PeerAllReduce::PeerAllReduce(std::shared_ptr<Store> store, int rank, int size, i
   XDDP_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&impl_->status_dev), impl_->status_host, 0));
   impl_->one.open(store, "1", rank, size, kPeerMaxBlocks, capacity);
   if (two_shot_capacity > 0) {
-    // XDDP_PEER_TWO_SHOT_BLOCKS: workgroups of the two-shot grid (8..256; fewer = fewer waves
-    // resident while a launch waits for its peers)
-    int nb = kPeerTwoShotBlocks;
+    // XDDP_PEER_TWO_SHOT_BLOCKS: workgroups of the two-shot grid (8..256, default 64). Every
+    // workgroup of a launch is resident while it waits for its peers, and a CU holding one cannot
+    // take a whole-CU compute workgroup (all LDS, or 512 registers per SIMD): 64 keeps 3/4 of the
+    // CUs for the backward that the all-reduce overlaps. With 256, two processes on one GPU whose
+    // GEMMs run concurrently stalled every launch until the timeout (scripts/peer_stress.py).
+    int nb = kPeerTwoShotDefaultBlocks;
     if (const char* e = std::getenv("XDDP_PEER_TWO_SHOT_BLOCKS")) nb = std::max(8, std::min(kPeerTwoShotBlocks, std::atoi(e)));
     impl_->two.open(store, "2", rank, size, nb, two_shot_capacity);
   }

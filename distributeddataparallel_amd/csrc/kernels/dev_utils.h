@@ -38,6 +38,31 @@ __device__ __forceinline__ uint32_t pack_f16x2(float a, float b) {
 }
 __device__ __forceinline__ uint16_t f32_to_f16(float a) { return __builtin_bit_cast(uint16_t, (_Float16)a); }
 
+// ---- exact (erf-form) GELU at a few VALU ops ---------------------------------------
+// erf(z) = 1 - t (a1 + t (a2 + t (a3 + t (a4 + t a5)))) e^{-z^2}, t = 1 / (1 + p z), z >= 0
+// (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7: below fp32 GELU rounding at the bf16 outputs
+// these feed): one v_rcp_f32, one v_exp_f32 and ~10 FMAs, branch-free, instead of the library
+// erff's two-range polynomial. For z = |x| / sqrt(2), e^{-z^2} = e^{-x^2/2} is also the Gaussian
+// factor of gelu', so the gradient reuses it.
+struct GeluTerms {
+  float cdf;  // Phi(x) = (1 + erf(x / sqrt 2)) / 2
+  float pdf;  // phi(x) = e^{-x^2/2} / sqrt(2 pi)
+};
+__device__ __forceinline__ GeluTerms gelu_terms(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
+  const float poly = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
+                              0.254829592f);
+  const float g = __builtin_amdgcn_exp2f(-z * z * 1.44269504088896341f);  // e^{-z^2}
+  const float e = fmaf(-poly, g, 1.f);                                    // erf(|x| / sqrt 2)
+  return {0.5f + copysignf(0.5f * e, x), 0.39894228040143268f * g};
+}
+__device__ __forceinline__ float gelu(float x) { return x * gelu_terms(x).cdf; }
+__device__ __forceinline__ float gelu_grad(float x) {
+  const GeluTerms k = gelu_terms(x);
+  return fmaf(x, k.pdf, k.cdf);
+}
+
 // ---- scalar access in compute type ------------------------------------------------
 template <typename T, typename C>
 struct Elem;

@@ -17,8 +17,8 @@
 // loads in the loop). The MFMA computes the
 // transposed tile (B rows as the first operand), so a lane's four accumulators are four
 // consecutive output columns of one row: the C tile goes to LDS as 8-B writes and leaves as full
-// 16-B row chunks, where the epilogue math runs. Block ids are remapped XCD-contiguously: the
-// N tiles of one M panel (which share the A panel) and neighbouring panels sit in one XCD's L2.
+// 16-B row chunks, where the epilogue math runs. Block ids are remapped XCD-contiguously and
+// each XCD's concurrent tiles form a GM x (32 / GM) block that shares A and B panels in its L2.
 // Rows past M re-read row M - 1 and are not stored.
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
@@ -27,6 +27,7 @@
 
 #include "common.h"
 #include "kernels/dev_utils.h"
+#include "kernels/norm.h"
 
 namespace xddp {
 namespace kernels {
@@ -38,32 +39,37 @@ using dev::f32x4;
 using dev::u32x4;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-constexpr int kBM = 256, kBK = 64, kWM = 2;  // waves along M; NW / kWM along N
+constexpr int kBM = 256, kBK = 64, kWM = 2, kWN = 4, NW = kWM * kWN, kThreads = 64 * NW;
 
-enum Epi : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiResidual = 3 };
+enum Epi : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiResidual = 3, kEpiDGelu = 4 };
 
 
 __device__ __forceinline__ float bf(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
-template <int BN, int EPI, int NW>
-__global__ __launch_bounds__(64 * NW, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A,
+template <int BN, int EPI>
+__global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A,
                                                               const uint16_t* __restrict__ B,
                                                               uint16_t* Y, uint16_t* __restrict__ Y2,
                                                               const uint16_t* __restrict__ bias,
-                                                              const uint16_t* res,
+                                                              const uint16_t* res, float* __restrict__ part,
                                                               int M, int N, int K, int ntiles, int64_t ldr) {
-  constexpr int kThreads = 64 * NW, kWN = NW / kWM;
   constexpr int AI = kBM / 8 / NW, BI = BN / 8 / NW;  // DMA wave-instructions per stage (8 rows each)
-  static_assert(NW == 4 || NW == 8, "4 waves (128 x BN/2 each, one per SIMD) or 8 (128 x BN/4, two per SIMD)");
   static_assert(AI * NW * 8 == kBM && BI * NW * 8 == BN, "tile rows must split evenly over the waves");
   constexpr int WTM = kBM / kWM, WTN = BN / kWN, TM = WTM / 16, TN = WTN / 16;
   constexpr int STAGE = (kBM + BN) * 128;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / kWN, wn = wid % kWN;
+  // Tile order: the XCD remap gives each XCD a contiguous run of logical tiles (32 at a time on
+  // its 32 CUs); logical tiles go through groups of GM m-tiles, M fastest inside a group, so such
+  // a run is a GM x (32 / GM) block of tiles that shares GM A panels and 32 / GM B panels in that
+  // XCD's L2 — instead of one A panel and 32 B panels (a full row of N tiles), which made every
+  // XCD stream all of B (2.6x hipBLASLt's HBM bytes on 8192^3, profiles/r3_pmc_kernels.txt).
+  constexpr int GM = BN == 256 ? 8 : 4;  // 8 x 4 tiles of 256 x 256, 4 x 8 of 256 x 128
   const int wg = dev::xcd_remap(blockIdx.x, gridDim.x);
-  const int nt = wg % ntiles, mt = wg / ntiles;
+  const int mtiles = gridDim.x / ntiles, grp = wg / (GM * ntiles), first_m = grp * GM;
+  const int gm = min(mtiles - first_m, GM), local = wg - grp * GM * ntiles;
+  const int mt = first_m + local % gm, nt = local / gm;
   const int n0 = nt * BN, m0 = mt * kBM;
   const int pos = lane & 7;  // 16-B slot this lane fills in its 128-B LDS row
   const int nk = K / kBK;
@@ -72,7 +78,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_kernel(const uint16_t* __r
   // offsets are recomputed per issue from two per-lane values (few live VGPRs: the 4-phase loop
   // needs ~224 for accumulators and fragments). Rows past M re-read row M - 1 (never stored).
   const int drow = wid * 8 + (lane >> 3);                    // + i * 8 NW (A, i < AI) / j * 8 NW (B)
-  const int dchunk = 8 * (pos ^ ((drow >> 1) & 7));          // (row >> 1) & 7 is the same for row + 32 i
+  const int dchunk = 8 * (pos ^ ((drow >> 1) & 7));          // (row >> 1) & 7 is the same for row + 64 i
   auto issue = [&](int kt, int buf) {
     uint8_t* As = smem + buf * STAGE;
 #pragma unroll
@@ -226,7 +232,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_kernel(const uint16_t* __r
       const int row = wm * WTM + i * 16 + (lane & 15);
       const int col = wn * WTN + j * 16 + (lane >> 4) * 4;
       f32x4 v = acc[i][j];
-      if (EPI != kEpiNone && EPI != kEpiResidual) {  // bias in fp32 before the one rounding
+      if (EPI == kEpiBias || EPI == kEpiBiasGelu) {  // bias in fp32 before the one rounding
         const uint2 bb = *reinterpret_cast<const uint2*>(bias + n0 + col);
         v[0] += bf(bb.x & 0xffffu);
         v[1] += bf(bb.x >> 16);
@@ -246,6 +252,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_kernel(const uint16_t* __r
   const int rows_valid = min(kBM, M - m0);
   u32x4 rb{};
   if (EPI == kEpiResidual && bias) rb = *reinterpret_cast<const u32x4*>(bias + n0 + cc * 8);
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // kEpiDGelu: this thread's column sums
 #pragma unroll 4
   for (int q = tid; q < kBM * CPR; q += kThreads) {
     const int row = q / CPR;
@@ -257,8 +264,20 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_kernel(const uint16_t* __r
       u32x4 g;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        g[e] = dev::pack_bf16x2(gelu_erf(bf(v[e] & 0xffffu)), gelu_erf(bf(v[e] >> 16)));
+        g[e] = dev::pack_bf16x2(dev::gelu(bf(v[e] & 0xffffu)), dev::gelu(bf(v[e] >> 16)));
       *reinterpret_cast<u32x4*>(Y2 + off) = g;
+    } else if (EPI == kEpiDGelu) {
+      // dh = (g·W, the bf16 C tile) · gelu'(h) in fp32; the fp32 dh also feed the column sums
+      const u32x4 hv = *reinterpret_cast<const u32x4*>(res + (int64_t)(m0 + row) * ldr + n0 + cc * 8);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = bf(v[e] & 0xffffu) * dev::gelu_grad(bf(hv[e] & 0xffffu));
+        const float hi = bf(v[e] >> 16) * dev::gelu_grad(bf(hv[e] >> 16));
+        csum[2 * e] += lo;
+        csum[2 * e + 1] += hi;
+        v[e] = dev::pack_bf16x2(lo, hi);
+      }
+      *reinterpret_cast<u32x4*>(Y + off) = v;
     } else if (EPI == kEpiResidual) {
       // y = res + (A·Bᵀ, already rounded to bf16 in the C tile) [+ bias]: one extra rounding of
       // the product against addmm_'s single one (the residual term dominates the sum)
@@ -277,22 +296,39 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_nt_kernel(const uint16_t* __r
       *reinterpret_cast<u32x4*>(Y + off) = v;
     }
   }
+  if (EPI == kEpiDGelu) {
+    // column sums of the tile: the kThreads / CPR row groups meet in LDS past the C tile, then
+    // thread c < BN writes part[m-tile][n0 + c] (colsum_partials adds the m-tiles up)
+    constexpr int RG = kThreads / CPR;
+    float* red = reinterpret_cast<float*>(smem + kBM * CST);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[(tid / CPR) * BN + cc * 8 + e] = csum[e];
+    __syncthreads();
+    if (tid < BN) {
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < RG; ++r) t += red[r * BN + tid];
+      part[(int64_t)mt * N + n0 + tid] = t;
+    }
+  }
 }
 
-template <int BN, int EPI, int NW>
+template <int BN, int EPI>
 void launch_gemm(const at::Tensor& a, const at::Tensor& b, uint16_t* y, uint16_t* y2, const uint16_t* bias,
-                 const uint16_t* res, int64_t ldr, int M, int N, int K, hipStream_t stream) {
+                 const uint16_t* res, float* part, int64_t ldr, int M, int N, int K, hipStream_t stream) {
   const int mtiles = (M + kBM - 1) / kBM, ntiles = N / BN;
-  const size_t lds = std::max<size_t>((size_t)2 * (kBM + BN) * 128, (size_t)kBM * (BN * 2 + 16));
+  // stages | C tile (+ the column-sum exchange of the dGELU epilogue)
+  const size_t lds = std::max<size_t>((size_t)2 * (kBM + BN) * 128,
+                                      (size_t)kBM * (BN * 2 + 16) + (EPI == kEpiDGelu ? (size_t)2048 * NW : 0));
   static bool attr = false;
   if (!attr) {
-    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI, NW>,
+    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI, NW>), dim3(mtiles * ntiles), dim3(64 * NW), lds, stream,
+  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI>), dim3(mtiles * ntiles), dim3(kThreads), lds, stream,
                      reinterpret_cast<const uint16_t*>(a.data_ptr()), reinterpret_cast<const uint16_t*>(b.data_ptr()),
-                     y, y2, bias, res, M, N, K, ntiles, ldr);
+                     y, y2, bias, res, part, M, N, K, ntiles, ldr);
   XDDP_HIP_CHECK(hipGetLastError());
 }
 
@@ -312,7 +348,9 @@ int pick_bn(int64_t M, int64_t N, int cus) {
 // a [M, K] bf16 (row-major, rows 16-B aligned), w [N, K] bf16 -> y [M, N] bf16 = a · wᵀ with
 // epilogue `epi`: 0 none, 1 + bias, 2 + bias then GELU (returns {pre-activation, activation}),
 // 3 + residual (y may be `out` = the residual itself: the in-place x += a·wᵀ of a pre-norm block;
-// + bias if given). K % 64 == 0, N % 128 == 0.
+// + bias if given), 4 the GELU backward of an MLP: `residual` is the pre-activation h and the
+// result is {dh = (a·wᵀ)·gelu'(h), Σ_rows dh} (the second in bias's dtype if a bias is passed —
+// only its dtype is used — else fp32). K % 64 == 0, N % 128 == 0.
 std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                                 int64_t epi, const c10::optional<at::Tensor>& residual,
                                 const c10::optional<at::Tensor>& out) {
@@ -326,7 +364,7 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
               "gemm_nt: needs K % 64 == 0 and N % 128 == 0");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
               "gemm_nt: 16-B aligned operands required");
-  TORCH_CHECK(epi >= 0 && epi <= 3, "gemm_nt: epi must be 0..3");
+  TORCH_CHECK(epi >= 0 && epi <= 4, "gemm_nt: epi must be 0..4");
   const bool has_bias = bias.has_value() && bias->defined();
   if (has_bias)
     TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kBFloat16 && bias->numel() == N && bias->is_contiguous() &&
@@ -335,8 +373,8 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
   TORCH_CHECK((epi != 1 && epi != 2) || has_bias, "gemm_nt: epilogues 1 and 2 need a bias");
   at::Tensor res;
   int64_t ldr = N;
-  if (epi == 3) {
-    TORCH_CHECK(residual.has_value() && residual->defined(), "gemm_nt: epilogue 3 needs a residual");
+  if (epi == 3 || epi == 4) {
+    TORCH_CHECK(residual.has_value() && residual->defined(), "gemm_nt: epilogues 3 and 4 need a residual / h");
     res = *residual;
     TORCH_CHECK(res.scalar_type() == at::kBFloat16 && res.dim() == 2 && res.size(0) == M && res.size(1) == N &&
                     res.stride(1) == 1 && res.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(res.data_ptr()) % 16 == 0,
@@ -348,6 +386,7 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
     y = *out;
     TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 2 && y.size(0) == M && y.size(1) == N && y.is_contiguous(),
                 "gemm_nt: out must be a contiguous bf16 [M, N] tensor");
+    TORCH_CHECK(epi != 4, "gemm_nt: epilogue 4 allocates its outputs");
     TORCH_CHECK(epi != 3 || y.data_ptr() == res.data_ptr() || !(y.data_ptr() < (char*)res.data_ptr() + res.nbytes() &&
                                                                   res.data_ptr() < (char*)y.data_ptr() + y.nbytes()),
                 "gemm_nt: out may alias the residual only exactly");
@@ -372,29 +411,29 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
   auto* yp = reinterpret_cast<uint16_t*>(y.data_ptr());
   auto* y2p = epi == 2 ? reinterpret_cast<uint16_t*>(y2.data_ptr()) : nullptr;
   const auto* bp = has_bias ? reinterpret_cast<const uint16_t*>(bias->data_ptr()) : nullptr;
-  const auto* rp = epi == 3 ? reinterpret_cast<const uint16_t*>(res.data_ptr()) : nullptr;
-#define XDDP_GEMM(BN_, NW_)                                                                                  \
-  switch (epi) {                                                                                             \
-    case 0: launch_gemm<BN_, kEpiNone, NW_>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break;     \
-    case 1: launch_gemm<BN_, kEpiBias, NW_>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break;     \
-    case 2: launch_gemm<BN_, kEpiBiasGelu, NW_>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break; \
-    default: launch_gemm<BN_, kEpiResidual, NW_>(a, w, yp, y2p, bp, rp, ldr, (int)M, (int)N, (int)K, stream); break; \
+  const auto* rp = epi >= 3 ? reinterpret_cast<const uint16_t*>(res.data_ptr()) : nullptr;
+  at::Tensor part = epi == 4 ? at::empty({(M + kBM - 1) / kBM, N}, a.options().dtype(at::kFloat)) : at::Tensor();
+  float* pp = epi == 4 ? part.data_ptr<float>() : nullptr;
+#define XDDP_GEMM(BN_)                                                                                    \
+  switch (epi) {                                                                                          \
+    case 0: launch_gemm<BN_, kEpiNone>(a, w, yp, y2p, bp, rp, pp, ldr, (int)M, (int)N, (int)K, stream); break;     \
+    case 1: launch_gemm<BN_, kEpiBias>(a, w, yp, y2p, bp, rp, pp, ldr, (int)M, (int)N, (int)K, stream); break;     \
+    case 2: launch_gemm<BN_, kEpiBiasGelu>(a, w, yp, y2p, bp, rp, pp, ldr, (int)M, (int)N, (int)K, stream); break; \
+    case 3: launch_gemm<BN_, kEpiResidual>(a, w, yp, y2p, bp, rp, pp, ldr, (int)M, (int)N, (int)K, stream); break; \
+    default: launch_gemm<BN_, kEpiDGelu>(a, w, yp, y2p, bp, rp, pp, ldr, (int)M, (int)N, (int)K, stream); break;   \
   }
-  const char* we = std::getenv("XDDP_GEMM_WAVES");  // A/B: 4 waves (one per SIMD) or 8
-  const int waves = we && std::atoi(we) == 4 ? 4 : 8;
-  if (waves == 4) {
-    if (BN == 256) {
-      XDDP_GEMM(256, 4)
-    } else {
-      XDDP_GEMM(128, 4)
-    }
-  } else if (BN == 256) {
-    XDDP_GEMM(256, 8)
+  if (BN == 256) {
+    XDDP_GEMM(256)
   } else {
-    XDDP_GEMM(128, 8)
+    XDDP_GEMM(128)
   }
 #undef XDDP_GEMM
   if (epi == 2) return {y, y2};
+  if (epi == 4) {
+    at::Tensor db = at::empty({N}, has_bias ? bias->options() : a.options().dtype(at::kFloat));
+    colsum_partials(part, db);
+    return {y, db};
+  }
   return {y};
 }
 

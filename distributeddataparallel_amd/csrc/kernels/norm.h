@@ -44,7 +44,8 @@ std::vector<at::Tensor> bn_backward_from_partials(const at::Tensor& part, int64_
 at::Tensor bn_backward_elem(const at::Tensor& g, const at::Tensor& x, const at::Tensor& mean, const at::Tensor& coef);
 // 3x3 pad-1 conv (stride 1/2) as an implicit MFMA GEMM (csrc/kernels/conv3x3.hip)
 // Transformer linear layers (gemm.hip): y = a · wᵀ with epilogue 0 none | 1 + bias |
-// 2 + bias -> GELU (returns {pre-activation, activation}) | 3 + residual (in place with out).
+// 2 + bias -> GELU (returns {pre-activation, activation}) | 3 + residual (in place with out) |
+// 4 GELU backward: residual = h, returns {(a·wᵀ)·gelu'(h), its column sums}.
 std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                                 int64_t epi, const c10::optional<at::Tensor>& residual,
                                 const c10::optional<at::Tensor>& out);

@@ -96,10 +96,9 @@ __global__ __launch_bounds__(kBlock) void swiglu_bwd_kernel(const T* __restrict_
 
 // GELU (exact, erf form): gelu(x) = x Φ(x), Φ(x) = (1 + erf(x / √2)) / 2;
 // gelu'(x) = Φ(x) + x φ(x), φ(x) = exp(-x² / 2) / √(2π).
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad(float x) {
-  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
-}
+// (dev::gelu / dev::gelu_grad: the branch-free erf of dev_utils.h, shared with the GEMM epilogues)
+__device__ __forceinline__ float gelu_f(float x) { return dev::gelu(x); }
+__device__ __forceinline__ float gelu_grad(float x) { return dev::gelu_grad(x); }
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void gelu_fwd_kernel(const T* __restrict__ h, T* __restrict__ a, int64_t nvec) {

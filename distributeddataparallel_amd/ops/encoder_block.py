@@ -9,7 +9,8 @@ add that ``select`` backward uses to assemble the packed q/k/v gradient. Here:
 
 * forward: LN1 also writes ``xb = x + b_proj`` and LN2 ``x1b = x1 + b_fc2``; each residual sum is
   then the beta = 1 GEMM ``xb += o·Wprojᵀ`` (hipBLASLt reads C in its epilogue) — no add passes;
-* backward: ``bias_grad`` forms dh = g·gelu'(h) and Σ dh (fc1's bias gradient) in one pass;
+* backward: fc2's input-gradient GEMM forms dh = (g·W_2)·gelu'(h) and Σ dh (fc1's bias gradient)
+  in its epilogue (own GEMM; with hipBLASLt ``bias_grad`` does it in one pass after the GEMM);
   LN2's backward adds the residual gradient and also sums both residual gradients (the bias
   gradients of fc2 and of the out projection); LN1's backward adds its residual gradient;
   the flash-attention backward writes dq/dk/dv straight into one packed [B, S, 3, H, Dh] buffer,
@@ -91,9 +92,11 @@ class _EncoderBlockFn(torch.autograd.Function):
         heads, dh = ctx.heads, D // ctx.heads
         g2 = g.reshape(-1, D).contiguous()
         # MLP
-        da = torch.mm(g2, w_2)
+        if _own_gemm(D, w_1.shape[0]):  # dh = (g·W_2)·gelu'(h) and Σ dh in the dgrad GEMM's epilogue
+            dhid, db_1 = C.gemm_nt(g2, w_2.t().contiguous(), b_1, 4, h)
+        else:
+            db_1, dhid = C.bias_grad(torch.mm(g2, w_2), h, b_1)
         dw_2 = torch.mm(g2.t(), a)
-        db_1, dhid = C.bias_grad(da, h, b_1)
         dy2 = torch.mm(dhid, w_1)
         dw_1 = torch.mm(dhid.t(), y2)
         # LN2 + residual: g1 = g2 + LN2ᵀ(dy2); Σ g2 = fc2's bias grad, Σ g1 = the out projection's
@@ -115,9 +118,9 @@ class _EncoderBlockFn(torch.autograd.Function):
 
 
 def _own_gemm(D: int, hidden: int) -> bool:
-    """Forward projections on the own LDS-DMA MFMA GEMM (csrc/kernels/gemm.hip) with the bias,
-    bias+GELU and residual epilogues fused; XDDP_OWN_GEMM=0 keeps hipBLASLt (addmm) + the
-    separate GELU pass (A/B switch)."""
+    """Forward projections and fc2's input gradient on the own LDS-DMA MFMA GEMM
+    (csrc/kernels/gemm.hip) with the bias, bias+GELU, residual and dGELU+bias-gradient epilogues
+    fused; XDDP_OWN_GEMM=0 keeps hipBLASLt (addmm / mm) + the separate GELU passes (A/B switch)."""
     return (os.environ.get("XDDP_OWN_GEMM", "1") != "0" and D % 128 == 0 and hidden % 128 == 0
             and (3 * D) % 128 == 0)
 

@@ -41,14 +41,7 @@ for name, M, K, N in SHAPES:
     ref = torch.mm(a, w.t())
     err = ((C.gemm_nt(a, w)[0].float() - ref.float()).norm() / ref.float().norm()).item()
     fl = 2.0 * M * N * K
-    def w4():
-        os.environ["XDDP_GEMM_WAVES"] = "4"
-        try:
-            return C.gemm_nt(a, w)
-        finally:
-            del os.environ["XDDP_GEMM_WAVES"]
-
-    arms = {"blas": lambda: torch.mm(a, w.t()), "own": lambda: C.gemm_nt(a, w), "own_w4": w4}
+    arms = {"blas": lambda: torch.mm(a, w.t()), "own": lambda: C.gemm_nt(a, w)}
     if name.startswith("vit fc1"):
         arms["blas_bias_gelu"] = lambda: F.gelu(torch.addmm(b, a, w.t()))
         arms["own_bias_gelu"] = lambda: C.gemm_nt(a, w, b, 2)
@@ -62,7 +55,7 @@ for name, M, K, N in SHAPES:
     med = {k: statistics.median(v) for k, v in t.items()}
     line = (f"{name:16s} M{M} K{K} N{N}: hipBLASLt {med['blas']:.3f} ms ({fl / med['blas'] / 1e9:.0f} TF/s) | "
             f"own {med['own']:.3f} ms ({fl / med['own'] / 1e9:.0f} TF/s) = {med['blas'] / med['own']:.2f}x "
-            f"(rel err {err:.1e}); 4 waves {fl / med['own_w4'] / 1e9:.0f} TF/s")
+            f"(rel err {err:.1e})")
     if "own_bias_gelu" in med:
         line += (f" | +bias+GELU: hipBLASLt addmm + gelu {med['blas_bias_gelu']:.3f} ms, own fused "
                  f"{med['own_bias_gelu']:.3f} ms")

@@ -71,7 +71,7 @@ def main():
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
     from _dist_utils import run_ranks
 
-    print(f"[stress] world={a.world} priority={a.priority} compute={a.compute} blocks={a.blocks or 256}", flush=True)
+    print(f"[stress] world={a.world} priority={a.priority} compute={a.compute} blocks={a.blocks or 64}", flush=True)
     run_ranks(_rank, world=a.world, args=(a,))
     print("[stress] ok", flush=True)
 

@@ -86,3 +86,24 @@ def test_own_linear_autograd_matches_fp32():
     for a, b in ((x.grad, xf.grad), (w.grad, wf.grad), (r.grad, rf.grad)):
         assert _rel(a, b) < 1e-2
 
+
+
+@pytest.mark.parametrize("M,K,N", [(777, 512, 1024), (12608 // 8, 1024, 4096), (300, 192, 384)])
+def test_gemm_nt_dgelu_bias_grad(M, K, N):
+    """Epilogue 4 (the MLP's GELU backward in fc2's input-gradient GEMM): dh = (g·Wᵀ)·gelu'(h)
+    and its column sums (fc1's bias gradient), vs fp32 torch autograd of GELU."""
+    C = _C()
+    g = torch.Generator(device="cuda").manual_seed(M)
+    a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    h = (torch.randn(M, N, device="cuda", generator=g) * 2).to(torch.bfloat16)
+    b = torch.zeros(N, device="cuda", dtype=torch.bfloat16)
+    dh, db = C.gemm_nt(a, w, b, 4, h)
+    assert dh.shape == (M, N) and db.shape == (N,) and db.dtype == torch.bfloat16
+    hf = h.float().requires_grad_()
+    up = a.float() @ w.float().t()
+    F.gelu(hf).backward(up)
+    assert _rel(dh, hf.grad) < 1e-2
+    assert _rel(db, hf.grad.sum(0)) < 1e-2
+    _, db32 = C.gemm_nt(a, w, None, 4, h)  # no bias: fp32 sums
+    assert db32.dtype == torch.float32 and _rel(db32, hf.grad.sum(0)) < 5e-3
