@@ -19,5 +19,8 @@ XDDP_OWN_GEMM=0 step vit_own0 300 python -u bench.py --model vit_l_16 --steps 5 
 step llama_own1 400 python -u bench.py --model llama3_8b --steps 3 --warmup 2 --json-out gpurun_out/r3_llama_own1.json
 XDDP_OWN_GEMM=0 step llama_own0 400 python -u bench.py --model llama3_8b --steps 3 --warmup 2 --json-out gpurun_out/r3_llama_own0.json
 bash scripts/gpu_r3_pmc.sh || exit $?
+cd /tmp && export TMPDIR=/tmp
+XDDP_RCCL_FORCE_LAUNCH=1 step prof_llama_overlap 500 rocprofv3 --kernel-trace -d "$ROOT/gpurun_out/prof_llama_overlap" -o run --output-format csv -- python3 "$ROOT/bench.py" --model llama3_8b --steps 3 --warmup 2 --diag-steps 0 --overlap-optim 1
+python3 "$ROOT/scripts/overlap_trace.py" "$ROOT/gpurun_out/prof_llama_overlap" --out "$ROOT/gpurun_out/r3_llama_overlap_tail.txt"
 cd "$ROOT"
 step pytest_all 1000 $PYT -m gpu tests
