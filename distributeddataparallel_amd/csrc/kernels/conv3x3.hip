@@ -301,14 +301,9 @@ const uint16_t* zero_line(const at::Tensor& like) {
   return reinterpret_cast<const uint16_t*>(z[d]->data_ptr());
 }
 
-int tile_choice(int N) {
-  int t = N % 128 == 0 ? 0 : 4;  // 256x128 (8 waves, 1 block/CU); N = 64: 128x64 (4 waves, 2 blocks/CU)
-  if (const char* e = std::getenv("XDDP_C3_TILE")) t = std::atoi(e);
-  if (N % 128 != 0)
-    if (const char* e = std::getenv("XDDP_C3_TILE64")) t = std::atoi(e);  // the 64-channel layers only
-  if (N % 128 != 0 && t < 2) t += 2;  // 128-wide N tiles need N % 128 == 0
-  return t;
-}
+// Block tile (r1/r2 A/Bs on the ResNet-50 shapes, fixed since): 256x128 (8 waves, one block per
+// CU) when N % 128 == 0, else 128x64 (4 waves, two blocks per CU) for the 64-channel layers.
+int tile_choice(int N) { return N % 128 == 0 ? 0 : 4; }
 
 }  // namespace
 
@@ -358,12 +353,8 @@ std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w
   } while (0)
   switch (cfg) {
     case 0: XDDP_C3(256, 128, 4, 2); break;
-    case 1: XDDP_C3(128, 128, 2, 2); break;
-    case 2: XDDP_C3(256, 64, 4, 1); break;
-    case 3: XDDP_C3(128, 64, 2, 1); break;
     case 4: XDDP_C3(128, 64, 2, 2); break;
-    case 5: XDDP_C3(256, 64, 4, 2); break;
-    default: TORCH_CHECK(false, "conv3x3_forward: XDDP_C3_TILE must be 0..5");
+    default: TORCH_CHECK(false, "conv3x3_forward: bad tile config");
   }
 #undef XDDP_C3
   return {y, part};
@@ -390,11 +381,7 @@ std::vector<at::Tensor> conv1x1_dma_forward(const at::Tensor& x, const at::Tenso
   const int64_t OH = (IH - 1) / stride + 1, OW = (IW - 1) / stride + 1, M = B * OH * OW;
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "conv1x1_dma_forward: bad size");
   auto y = at::empty({B, N, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  static const int tile_env = [] {
-    const char* e = std::getenv("XDDP_C1_TILE");
-    return e ? std::atoi(e) : -1;
-  }();
-  int cfg = tile == 0 || tile == 4 ? (int)tile : (tile_env == 0 || tile_env == 4 ? tile_env : -1);
+  int cfg = tile == 0 || tile == 4 ? (int)tile : -1;
   if (N % 128 != 0) cfg = 4;
   if (cfg < 0) cfg = ((M + 255) / 256) * (N / 128) >= 512 ? 0 : 4;
   const int BM = cfg == 0 ? 256 : 128, BN = cfg == 0 ? 128 : 64;
@@ -446,11 +433,7 @@ at::Tensor conv3x3_dgrad_s2(const at::Tensor& dy, const at::Tensor& w_rot, int64
               "conv3x3_dgrad_s2: 16-B aligned operands required");
   TORCH_CHECK(B * H * W < (int64_t(1) << 31) && dy.numel() < (int64_t(1) << 40), "conv3x3_dgrad_s2: bad size");
   auto dx = at::empty({B, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
-  int cfg = tile_choice((int)C);
-  if (const char* e = std::getenv("XDDP_DG2_TILE")) {  // A/B: the phase grids' tile on its own
-    cfg = std::atoi(e);
-    if (C % 128 != 0 && cfg < 2) cfg += 2;
-  }
+  const int cfg = tile_choice((int)C);
   const int BM = cfg == 1 || cfg == 3 || cfg == 4 ? 128 : 256, BN = cfg <= 1 ? 128 : 64;
   const int ntiles = (int)(C / BN);
   Dg2Geo dg{(int)B, (int)H, (int)W, {0, 0, 0, 0}};
@@ -479,12 +462,8 @@ at::Tensor conv3x3_dgrad_s2(const at::Tensor& dy, const at::Tensor& w_rot, int64
   go(conv3x3_fwd_kernel<BM_, BN_, WM_, WN_, false, 9, true>, 64 * WM_ * WN_, (size_t)kStages * (BM_ + BN_) * 128)
   switch (cfg) {
     case 0: XDDP_D2(256, 128, 4, 2); break;
-    case 1: XDDP_D2(128, 128, 2, 2); break;
-    case 2: XDDP_D2(256, 64, 4, 1); break;
-    case 3: XDDP_D2(128, 64, 2, 1); break;
     case 4: XDDP_D2(128, 64, 2, 2); break;
-    case 5: XDDP_D2(256, 64, 4, 2); break;
-    default: TORCH_CHECK(false, "conv3x3_dgrad_s2: XDDP_C3_TILE must be 0..5");
+    default: TORCH_CHECK(false, "conv3x3_dgrad_s2: bad tile config");
   }
 #undef XDDP_D2
   return dx;

@@ -36,10 +36,7 @@ using dev::f32x4;
 using dev::u32x4;
 
 constexpr int kBK = 64;       // K per tile (one 128-B LDS row per operand row)
-#ifndef XDDP_GEMM_NTSTORE
-#define XDDP_GEMM_NTSTORE 1
-#endif
-constexpr bool NTSTORE = XDDP_GEMM_NTSTORE;  // streaming (non-temporal) output stores
+constexpr bool NTSTORE = true;  // streaming (non-temporal) output stores
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ ((row >> 1) & 7)); }
 
@@ -1056,52 +1053,21 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
     }
   }
   const int BN = (N % 128 == 0) ? 128 : 64;
-  // The BN-reduce epilogue GEMM on 64x128 tiles (8 waves of 32x32, two blocks per CU, 128 VGPRs
-  // without spills): half the live epilogue registers of the 128x128 tile, so two tiles' loads
-  // are in flight per CU — 271/157/89/73 vs 337/190/104/79 us on the ResNet-50 stage shapes
-  // (profiles/r2_epi_dgrad_shapes.txt), 12,418-12,422 vs 12,120-12,154 img/s.
-  // XDDP_GEMM_EPI_BM=128 keeps the 128x128 tile at one block per CU.
-  static const bool epi_bm64 = [] {
-    const char* e = std::getenv("XDDP_GEMM_EPI_BM");
-    return !(e && std::atoi(e) == 128);
-  }();
-  // A/B: XDDP_GEMM_BM64=fwd,pro also puts the forward-with-statistics GEMM and/or the
-  // BN-backward-prologue input gradient on 64x128 tiles (measured: fwd 12,304, pro 12,446 vs
-  // 12,438-12,454 img/s default — neither pays, unlike the epilogue-heavy EPI GEMM)
-  static const int bm64_other = [] {
-    const char* e = std::getenv("XDDP_GEMM_BM64");
-    const std::string v = e ? e : "";
-    return (v.find("fwd") != std::string::npos ? 1 : 0) | (v.find("pro") != std::string::npos ? 2 : 0);
-  }();
-  const bool bm64_gen = BN == 128 && !epi_on &&
-                        (((bm64_other & 1) && stats && pro == 0 && !w_t) || ((bm64_other & 2) && pro >= 2 && w_t));
-  const bool bm64 = (epi_on && epi_bm64 && BN == 128) || bm64_gen;
+  // Tile / occupancy choices, each measured on ResNet-50 bs256 (r2 A/Bs, now fixed):
+  // * the BN-reduce epilogue GEMM (EPI) runs 64x128 tiles (8 waves of 32x32, two blocks per CU,
+  //   128 VGPRs without spills): half the live epilogue registers of the 128x128 tile, so two
+  //   tiles' loads are in flight per CU — 271/157/89/73 vs 337/190/104/79 us on the stage shapes
+  //   (profiles/r2_epi_dgrad_shapes.txt), 12,418-12,422 vs 12,120-12,154 img/s; the forward and
+  //   BN-backward-prologue GEMMs on 64x128 measured no gain (12,304 / 12,446 vs 12,438-12,454);
+  // * a 64-wide EPI tile (N % 128 != 0) runs at occupancy 2 (one block per CU, 190 VGPRs): its
+  //   epilogue loads stay live across the K loop and spill 76 registers within the 128 of
+  //   occupancy 4 (331/189/105/78 vs 614/334/200/96 us, 11,969 vs 10,915 img/s);
+  // * everything else at occupancy 4, persistent grid of 2 blocks per CU (one resident round).
+  const bool bm64 = epi_on && BN == 128;
   const int BM = bm64 ? 64 : 128;
   const int mtiles = (int)((M + BM - 1) / BM), ntiles = (int)(N / BN);
-  // 2-3 blocks per CU resident (LDS 48-64 KB, <= 128 VGPRs): size the grid to a few rounds
-  static const int blocks_per_cu = [] {
-    const char* e = std::getenv("XDDP_GEMM_BLOCKS_PER_CU");
-    return e ? std::max(1, std::atoi(e)) : 2;  // persistent: one resident round (2 blocks per CU) measured best
-  }();
-  static const int occ = [] {
-    const char* e = std::getenv("XDDP_GEMM_OCC");
-    return e && std::atoi(e) == 2 ? 2 : 4;
-  }();
-  static const int epi_occ = [] {  // the BN-reduce epilogue variant's own choice (XDDP_GEMM_EPI_OCC)
-    // default 2 (one block per CU, 190 VGPRs, no spills): its epilogue loads are issued at the
-    // tile start and stay live across the K loop, which spills 76 registers within the 128 of
-    // occupancy 4 (331/189/105/78 vs 614/334/200/96 us on the ResNet-50 stage shapes,
-    // profiles/r2_epi_dgrad_shapes.txt; 11,969 vs 10,915 img/s)
-    const char* e = std::getenv("XDDP_GEMM_EPI_OCC");
-    return e ? (std::atoi(e) == 4 ? 4 : 2) : 2;
-  }();
-  // the BN-backward-prologue input gradients' own choice (XDDP_GEMM_PRO_OCC): 4 measured better
-  // (12,224-12,227 vs 12,117-12,123 img/s at 2, ResNet-50 bs256)
-  static const int pro_occ = [] {
-    const char* e = std::getenv("XDDP_GEMM_PRO_OCC");
-    return e ? (std::atoi(e) == 2 ? 2 : 4) : 4;
-  }();
-  const int kocc = bm64 ? 4 : (epi_on ? epi_occ : (pro >= 2 ? pro_occ : occ));
+  const int kocc = bm64 ? 4 : (epi_on ? 2 : 4);
+  constexpr int blocks_per_cu = 2;
   const int target = num_cus() * (kocc == 2 ? 1 : blocks_per_cu);
   int groups = std::max(1, std::min(mtiles, (target + ntiles - 1) / ntiles));
   at::Tensor part = stats ? at::empty({groups, 3, N}, x.options().dtype(at::kFloat))
@@ -1128,10 +1094,7 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
 #define XDDP_LG(BN_, WM_, WN_, OCC_)                                                                            \
   launch_gemm<128, BN_, WM_, WN_, OCC_>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, \
                                         mtiles, ntiles, groups, x2p, epi)
-  if (bm64_gen) {
-    launch_gemm<64, 128, 2, 4, 4>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles,
-                                  ntiles, groups, x2p, epi);
-  } else if (bm64) {  // (EPI implies w_t; pro is 0 or the BN-backward form 2)
+  if (bm64) {  // (EPI implies w_t; pro is 0 or the BN-backward form 2)
     auto kern = pro == 2 ? conv1x1_gemm_kernel<64, 128, 2, 4, 2, false, false, true, true, 4>
                          : conv1x1_gemm_kernel<64, 128, 2, 4, 0, false, false, true, true, 4>;
     hipLaunchKernelGGL(kern, grid, dim3(512), lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,

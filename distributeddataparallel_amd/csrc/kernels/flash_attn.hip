@@ -420,8 +420,8 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_kernel(
 // Wave (group G, index wq) owns keys k0 + 32 wq .. +31; the groups split the (query head of the
 // GQA group, 32-row query tile) work items (G takes items G, G + NG, ...), so two waves share each
 // SIMD, and sum their dK^T / dV^T accumulators through LDS at the end. KW = 4 (128-key blocks) is
-// the default; KW = 2 (XDDP_FA_DKDV_KW=2) balances causal work better (twice as many half-size
-// blocks) but re-reads every Q / dO tile per 64 keys: Llama-shape fwd+bwd 1.30 vs 1.16 ms. Per item: S = Q·K^T and
+// the default; KW = 2 balanced causal work better (twice as many half-size blocks) but re-read
+// every Q / dO tile per 64 keys: Llama-shape fwd+bwd 1.30 vs 1.16 ms (r2), so it was dropped. Per item: S = Q·K^T and
 // dP = dO·V^T with the KEY on the lane (K fragments in registers, the V block in LDS), then
 // dV^T += dO^T·P and dK^T += Q^T·dS with P / dS as the B operands straight from their
 // accumulators. Q / dO / lse / delta tiles go global -> LDS by LDS-DMA (no VGPR staging), two
@@ -729,12 +729,8 @@ std::vector<at::Tensor> flash_attn_forward(const at::Tensor& q, const at::Tensor
   auto lse = at::empty({B, Hq, Sq}, q.options().dtype(at::kFloat));
   auto stream = c10::hip::getCurrentHIPStream(q.device().index()).stream();
   // 8 waves (256 query rows) per workgroup; 4 when 256-row blocks would leave CUs idle
-  static const int nw_env = [] {
-    const char* e = std::getenv("XDDP_FA_WAVES");
-    return e ? std::atoi(e) : 0;
-  }();
   const int64_t wg8 = ((Sq + 255) / 256) * B * Hq;
-  const int nw = nw_env == 4 || nw_env == 8 ? nw_env : (wg8 >= 256 ? 8 : 4);
+  const int nw = wg8 >= 256 ? 8 : 4;
   const int nqb = (int)((Sq + 32 * nw - 1) / (32 * nw));
   const dim3 grid((unsigned)(causal ? (nqb + 1) / 2 : nqb), (unsigned)(B * Hq));
   const float sl2 = (float)(scale * 1.4426950408889634);
@@ -798,26 +794,13 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
     if (D == 128) go(fa_bwd_pre_kernel<128>, 16); else go(fa_bwd_pre_kernel<64>, 8);
   }
   const float sl2 = (float)(scale * 1.4426950408889634), sc = (float)scale;
-  static const int kw_env = [] {
-    const char* e = std::getenv("XDDP_FA_DKDV_KW");
-    return e ? std::atoi(e) : 0;  // 0 = by shape
-  }();
-  // short non-causal D = 64 sequences (ViT): the whole key range in one 8-wave block
-  // (XDDP_FA_DKDV_KW=4 keeps two 128-key blocks), which then also computes dQ
-  // (XDDP_FA_FUSED_DQ=0: the separate dQ pass instead)
-  const int kwv = kw_env == 2 || kw_env == 4 ? kw_env : (D == 64 && !causal && Sk <= 256 ? 8 : 4);
-  static const bool fdq_env = [] {
-    const char* e = std::getenv("XDDP_FA_FUSED_DQ");
-    return !(e && std::atoi(e) == 0);
-  }();
-  const bool fused_dq = kwv == 8 && fdq_env;
+  // short non-causal D = 64 sequences (ViT): the whole key range in one 8-wave block, which then
+  // also computes dQ (r2: measured faster than two 128-key blocks + the separate dQ pass)
+  const int kwv = D == 64 && !causal && Sk <= 256 ? 8 : 4;
+  const bool fused_dq = kwv == 8;
   if (!fused_dq) {
-    static const int nw_env = [] {
-      const char* e = std::getenv("XDDP_FA_WAVES");
-      return e ? std::atoi(e) : 0;
-    }();
     const int64_t wg8 = ((Sq + 255) / 256) * B * Hq;
-    const int nw = nw_env == 4 || nw_env == 8 ? nw_env : (wg8 >= 256 ? 8 : 4);
+    const int nw = wg8 >= 256 ? 8 : 4;
     const int nqb = (int)((Sq + 32 * nw - 1) / (32 * nw));
     const dim3 grid((unsigned)(causal ? (nqb + 1) / 2 : nqb), (unsigned)(B * Hq));
     auto go = [&](auto kern) {
@@ -837,14 +820,9 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
   }
   {
     const int nkb = (int)((Sk + 32 * kwv - 1) / (32 * kwv));
-    // GQA head split for causal attention (balance, see the kernel); XDDP_FA_DKDV_SPLIT overrides
-    static const int split_env = [] {
-      const char* e = std::getenv("XDDP_FA_DKDV_SPLIT");
-      return e ? std::atoi(e) : 0;
-    }();
+    // GQA head split for causal attention (balance, see the kernel)
     const int grp = (int)(Hq / Hkv);
     int nsplit = causal ? grp : 1;
-    if (split_env > 0) nsplit = split_env;
     if (nsplit < 1 || grp % nsplit != 0) nsplit = 1;
     at::Tensor wsk, wsv;
     if (nsplit > 1) {
@@ -864,12 +842,9 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
                          strides_of(dq));
       XDDP_HIP_CHECK(hipGetLastError());
     };
-#define XDDP_FA(D_, C_) \
-  if (kwv == 4) go(fa_bwd_dkdv_kernel<D_, C_, 4>); else go(fa_bwd_dkdv_kernel<D_, C_, 2>)
-    if (D == 128) { if (causal) { XDDP_FA(128, true); } else { XDDP_FA(128, false); } }
-    else if (kwv == 8) { if (fused_dq) go(fa_bwd_dkdv_kernel<64, false, 8, true>); else go(fa_bwd_dkdv_kernel<64, false, 8>); }
-    else { if (causal) { XDDP_FA(64, true); } else { XDDP_FA(64, false); } }
-#undef XDDP_FA
+    if (D == 128) { if (causal) go(fa_bwd_dkdv_kernel<128, true, 4>); else go(fa_bwd_dkdv_kernel<128, false, 4>); }
+    else if (kwv == 8) go(fa_bwd_dkdv_kernel<64, false, 8, true>);
+    else { if (causal) go(fa_bwd_dkdv_kernel<64, true, 4>); else go(fa_bwd_dkdv_kernel<64, false, 4>); }
     if (nsplit > 1) {  // the split-sum writes dense [B, Sk, Hkv, D]: strided outputs get a copy
       const int64_t n8 = B * Sk * Hkv * D / 8;
       auto dkc = dk.is_contiguous() ? dk : at::empty({B, Sk, Hkv, D}, k.options());

@@ -264,12 +264,8 @@ std::vector<at::Tensor> bias_grad(const at::Tensor& g, const c10::optional<at::T
   const int cpr = (int)(N / 8);
   // each thread sums rows / rgroups rows of its column chunk. With GELU the pass also evaluates
   // erf + exp per element and is latency/ALU-limited at 128K threads (8 waves per CU: 283 us,
-  // 4.4 TB/s on ViT-L/16's [50432, 4096]); 512K threads fill the CUs (XDDP_BIAS_GRAD_THREADS)
-  static const int64_t target_gelu = [] {
-    const char* e = std::getenv("XDDP_BIAS_GRAD_THREADS");
-    return e ? std::max<int64_t>(1024, std::atoll(e)) : (int64_t)524288;
-  }();
-  const int64_t target = gelu ? target_gelu : 131072;
+  // 4.4 TB/s on ViT-L/16's [50432, 4096]); 512K threads fill the CUs
+  const int64_t target = gelu ? 524288 : 131072;
   const int rgroups = (int)std::max<int64_t>(1, std::min<int64_t>(rows, (target + cpr - 1) / cpr));
   auto part = at::empty({rgroups, N}, g.options().dtype(at::kFloat));
   if (rows == 0) {

@@ -29,6 +29,7 @@ import os
 import torch
 
 from .._native import load
+from .linear import own_gemm_mode
 
 __all__ = ["encoder_block", "encoder_block_supported"]
 
@@ -60,7 +61,7 @@ class _EncoderBlockFn(torch.autograd.Function):
         dh = D // heads
         scale = 1.0 / math.sqrt(dh)
         x2 = x.reshape(-1, D).contiguous()
-        own = _own_gemm(D, w_1.shape[0])
+        own = _own_gemm(D, w_1.shape[0], backward=False)
         y1, mean1, rstd1, xb = C.ln_forward(x2, ln1_w, ln1_b, eps1, False, b_o)
         qkv = C.gemm_nt(y1, w_qkv, b_qkv, 1)[0] if own else torch.addmm(b_qkv, y1, w_qkv.t())
         q5 = qkv.view(B, S, 3, heads, dh)
@@ -92,7 +93,7 @@ class _EncoderBlockFn(torch.autograd.Function):
         heads, dh = ctx.heads, D // ctx.heads
         g2 = g.reshape(-1, D).contiguous()
         # MLP
-        if _own_gemm(D, w_1.shape[0]):  # dh = (g·W_2)·gelu'(h) and Σ dh in the dgrad GEMM's epilogue
+        if _own_gemm(D, w_1.shape[0], backward=True):  # dh = (g·W_2)·gelu'(h), Σ dh in the GEMM epilogue
             dhid, db_1 = C.gemm_nt(g2, w_2.t().contiguous(), b_1, 4, h)
         else:
             db_1, dhid = C.bias_grad(torch.mm(g2, w_2), h, b_1)
@@ -117,12 +118,14 @@ class _EncoderBlockFn(torch.autograd.Function):
                 None, None, None)
 
 
-def _own_gemm(D: int, hidden: int) -> bool:
-    """Forward projections and fc2's input gradient on the own LDS-DMA MFMA GEMM
-    (csrc/kernels/gemm.hip) with the bias, bias+GELU, residual and dGELU+bias-gradient epilogues
-    fused; XDDP_OWN_GEMM=0 keeps hipBLASLt (addmm / mm) + the separate GELU passes (A/B switch)."""
-    return (os.environ.get("XDDP_OWN_GEMM", "1") != "0" and D % 128 == 0 and hidden % 128 == 0
-            and (3 * D) % 128 == 0)
+def _own_gemm(D: int, hidden: int, backward: bool) -> bool:
+    """Own LDS-DMA MFMA GEMM (csrc/kernels/gemm.hip) for this block? Forward projections (bias,
+    bias+GELU and residual epilogues) only with XDDP_OWN_GEMM=1; fc2's input gradient with the
+    dGELU + bias-gradient epilogue also with the default ``bwd`` (ops/linear.own_gemm_mode)."""
+    mode = own_gemm_mode()
+    if mode == "0" or (mode == "bwd" and not backward):
+        return False
+    return D % 128 == 0 and hidden % 128 == 0 and (3 * D) % 128 == 0
 
 
 def encoder_block(x: torch.Tensor, blk) -> torch.Tensor:

@@ -4,7 +4,14 @@ pre-norm block's skip connection added in the GEMM epilogue instead of a separat
 on the LDS-DMA MFMA kernel; the backward's ``dX = dY·W`` and ``dW = dYᵀ·X`` stay on hipBLASLt.
 
 The module structure is untouched (``nn.Linear`` parameters), so state_dicts and DDP buckets are
-the same as the eager model's. ``XDDP_OWN_GEMM=0`` keeps ``F.linear`` (A/B switch).
+the same as the eager model's.
+
+``XDDP_OWN_GEMM`` selects where the own GEMM runs: ``1`` every supported projection (forward
+epilogues included), ``bwd`` (default) only the backward GEMM that carries a fused epilogue
+hipBLASLt cannot do (the ViT MLP's dGELU + bias gradient), ``0`` nowhere. On one MI355X the own
+kernel reaches 0.80-0.93x hipBLASLt's plain-GEMM speed on the transformer shapes
+(``profiles/r3_gemm_nt_vs_hipblaslt_v4.txt``), so forward projections stay on hipBLASLt, whose
+beta = 1 residual accumulate is free, unless asked for.
 """
 from __future__ import annotations
 
@@ -16,11 +23,17 @@ import torch.nn.functional as F
 
 from .._native import load
 
-__all__ = ["linear", "own_gemm_ok"]
+__all__ = ["linear", "own_gemm_ok", "own_gemm_mode"]
+
+
+def own_gemm_mode() -> str:
+    """``XDDP_OWN_GEMM``: ``"1"`` (all), ``"bwd"`` (fused-epilogue backward GEMMs only, default) or ``"0"``."""
+    v = os.environ.get("XDDP_OWN_GEMM", "bwd")
+    return v if v in ("0", "1", "bwd") else "bwd"
 
 
 def own_gemm_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
-    if os.environ.get("XDDP_OWN_GEMM", "1") == "0" or torch.is_autocast_enabled():
+    if own_gemm_mode() != "1" or torch.is_autocast_enabled():
         return False
     N, K = weight.shape
     return (x.is_cuda and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and K % 64 == 0

@@ -23,17 +23,16 @@ def main():
     ev = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows))
     ar = [(s, e) for s, e, n in ev if "oneRankReduce" in n or "ncclDevKernel" in n]
     adam = [(s, e) for s, e, n in ev if "adam_kernel" in n]
-    # iterations: all-reduces separated by a gap longer than the longest all-reduce of the run
-    # (between two backward passes there is a forward and the loss)
+    # iterations: all-reduces separated by more than 20 ms (between two backward passes there is
+    # a forward and the loss; inside a backward the buckets follow each other within a few ms)
     lines = [f"# {os.path.basename(f)}: {len(ar)} all-reduce kernels, {len(adam)} AdamW update kernels"]
     if not ar:
         text = "\n".join(lines + ["no all-reduce kernels in the trace"]) + "\n"
         print(text)
         return
-    longest = max(e - s for s, e in ar)
     iters, cur = [], [ar[0]]
     for p, q in zip(ar, ar[1:]):
-        if q[0] - p[1] > max(5 * longest, 5_000_000):  # > 5 ms gap: next iteration
+        if q[0] - p[1] > 20_000_000:
             iters.append(cur)
             cur = []
         cur.append(q)
@@ -44,13 +43,18 @@ def main():
         return sum(max(0, min(x[1], e) - max(x[0], s)) for s, e in ys)
 
     lines.append(f"{'iter':>4s} {'allreduces':>10s} {'tail ms':>8s} {'AdamW kernels during tail':>26s} "
-                 f"{'AdamW ms under tail':>20s} {'AdamW before tail start':>24s}")
+                 f"{'AdamW ms under tail':>20s} {'AdamW before tail start':>24s} {'AdamW after tail end':>21s} "
+                 f"{'last AdamW end - tail end ms':>29s}")
     for i, it in enumerate(iters):
         tail = it[-1]
         during = [x for x in adam if x[0] < tail[1] and x[1] > tail[0]]
         before = [x for x in adam if x[1] <= tail[0] and x[0] >= it[0][0]]
+        nxt = iters[i + 1][0][0] if i + 1 < len(iters) else float("inf")
+        after = [x for x in adam if x[0] >= tail[1] and x[1] <= nxt]
+        last = max((x[1] for x in after), default=tail[1])
         lines.append(f"{i:4d} {len(it):10d} {(tail[1] - tail[0]) / 1e6:8.3f} {len(during):26d} "
-                     f"{overlap(tail, adam) / 1e6:20.3f} {len(before):24d}")
+                     f"{overlap(tail, adam) / 1e6:20.3f} {len(before):24d} {len(after):21d} "
+                     f"{(last - tail[1]) / 1e6:29.3f}")
     under_any = sum(overlap(x, ar) for x in adam)
     lines.append(f"AdamW kernel time {tot_adam / 1e6:.3f} ms, of which {under_any / 1e6:.3f} ms ran while an "
                  f"all-reduce kernel was executing")

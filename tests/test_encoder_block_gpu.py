@@ -103,7 +103,11 @@ def _run(blk, x, gout, fused_env):
             os.environ["XDDP_FUSED_BLOCK"] = old
 
 
-def test_fused_encoder_block_matches_fp32():
+@pytest.mark.parametrize("own", ["0", "bwd", "1"])
+def test_fused_encoder_block_matches_fp32(own, monkeypatch):
+    """The fused block on hipBLASLt only (0), with fc2's dgrad + dGELU + bias-gradient on the own
+    GEMM (bwd, default), and with every projection on the own GEMM (1)."""
+    monkeypatch.setenv("XDDP_OWN_GEMM", own)
     torch.manual_seed(3)
     D, H, MLP = 1024, 16, 4096
     blk32 = EncoderBlock(D, H, MLP, FusedLayerNorm).cuda()

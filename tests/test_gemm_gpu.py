@@ -68,15 +68,20 @@ def test_gemm_nt_rejects_bad_shapes():
         C.gemm_nt(a, w)
 
 
-def test_own_linear_autograd_matches_fp32():
-    """ops/linear.py: forward on gemm_nt (with the residual epilogue), backward on hipBLASLt."""
-    from distributeddataparallel_amd.ops.linear import linear
+def test_own_linear_autograd_matches_fp32(monkeypatch):
+    """ops/linear.py with XDDP_OWN_GEMM=1: forward on gemm_nt (with the residual epilogue),
+    backward on hipBLASLt."""
+    from distributeddataparallel_amd.ops.linear import linear, own_gemm_ok
+
+    monkeypatch.setenv("XDDP_OWN_GEMM", "1")
 
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.randn(2, 200, 512, device="cuda", generator=g).to(torch.bfloat16).requires_grad_(True)
     w = (torch.randn(768, 512, device="cuda", generator=g) * 512 ** -0.5).to(torch.bfloat16).requires_grad_(True)
     r = torch.randn(2, 200, 768, device="cuda", generator=g).to(torch.bfloat16).requires_grad_(True)
+    assert own_gemm_ok(x, w)
     y = linear(x, w, r)
+    assert y.grad_fn is not None and "_Linear" in type(y.grad_fn).__name__
     dy = torch.randn_like(y)
     y.backward(dy)
     xf, wf, rf = (t.detach().float().requires_grad_(True) for t in (x, w, r))
