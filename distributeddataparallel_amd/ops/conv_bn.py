@@ -418,7 +418,7 @@ def _conv3x3() -> bool:
 def _dgrad3_s2() -> bool:
     """XDDP_CONV3X3_DGRAD_S2=1 runs the stride-2 3x3 input gradient on the phase-grid kernel
     (conv3x3.hip DG2). Off by default: MIOpen is faster on all three ResNet-50 shapes, zero-fill
-    included (177/149/139 vs 185/168/169 us at bs256, scripts/dg2_bench.py,
+    included (177/149/139 vs 185/168/169 us at bs256, r2 measurement,
     profiles/r2_dg2_vs_miopen.txt) — the 1- and 2-tap phases are too short to fill the 3-stage
     pipeline of a one-block-per-CU tile."""
     return os.environ.get("XDDP_CONV3X3_DGRAD_S2", "0") == "1"
