@@ -9,7 +9,7 @@ in the workload launches); ``gpurun_out/pmc_r3_plan.json`` records, in launch or
 pattern, the call count and the analytic FLOPs / unique HBM bytes of one call, so
 ``scripts/pmc_summary.py`` can put each op's dispatches on the roofline.
 
-usage: python scripts/pmc_r3.py [--plan-out PATH]
+usage: python scripts/pmc_r3.py [--plan-out PATH] [--only-gemm]
 """
 import json
 import os
@@ -33,6 +33,8 @@ def bf(*shape, scale=1.0, fmt=cl):
 
 
 def run(label, pattern, flops, nbytes, fn):
+    if ONLY_GEMM and "gemm_nt" not in label and "hipBLASLt" not in label:
+        return
     fn()  # warm (first-call allocations, tuning) — not part of the plan
     torch.cuda.synchronize()
     plan.append({"label": label, "pattern": pattern, "calls": CALLS, "flops": float(flops), "bytes": float(nbytes)})
@@ -43,6 +45,7 @@ def run(label, pattern, flops, nbytes, fn):
     torch.cuda.synchronize()
 
 
+ONLY_GEMM = "--only-gemm" in sys.argv  # stall-counter passes over the transformer GEMMs alone
 B = 256
 # 3x3 forward (+ BN statistics epilogue) and the stride-1 input gradient (same kernel, rotated W)
 for cin, hw in ((64, 56), (128, 28), (256, 14)):
@@ -99,8 +102,10 @@ for name, M, K, N in (("8192^3", 8192, 8192, 8192), ("vit fc1", 12608, 1024, 409
     del a, w
 
 out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "pmc_r3_plan.json")
-if len(sys.argv) > 2 and sys.argv[1] == "--plan-out":
-    out = sys.argv[2]
+if "--plan-out" in sys.argv:
+    out = sys.argv[sys.argv.index("--plan-out") + 1]
+elif ONLY_GEMM:
+    out = out.replace("pmc_r3_plan.json", "pmc_r3_gemm_plan.json")
 os.makedirs(os.path.dirname(out), exist_ok=True)
 with open(out, "w") as fh:
     json.dump(plan, fh, indent=1)

@@ -116,6 +116,18 @@ def main():
         lb = f"{c['SQ_LDS_IDX_ACTIVE'] / cu_cyc:7.3f}" if cu_cyc and "SQ_LDS_IDX_ACTIVE" in c else f"{'-':>7s}"
         lines.append(f"{e['label']:38s} {us:8.1f} {tf:7.1f} {100 * tf / PEAK_TF:5.1f} {mf} {ldss} "
                      f"{hbm / 1e6:8.1f} {tbs:5.2f} {ai:6.0f} {100 * tf / roof:6.1f} {mb} {lb}  {bound} ({src} bytes)")
+    # stall counters (a pass of their own): fractions of the op's wave-cycles
+    stall = ["SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_LDS_DATA_FIFO_FULL", "SQ_LDS_CMD_FIFO_FULL"]
+    if any(c.get("SQ_WAVE_CYCLES") and any(k in c for k in stall) for c in counters):
+        lines.append("")
+        lines.append(f"{'op':38s} " + " ".join(f"{k.replace('SQ_', '').lower():>18s}" for k in stall)
+                     + "   (per wave-cycle)")
+        for i, e in enumerate(plan):
+            c = counters[i]
+            if not c.get("SQ_WAVE_CYCLES"):
+                continue
+            lines.append(f"{e['label']:38s} " + " ".join(
+                f"{c[k] / c['SQ_WAVE_CYCLES']:18.3f}" if k in c else f"{'-':>18s}" for k in stall))
     text = "\n".join(lines) + "\n"
     print(text)
     if a.out:
