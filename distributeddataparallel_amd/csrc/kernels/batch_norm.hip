@@ -386,7 +386,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
                                                               int64_t M, const W* __restrict__ weight,
                                                               const float* __restrict__ invstd, W* dweight,
                                                               W* dbias, float* __restrict__ coef,
-                                                              const float* __restrict__ fold_mean) {
+                                                              const float* __restrict__ fold_mean,
+                                                              const float* __restrict__ ss_copy = nullptr) {
   __shared__ float red[4][16];
   const int cv = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   float acc[16];
@@ -424,6 +425,11 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   coef[2 * C + c] = -g * inv * sd * invM;              // k3
   // fold_mean: dx = k1·g + k2·x + (k3 - k2·mean), the form a consumer GEMM prologue applies
   if (fold_mean) coef[2 * C + c] -= coef[C + c] * fold_mean[c];
+  // ss_copy: rows 3-4 carry the forward scale / shift (the consumer recomputes the ReLU mask)
+  if (ss_copy) {
+    coef[3 * C + c] = ss_copy[c];
+    coef[4 * C + c] = ss_copy[C + c];
+  }
 }
 
 template <typename T, int MASK, bool DRES, bool DUAL>
@@ -756,13 +762,11 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
                          has_w ? reinterpret_cast<const W*>(weight->data_ptr()) : nullptr, invstd.data_ptr<float>(),
                          dw.defined() ? reinterpret_cast<W*>(dw.data_ptr()) : nullptr,
                          db.defined() ? reinterpret_cast<W*>(db.data_ptr()) : nullptr, coef.data_ptr<float>(),
-                         coef_only ? mean.data_ptr<float>() : nullptr);
+                         coef_only ? mean.data_ptr<float>() : nullptr,
+                         coef_only && coef_mask ? ss->data_ptr<float>() : nullptr);
       XDDP_HIP_CHECK(hipGetLastError());
       const int64_t nvec = M * C / 8;
       if (coef_only) {  // nothing more: the consumer applies the coefficients
-        if (coef_mask)
-          XDDP_HIP_CHECK(hipMemcpyAsync(coef.data_ptr<float>() + 3 * C, ss->data_ptr<float>(), 2 * C * sizeof(float),
-                                        hipMemcpyDeviceToDevice, stream));
       } else if (wg) {
         hipLaunchKernelGGL((bn_bwd_elem_kernel<T, 0, false, false>), dim3(elem_grid(nvec)), dim3(kBlock), 0, stream,
                            reinterpret_cast<const T*>(dres.data_ptr()), nullptr,
