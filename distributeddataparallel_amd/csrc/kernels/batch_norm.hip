@@ -648,7 +648,8 @@ at::Tensor bn_grad_partials(const at::Tensor& dy_in, const at::Tensor& x, const 
 std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, const c10::optional<at::Tensor>& residual,
                                  bool relu, bool save_mask, const c10::optional<at::Tensor>& num_batches_tracked,
                                  const c10::optional<at::Tensor>& residual_ss,
-                                 const c10::optional<at::Tensor>& residual_nbt) {
+                                 const c10::optional<at::Tensor>& residual_nbt, const c10::optional<at::Tensor>& out,
+                                 const c10::optional<at::Tensor>& out_bits) {
   check_nhwc(x);
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), Wd = x.size(3);
   TORCH_CHECK(ss.is_cuda() && ss.scalar_type() == at::kFloat && ss.numel() == 2 * C && ss.is_contiguous(),
@@ -663,9 +664,20 @@ std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, cons
     TORCH_CHECK(has_res && residual_ss->is_cuda() && residual_ss->scalar_type() == at::kFloat &&
                     residual_ss->numel() == 2 * C && residual_ss->is_contiguous(),
                 "bn_apply: residual scale/shift must be float [2, C] with a residual");
-  auto y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
-  at::Tensor mask_bits = (relu && save_mask) ? at::empty({N * H * Wd * C / 8}, x.options().dtype(at::kByte))
-                                             : at::Tensor();
+  // out / out_bits: write into given tensors (a deferred apply whose output tensor already exists)
+  const bool has_out = out.has_value() && out->defined();
+  if (has_out)
+    TORCH_CHECK(out->sizes() == x.sizes() && out->scalar_type() == x.scalar_type() &&
+                    out->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "bn_apply: out must match x (shape, dtype, channels_last)");
+  auto y = has_out ? *out : at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  const bool has_obits = out_bits.has_value() && out_bits->defined();
+  if (has_obits)
+    TORCH_CHECK(relu && save_mask && out_bits->scalar_type() == at::kByte && out_bits->numel() * 8 == x.numel(),
+                "bn_apply: out_bits must be uint8 with one byte per 8 elements (relu, save_mask)");
+  at::Tensor mask_bits = has_obits ? *out_bits
+                         : (relu && save_mask) ? at::empty({N * H * Wd * C / 8}, x.options().dtype(at::kByte))
+                                               : at::Tensor();
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
   const int64_t nvec = N * H * Wd * C / 8;
   int64_t* nbt_inc = (num_batches_tracked.has_value() && num_batches_tracked->defined())

@@ -77,6 +77,21 @@ struct EpiBN {
   int add_h, add_w;
 };
 
+// Prologue side output (PRO 1, 4, 5; forward, stride 1): the staged operand op(X) IS a BatchNorm
+// apply's output — BN2's relu(y2·s + t) for a bottleneck's conv3, or a block's final
+// relu(y3·s + t + r) for the next block's conv1 — so the blocks of N-tile 0 also store it (and,
+// for PRO 4/5, its ReLU bit mask in bn_apply's byte-per-8-channels layout) instead of a separate
+// apply pass writing it and this GEMM reading it back. rss: PRO 5's residual is a downsample's raw
+// conv output whose BN apply (bf16(r·rs + rh), as that BN's own apply would store it) is folded in
+// too. nbt1 / nbt2: the applied BNs' num_batches_tracked, bumped once by block 0.
+struct ProOut {
+  uint16_t* out;
+  uint8_t* bits;
+  const float* rss;
+  int64_t* nbt1;
+  int64_t* nbt2;
+};
+
 struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every stride-th pixel)
   int OH, OW, IH, IW, stride;
   template <bool STRIDED>
@@ -92,7 +107,9 @@ struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every st
 // PRO: 0 = plain A; 1 = relu(A·s_k + b_k) (the previous BN's apply); 2 = a_k·A + b_k·X2 + c_k, the
 // BatchNorm-backward elementwise pass (A = masked upstream gradient, X2 = the BN input) folded
 // into the input-gradient GEMM so that gradient is never written to HBM; 3 = as 2 with the BN's
-// ReLU mask recomputed in registers: A -> (X2·s_k + t_k > 0) ? A : 0.
+// ReLU mask recomputed in registers: A -> (X2·s_k + t_k > 0) ? A : 0; 4 = relu(A·s_k + t_k + X2)
+// (a bottleneck's final BN + residual + ReLU, X2 = the identity); 5 = as 4 with the identity a
+// deferred downsample BN's raw output, X2 -> bf16(X2·rs_k + rh_k) (ProOut::rss).
 // BT: the B operand is given K-major (Wt[k][n], e.g. the forward weight W[n_out][k_in] used as Wᵀ by
 // the input-gradient GEMM): staged as [64 k][BN n] rows (padded 32 B) and read into fragments with
 // the transposing ds_read_b64_tr_b16, so no transposed weight copy is made.
@@ -104,7 +121,8 @@ template <int BM, int BN, int WM, int WN, int PRO, bool STATS, bool STRIDED, boo
 __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, int64_t M, int N,
     int K, RowMap rm, const float* __restrict__ pro_ss, float* __restrict__ part, int mtiles, int ntiles,
-    int groups, const uint16_t* __restrict__ X2, EpiBN epi) {
+    int groups, const uint16_t* __restrict__ X2, EpiBN epi, ProOut po) {
+  static_assert(PRO < 4 || (!STRIDED && !BT && !EPI), "the block-output prologue is a stride-1 forward");
   constexpr int NT = 64 * WM * WN, RSTEP = NT / 8;  // threads; rows staged per pass (8 chunks per row)
   constexpr int AR = BM / RSTEP, BR = BN / RSTEP;    // 16-B loads per thread per operand tile
   constexpr int WTM = BM / WM, WTN = BN / WN;        // wave tile
@@ -151,7 +169,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
   // two operand buffers (kept out of the VGPRs that the MFMA phase needs)
   float* pro_lds = reinterpret_cast<float*>(smem + 2 * BUF);
   // EPI mask-recompute form: this N tile's (scale, shift) of the masked BN, after the coefficients
-  float* epi_ss_lds = pro_lds + (PRO == 3 ? 5 : PRO == 2 ? 3 : PRO == 1 ? 2 : 0) * K;
+  constexpr int NCOEF = PRO == 3 ? 5 : PRO == 2 ? 3 : PRO == 5 ? 4 : PRO ? 2 : 0;
+  float* epi_ss_lds = pro_lds + NCOEF * K;
   // EPI: and this N tile's mean of the previous BN (the shift of the st_ss products; LDS, not VGPRs)
   float* epi_mu_lds = epi_ss_lds + 2 * BN;
   if (EPI && epi.ss) {
@@ -161,9 +180,17 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
     for (int i = tid; i < BN; i += NT) epi_mu_lds[i] = epi.mean[n0 + i];
   }
   if (PRO) {
-    for (int i = tid; i < (PRO == 3 ? 5 : PRO == 2 ? 3 : 2) * K; i += NT) pro_lds[i] = pro_ss[i];
+    for (int i = tid; i < (PRO == 5 ? 2 : NCOEF) * K; i += NT) pro_lds[i] = pro_ss[i];
+    if (PRO == 5)
+      for (int i = tid; i < 2 * K; i += NT) pro_lds[2 * K + i] = po.rss[i];
   }
   if (PRO || EPI) lds_barrier();
+  // side output of the staged operand (uniform per block: N-tile 0 writes it, once per element)
+  const bool side = (PRO == 1 || PRO >= 4) && po.out != nullptr && nt == 0;
+  if ((PRO == 1 || PRO >= 4) && wg == 0 && tid == 0) {
+    if (po.nbt1) po.nbt1[0] += 1;
+    if (po.nbt2) po.nbt2[0] += 1;
+  }
   const uint16_t* arow[AR];
   const int64_t dx2 = PRO >= 2 ? X2 - X : 0;  // the second A source at the same element offsets
   // Rows past M load row M-1 (clamped, branch-free: a per-row "load or zero" select makes hipcc
@@ -189,7 +216,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
   auto store = [&](int buf, int kt) {
     uint8_t* A = smem + buf * BUF;
     uint8_t* B = A + ABYTES;
-    if (PRO >= 2) {  // BN backward on this thread's 8 channels: a·g + b·x + c (g masked by ReLU for 3)
+    if (PRO == 2 || PRO == 3) {  // BN backward on this thread's 8 channels: a·g + b·x + c (g masked by ReLU for 3)
       // coefficients two channels at a time (float2 LDS reads): few live VGPRs in this phase
       const int k0 = kt * kBK + lc * 8;
 #pragma unroll
@@ -227,6 +254,42 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
           const float hi = fmaxf(fmaf(__uint_as_float(sa[i][q] & 0xffff0000u), sc[2 * q + 1], sh[2 * q + 1]), 0.f);
           sa[i][q] = dev::pack_bf16x2(lo, hi);
         }
+      }
+    }
+    uint32_t mbits[PRO >= 4 ? AR : 1];
+    if (PRO >= 4) {  // block output: relu(y·s + t + r) on this thread's 8 channels, plus its mask bits
+      const int k0 = kt * kBK + lc * 8;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) mbits[i] = 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float2 sc = *reinterpret_cast<const float2*>(pro_lds + k0 + 2 * q);
+        const float2 sh = *reinterpret_cast<const float2*>(pro_lds + K + k0 + 2 * q);
+        float2 rs = {1.f, 1.f}, rh = {0.f, 0.f};
+        if (PRO == 5) {
+          rs = *reinterpret_cast<const float2*>(pro_lds + 2 * K + k0 + 2 * q);
+          rh = *reinterpret_cast<const float2*>(pro_lds + 3 * K + k0 + 2 * q);
+        }
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+          float r0 = __uint_as_float(sa2[i][q] << 16), r1 = __uint_as_float(sa2[i][q] & 0xffff0000u);
+          if (PRO == 5) {  // the downsample's BN apply, at storage precision (bn_apply_kernel's rss)
+            r0 = bf16_round(fmaf(r0, rs.x, rh.x));
+            r1 = bf16_round(fmaf(r1, rs.y, rh.y));
+          }
+          const float o0 = fmaf(__uint_as_float(sa[i][q] << 16), sc.x, sh.x) + r0;
+          const float o1 = fmaf(__uint_as_float(sa[i][q] & 0xffff0000u), sc.y, sh.y) + r1;
+          mbits[i] |= ((o0 > 0.f ? 1u : 0u) | (o1 > 0.f ? 2u : 0u)) << (2 * q);
+          sa[i][q] = dev::pack_bf16x2(fmaxf(o0, 0.f), fmaxf(o1, 0.f));
+        }
+      }
+    }
+    if (side) {
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const int64_t e = (arow[i] - X) + (int64_t)kt * kBK;  // element offset of this 8-channel chunk
+        *reinterpret_cast<u32x4*>(po.out + e) = sa[i];
+        if (PRO >= 4 && po.bits) po.bits[e >> 3] = (uint8_t)mbits[PRO >= 4 ? i : 0];
       }
     }
 #pragma unroll
@@ -963,7 +1026,7 @@ int num_cus() {
 template <int BM, int BN, int WM, int WN, int OCC>
 void launch_gemm(int pro, bool stats, bool bt, dim3 grid, size_t lds, hipStream_t s, const uint16_t* x,
                  const uint16_t* w, uint16_t* y, int64_t M, int N, int K, RowMap rm, const float* pss, float* part,
-                 int mt, int nt, int groups, const uint16_t* x2, const EpiBN& epi) {
+                 int mt, int nt, int groups, const uint16_t* x2, const EpiBN& epi, const ProOut& po) {
   auto go = [&](auto kern) {
     static size_t lds_set = 0;  // per kernel instantiation: opt in to > 64 KB of dynamic LDS once
     if (lds > 65536 && lds > lds_set) {
@@ -971,7 +1034,7 @@ void launch_gemm(int pro, bool stats, bool bt, dim3 grid, size_t lds, hipStream_
       lds_set = lds;
     }
     hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, s, x, w, y, M, N, K, rm, pss, part, mt, nt, groups, x2,
-                       epi);
+                       epi, po);
   };
 #define XDDP_G(P, S)                                                                                       \
   if (rm.stride > 1) go(conv1x1_gemm_kernel<BM, BN, WM, WN, P, S, true, false, false, OCC>);                \
@@ -1000,7 +1063,10 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
                                      const c10::optional<at::Tensor>& prologue_y, bool w_t,
                                      const c10::optional<at::Tensor>& epi_add, const c10::optional<at::Tensor>& epi_y,
                                      const c10::optional<at::Tensor>& epi_bits, const c10::optional<at::Tensor>& epi_mean,
-                                     const c10::optional<at::Tensor>& epi_ss, int64_t epi_add_stride) {
+                                     const c10::optional<at::Tensor>& epi_ss, int64_t epi_add_stride,
+                                     const c10::optional<at::Tensor>& pro_out, const c10::optional<at::Tensor>& pro_bits,
+                                     const c10::optional<at::Tensor>& pro_res, const c10::optional<at::Tensor>& pro_res_ss,
+                                     const c10::optional<at::Tensor>& pro_nbt, const c10::optional<at::Tensor>& pro_res_nbt) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == at::kBFloat16, "conv1x1_gemm: x must be 4-D bf16 on GPU");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv1x1_gemm: x must be channels_last");
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 1 && w.size(3) == 1 && w.scalar_type() == at::kBFloat16,
@@ -1017,12 +1083,38 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 31), "conv1x1_gemm: bad M");
   const bool has_y2 = prologue_y.has_value() && prologue_y->defined();
   const bool has_ss = prologue_ss.has_value() && prologue_ss->defined();
-  const int pro = has_y2 ? (has_ss && prologue_ss->numel() == 5 * K ? 3 : 2) : (has_ss ? 1 : 0);
-  const int ncoef = pro == 3 ? 5 : pro == 2 ? 3 : 2;
+  auto def = [](const c10::optional<at::Tensor>& t) { return t.has_value() && t->defined(); };
+  const bool has_res = def(pro_res), has_rss = def(pro_res_ss);
+  const int pro = has_res ? (has_rss ? 5 : 4)
+                          : has_y2 ? (has_ss && prologue_ss->numel() == 5 * K ? 3 : 2) : (has_ss ? 1 : 0);
+  const int ncoef = pro == 3 ? 5 : pro == 2 ? 3 : 2;  // (PRO 5's residual coefficients come in pro_res_ss)
+  if (has_res || def(pro_out) || def(pro_bits)) {
+    TORCH_CHECK(!has_y2 && !w_t && stride == 1 && !(epi_add.has_value() && epi_add->defined()) &&
+                    !(epi_ss.has_value() && epi_ss->defined()),
+                "conv1x1_gemm: the apply prologue's side output / residual is for stride-1 forwards");
+    TORCH_CHECK(has_ss, "conv1x1_gemm: the apply prologue needs prologue_ss");
+    if (has_res)
+      TORCH_CHECK(pro_res->sizes() == x.sizes() && pro_res->scalar_type() == at::kBFloat16 &&
+                      pro_res->is_contiguous(at::MemoryFormat::ChannelsLast),
+                  "conv1x1_gemm: pro_res must match x (bf16 channels_last)");
+    if (has_rss)
+      TORCH_CHECK(pro_res_ss->is_cuda() && pro_res_ss->scalar_type() == at::kFloat && pro_res_ss->numel() == 2 * K &&
+                      pro_res_ss->is_contiguous(),
+                  "conv1x1_gemm: pro_res_ss must be float [2, K]");
+    if (def(pro_out))
+      TORCH_CHECK(pro_out->sizes() == x.sizes() && pro_out->scalar_type() == at::kBFloat16 &&
+                      pro_out->is_contiguous(at::MemoryFormat::ChannelsLast),
+                  "conv1x1_gemm: pro_out must match x (bf16 channels_last)");
+    if (def(pro_bits))
+      TORCH_CHECK(has_res && def(pro_out) && pro_bits->scalar_type() == at::kByte && pro_bits->numel() * 8 == x.numel(),
+                  "conv1x1_gemm: pro_bits needs the residual form and pro_out (uint8, one byte per 8 elements)");
+    for (const auto* t : {&pro_nbt, &pro_res_nbt})
+      if (def(*t)) TORCH_CHECK((*t)->scalar_type() == at::kLong && (*t)->numel() == 1, "conv1x1_gemm: bad nbt");
+  }
   if (pro) TORCH_CHECK(has_ss && prologue_ss->scalar_type() == at::kFloat && prologue_ss->numel() == ncoef * K &&
                            prologue_ss->is_contiguous(),
                        "conv1x1_gemm: prologue coefficients must be float [2, K] (or [3|5, K] with prologue_y)");
-  if (pro >= 2)
+  if (pro == 2 || pro == 3)
     TORCH_CHECK(prologue_y->sizes() == x.sizes() && prologue_y->scalar_type() == at::kBFloat16 &&
                     prologue_y->is_contiguous(at::MemoryFormat::ChannelsLast) && stride == 1 && !stats,
                 "conv1x1_gemm: prologue_y must match x (bf16 channels_last), stride 1, no stats");
@@ -1063,7 +1155,11 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   //   epilogue loads stay live across the K loop and spill 76 registers within the 128 of
   //   occupancy 4 (331/189/105/78 vs 614/334/200/96 us, 11,969 vs 10,915 img/s);
   // * everything else at occupancy 4, persistent grid of 2 blocks per CU (one resident round).
-  const bool bm64 = epi_on && BN == 128;
+  // * the block-output prologue (pro 4 / 5: two A sources, the mask bits and the statistics live
+  //   together) on 128-wide N tiles runs 64-row tiles at occupancy 4 (its 128-row tile spills
+  //   35-41 registers there); on 64-wide N tiles the 128-row tile fits (124 VGPRs), the same tile
+  //   and grid as the plain statistics GEMM, so those statistics partials are bitwise the same
+  const bool bm64 = (epi_on && BN == 128) || (pro >= 4 && BN == 128);
   const int BM = bm64 ? 64 : 128;
   const int mtiles = (int)((M + BM - 1) / BM), ntiles = (int)(N / BN);
   const int kocc = bm64 ? 4 : (epi_on ? 2 : 4);
@@ -1083,9 +1179,15 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   RowMap rm{(int)OH, (int)OW, (int)IH, (int)IW, (int)stride};
   const dim3 grid(groups * ntiles);
   const size_t bbytes = w_t ? (size_t)64 * (BN * 2 + 32) : (size_t)BN * 128;
-  const size_t lds = 2 * ((size_t)BM * 128 + bbytes) + (pro ? ncoef * K * sizeof(float) : 0) +
+  const size_t lds = 2 * ((size_t)BM * 128 + bbytes) + (pro ? (pro == 5 ? 4 : ncoef) * K * sizeof(float) : 0) +
                      (epi_on ? 3 * (size_t)BN * sizeof(float) : 0);
-  const auto* x2p = pro >= 2 ? reinterpret_cast<const uint16_t*>(prologue_y->data_ptr()) : nullptr;
+  const auto* x2p = pro >= 4 ? reinterpret_cast<const uint16_t*>(pro_res->data_ptr())
+                   : pro >= 2 ? reinterpret_cast<const uint16_t*>(prologue_y->data_ptr()) : nullptr;
+  const ProOut po{def(pro_out) ? reinterpret_cast<uint16_t*>(pro_out->data_ptr()) : nullptr,
+                  def(pro_bits) ? pro_bits->data_ptr<uint8_t>() : nullptr,
+                  has_rss ? pro_res_ss->data_ptr<float>() : nullptr,
+                  def(pro_nbt) ? pro_nbt->data_ptr<int64_t>() : nullptr,
+                  def(pro_res_nbt) ? pro_res_nbt->data_ptr<int64_t>() : nullptr};
   const auto* xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
   const auto* wp = reinterpret_cast<const uint16_t*>(wc.data_ptr());
   auto* yp = reinterpret_cast<uint16_t*>(y.data_ptr());
@@ -1093,12 +1195,30 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
   float* pp = stats ? part.data_ptr<float>() : nullptr;  // (EPI partials travel in epi)
 #define XDDP_LG(BN_, WM_, WN_, OCC_)                                                                            \
   launch_gemm<128, BN_, WM_, WN_, OCC_>(pro, stats, w_t, grid, lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, \
-                                        mtiles, ntiles, groups, x2p, epi)
-  if (bm64) {  // (EPI implies w_t; pro is 0 or the BN-backward form 2)
+                                        mtiles, ntiles, groups, x2p, epi, po)
+  if (pro >= 4) {
+    auto go = [&](auto kern) {
+      static size_t lds_set = 0;
+      if (lds > 65536 && lds > lds_set) {
+        XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        lds_set = lds;
+      }
+      hipLaunchKernelGGL(kern, grid, dim3(512), lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,
+                         groups, x2p, epi, po);
+    };
+#define XDDP_P45(BM_, BN_, WM_, WN_)                                                                     \
+    if (pro == 5) { if (stats) go(conv1x1_gemm_kernel<BM_, BN_, WM_, WN_, 5, true, false, false, false, 4>);    \
+                    else go(conv1x1_gemm_kernel<BM_, BN_, WM_, WN_, 5, false, false, false, false, 4>); }   \
+    else { if (stats) go(conv1x1_gemm_kernel<BM_, BN_, WM_, WN_, 4, true, false, false, false, 4>);             \
+           else go(conv1x1_gemm_kernel<BM_, BN_, WM_, WN_, 4, false, false, false, false, 4>); }
+    if (BN == 128) { XDDP_P45(64, 128, 2, 4) } else { XDDP_P45(128, 64, 8, 1) }
+#undef XDDP_P45
+    XDDP_HIP_CHECK(hipGetLastError());
+  } else if (bm64) {  // (EPI implies w_t; pro is 0 or the BN-backward form 2)
     auto kern = pro == 2 ? conv1x1_gemm_kernel<64, 128, 2, 4, 2, false, false, true, true, 4>
                          : conv1x1_gemm_kernel<64, 128, 2, 4, 0, false, false, true, true, 4>;
     hipLaunchKernelGGL(kern, grid, dim3(512), lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,
-                       groups, x2p, epi);
+                       groups, x2p, epi, po);
     XDDP_HIP_CHECK(hipGetLastError());
   } else if (BN == 128) { if (kocc == 2) XDDP_LG(128, 4, 2, 2); else XDDP_LG(128, 4, 2, 4); }
   else { if (kocc == 2) XDDP_LG(64, 8, 1, 2); else XDDP_LG(64, 8, 1, 4); }

@@ -26,14 +26,18 @@ at::Tensor bn_grad_partials(const at::Tensor& dy, const at::Tensor& x, const at:
 std::vector<at::Tensor> bn_apply(const at::Tensor& x, const at::Tensor& ss, const c10::optional<at::Tensor>& residual,
                                  bool relu, bool save_mask, const c10::optional<at::Tensor>& num_batches_tracked,
                                  const c10::optional<at::Tensor>& residual_ss,
-                                 const c10::optional<at::Tensor>& residual_nbt);
+                                 const c10::optional<at::Tensor>& residual_nbt, const c10::optional<at::Tensor>& out,
+                                 const c10::optional<at::Tensor>& out_bits);
 // 1x1 conv as an MFMA GEMM with BN prologue (previous BN's apply+ReLU) / epilogue (stats partials)
 std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride,
                                      const c10::optional<at::Tensor>& prologue_ss, bool stats,
                                      const c10::optional<at::Tensor>& prologue_y, bool w_t,
                                      const c10::optional<at::Tensor>& epi_add, const c10::optional<at::Tensor>& epi_y,
                                      const c10::optional<at::Tensor>& epi_bits, const c10::optional<at::Tensor>& epi_mean,
-                                     const c10::optional<at::Tensor>& epi_ss, int64_t epi_add_stride);
+                                     const c10::optional<at::Tensor>& epi_ss, int64_t epi_add_stride,
+                                     const c10::optional<at::Tensor>& pro_out, const c10::optional<at::Tensor>& pro_bits,
+                                     const c10::optional<at::Tensor>& pro_res, const c10::optional<at::Tensor>& pro_res_ss,
+                                     const c10::optional<at::Tensor>& pro_nbt, const c10::optional<at::Tensor>& pro_res_nbt);
 // BN backward from external (sum g, sum g·(x - mean)) partials [groups, C, 2]: (coef [3, C] with the
 // mean folded in, dweight, dbias)
 std::vector<at::Tensor> bn_backward_from_partials(const at::Tensor& part, int64_t M,

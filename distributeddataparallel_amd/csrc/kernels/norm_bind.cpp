@@ -16,11 +16,13 @@ void bind_norm_kernels(py::module_& m) {
         py::arg("dy2") = py::none(), py::arg("mask_bits") = py::none(), py::arg("coef_only") = false);
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("scale_shift"), py::arg("residual"), py::arg("relu"),
         py::arg("save_mask"), py::arg("num_batches_tracked"), py::arg("residual_ss") = py::none(),
-        py::arg("residual_nbt") = py::none());
+        py::arg("residual_nbt") = py::none(), py::arg("out") = py::none(), py::arg("out_bits") = py::none());
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("prologue_ss"),
         py::arg("stats"), py::arg("prologue_y") = py::none(), py::arg("w_t") = false, py::arg("epi_add") = py::none(),
         py::arg("epi_y") = py::none(), py::arg("epi_bits") = py::none(), py::arg("epi_mean") = py::none(),
-        py::arg("epi_ss") = py::none(), py::arg("epi_add_stride") = 1);
+        py::arg("epi_ss") = py::none(), py::arg("epi_add_stride") = 1, py::arg("pro_out") = py::none(),
+        py::arg("pro_bits") = py::none(), py::arg("pro_res") = py::none(), py::arg("pro_res_ss") = py::none(),
+        py::arg("pro_nbt") = py::none(), py::arg("pro_res_nbt") = py::none());
   m.def("bn_backward_from_partials", &bn_backward_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),
         py::arg("mean"), py::arg("invstd"), py::arg("need_dweight"), py::arg("fold_mean") = true);
   m.def("bn_backward_elem", &bn_backward_elem, py::arg("g"), py::arg("x"), py::arg("mean"), py::arg("coef"));

@@ -9,6 +9,7 @@ HIP BatchNorm(+ReLU) without changing the parameter/buffer layout or state_dict 
 """
 from __future__ import annotations
 
+import threading
 from typing import Callable, List, Optional, Type, Union
 
 import torch
@@ -46,6 +47,16 @@ def _ds_link() -> bool:
     import os
 
     return os.environ.get("XDDP_CONV_EPI_DS", "1") != "0"
+
+
+# Set by ResNet.forward while its fused blocks may hand a pending output (ops/conv_bn.py
+# PendingApply) to the next block: only inside the model's own forward, where the next block's
+# conv1 is that output's first reader and the final output is resolved before it leaves.
+_PEND = threading.local()
+
+
+def _pending_ok() -> bool:
+    return getattr(_PEND, "on", False)
 
 
 def _ds_defer() -> bool:
@@ -130,13 +141,16 @@ class Bottleneck(nn.Module):
             if ds is not None and link is None:
                 identity = conv1x1_bn_act(xr, ds[0], ds[1], defer=defer)
             out = conv1x1_bn_act(x, self.conv1, self.bn1, relu=True, link_x=link)
-            out = self.act2(conv3x3_bn_relu(out, self.conv2, self.bn2))
+            # BN2's apply happens in conv3's GEMM prologue (ops/conv_bn.py:PendingApply)
+            out = self.act2(conv3x3_bn_relu(out, self.conv2, self.bn2, pending=True))
             if ds is None:
                 identity = xr
             elif link is not None:  # issued after conv2: its backward runs before conv1's
                 identity = conv1x1_bn_act(xr, ds[0], ds[1], link_ds=link, defer=defer)
+            # the block output's apply (BN3 + identity + ReLU) happens in the next block's conv1
+            # GEMM prologue when ResNet.forward allows it
             return conv1x1_bn_act(out, self.conv3, self.bn3, residual=identity, relu=True, dual_output=True,
-                                  link_res=link if ds is None else None)
+                                  link_res=link if ds is None else None, pending=_pending_ok())
         identity = xr if self.downsample is None else self.downsample(xr)
         out = self.act1(self.bn1(self.conv1(x)))
         out = self.act2(self.bn2(self.conv2(out)))
@@ -205,6 +219,19 @@ class ResNet(nn.Module):
                                 dilation=self.dilation, norm_layer=norm_layer))
         return nn.Sequential(*layers)
 
+    def _no_block_hooks(self) -> bool:
+        """No forward hook can see a block output (a pending one must not be read before the next
+        block's conv1 writes it): none on the layers, their blocks, or globally."""
+        from torch.nn.modules import module as _mod
+
+        if _mod._global_forward_hooks or _mod._global_forward_pre_hooks:
+            return False
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for m in (layer, *layer.children()):
+                if m._forward_hooks or m._forward_pre_hooks:
+                    return False
+        return True
+
     def forward(self, x):
         fused = (getattr(self.bn1, "fuses_relu", False) and getattr(self.bn1, "relu", False)
                  and getattr(self.maxpool, "dual_output", None) is not None and self.training and _stem_fusion())
@@ -223,12 +250,21 @@ class ResNet(nn.Module):
 
                 pooled = stem_bn_relu_maxpool(x, self.bn1, self.maxpool, dual=self.maxpool.dual_output)
         x = pooled if pooled is not None else self.maxpool(self.relu(self.bn1(x)))
-        x = self.layer1(x)
-        x = self.layer2(x)
-        x = self.layer3(x)
-        x = self.layer4(x)
+        prev = _pending_ok()
+        _PEND.on = fused and self._no_block_hooks()
+        try:
+            x = self.layer1(x)
+            x = self.layer2(x)
+            x = self.layer3(x)
+            x = self.layer4(x)
+        finally:
+            _PEND.on = prev
         if isinstance(x, tuple):  # fused blocks hand (output, alias) to the next block
             x = x[0]
+        if fused:
+            from ..ops.conv_bn import resolve
+
+            resolve(x)  # the last block's output has no conv1 to absorb its apply
         if fused and isinstance(self.avgpool, nn.AdaptiveAvgPool2d) and self.avgpool.output_size in (1, (1, 1)):
             from ..ops.pool import global_avg_pool
 

@@ -91,6 +91,54 @@ class _ApplyDeferred(torch.autograd.Function):
         return g, None, None
 
 
+class PendingApply:
+    """A BatchNorm apply (``relu(y·s + t [+ r])``) whose output tensor exists but is not written
+    yet: its consumer, the next 1x1 conv's GEMM, computes it while staging its A operand and
+    stores it as a side output (``conv1x1_gemm(..., pro_out=...)``, csrc/kernels/conv_gemm.hip
+    ProOut) — so the activation is written once and never read back by that conv, and the apply
+    pass disappears. Two producers: a bottleneck's conv2 + BN2 + ReLU (consumer: conv3, prologue
+    1) and a bottleneck's final BN3 + residual + ReLU (consumer: the next block's conv1, prologue
+    4 / 5 with the deferred downsample BN; the ReLU mask bits come out of the same prologue).
+
+    Any other reader must call :func:`resolve` first, which runs the ordinary apply into the same
+    tensors; the consumers in this module do so whenever they cannot absorb it, and the model
+    only creates pending block outputs when nothing else can see them (ResNet.forward: no
+    forward hooks, final output resolved). ``nbt`` / ``rnbt``: the counters the apply bumps."""
+
+    __slots__ = ("y", "ss", "res", "rss", "nbt", "rnbt", "out", "bits", "done")
+
+    def __init__(self, y, ss, res, rss, nbt, rnbt, out, bits):
+        self.y, self.ss, self.res, self.rss, self.nbt, self.rnbt = y, ss, res, rss, nbt, rnbt
+        self.out, self.bits, self.done = out, bits, False
+
+    def resolve(self):
+        if not self.done:
+            self.done = True
+            load().bn_apply(self.y, self.ss, self.res, True, self.bits is not None, self.nbt, self.rss, self.rnbt,
+                            self.out, self.bits)
+        self.y = self.res = self.ss = self.rss = None
+
+
+def resolve(t):
+    """Make a possibly-pending activation readable (no-op for ordinary tensors)."""
+    p = getattr(t, "_xddp_pend", None) if t is not None else None
+    if p is not None and not p.done:
+        p.resolve()
+    return t
+
+
+def _pending_apply() -> bool:
+    """XDDP_PENDING_APPLY=0 keeps the separate apply passes of BN2 and of the block output instead of
+    folding them into the consuming 1x1 GEMM's prologue (A/B switch)."""
+    return os.environ.get("XDDP_PENDING_APPLY", "1") != "0"
+
+
+def _new_pending(y, ss, res, rss, nbt, rnbt, with_bits):
+    out = torch.empty_like(y, memory_format=torch.channels_last)
+    bits = torch.empty(y.numel() // 8, dtype=torch.uint8, device=y.device) if with_bits else None
+    return PendingApply(y, ss, res, rss, nbt, rnbt, out, bits)
+
+
 def _deferred(t):
     return getattr(t, "_xddp_bnss", None) if t is not None else None
 
@@ -144,11 +192,19 @@ def _same_tensor(a, b) -> bool:
 class _Conv1x1BN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, residual, relu, dual,
-                stride, link_out, link_x, link_res, link_in, link_ds, defer, res_defer):
+                stride, link_out, link_x, link_res, link_in, link_ds, defer, res_defer, pend_in, pend_out):
         C = load()
         ctx.set_materialize_grads(False)
         dma = _c1_dma(x, w)
-        if dma:  # deep-K / few-tile shapes: the 3-stage LDS-DMA pipeline (csrc/kernels/conv3x3.hip TAPS=1)
+        if pend_in is not None:
+            # x is a pending BN apply (PendingApply): computed in this GEMM's prologue and stored
+            # into x's storage by the N-tile-0 blocks (the caller checked _absorbs)
+            p = pend_in
+            y, part = C.conv1x1_gemm(p.y, w, 1, p.ss, True, pro_out=p.out, pro_bits=p.bits, pro_res=p.res,
+                                     pro_res_ss=p.rss, pro_nbt=p.nbt, pro_res_nbt=p.rnbt)
+            p.done = True
+            p.y = p.res = p.ss = p.rss = None
+        elif dma:  # deep-K / few-tile shapes: the 3-stage LDS-DMA pipeline (csrc/kernels/conv3x3.hip TAPS=1)
             y, part = C.conv1x1_dma_forward(x, w, stride, True)
         elif stride == 1 and x.size(1) >= _c1_blas_min_k():
             # deep-K, few-tile layers (ResNet-50 layer3/4 conv1: K = 1024 / 2048, 400-800 output
@@ -168,6 +224,11 @@ class _Conv1x1BN(torch.autograd.Function):
         if defer is not None:  # the consumer applies this BN (DeferredBN): output the raw conv output
             defer.ss, defer.nbt = ss, nbt
             out, bits = y, None
+        elif pend_out is not None and keep_mask:  # the next block's conv1 applies it (PendingApply)
+            p = _new_pending(y, ss, residual, res_defer.ss if res_defer is not None else None, nbt,
+                             res_defer.nbt if res_defer is not None else None, True)
+            pend_out.append(p)
+            out, bits = p.out, p.bits
         elif res_defer is not None:
             out, bits = C.bn_apply(y, ss, residual, relu, keep_mask, nbt, res_defer.ss, res_defer.nbt)
         else:
@@ -214,7 +275,7 @@ class _Conv1x1BN(torch.autograd.Function):
         if dout is None:
             dout, dout2 = dout2, None
         if dout is None:
-            return (None,) * 21
+            return (None,) * 23
         need_bn_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         s = ctx.stride
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
@@ -300,12 +361,12 @@ class _Conv1x1BN(torch.autograd.Function):
 
 
 def _grads(ctx, dx, dw, dw_bn, db_bn, dres):
-    """The 21 input gradients of _Conv1x1BN; a linked residual gradient goes to the consumer link."""
+    """The 23 input gradients of _Conv1x1BN; a linked residual gradient goes to the consumer link."""
     if dres is not None and ctx.link_res is not None:
         ctx.link_res.add, dres = dres, None
     return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
             None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None, None, None, None,
-            None, None, None, None)
+            None, None, None, None, None, None)
 
 
 def _bwd_fused_ok(ctx, C, w) -> bool:
@@ -338,14 +399,19 @@ def _dgrad_in(ctx, C, g, w, coef, y):
 
 class _Conv3x3BNReLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, stride, link):
+    def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, stride, link, pend_out):
         C = load()
         ctx.set_materialize_grads(False)
         y, part = C.conv3x3_forward(x, w, stride, True)
         M = y.numel() // y.size(1)
         mean, invstd, ss = C.bn_stats_from_partials(part, M, weight, bias, running_mean, running_var, nbt, momentum,
                                                     cma, eps, True)
-        out, _ = C.bn_apply(y, ss, None, True, False, nbt)
+        if pend_out is not None:  # conv3's GEMM prologue applies it (PendingApply)
+            p = _new_pending(y, ss, None, None, nbt, None, False)
+            pend_out.append(p)
+            out = p.out
+        else:
+            out, _ = C.bn_apply(y, ss, None, True, False, nbt)
         ctx.stride = stride
         ctx.save_for_backward(x, w, y, weight, mean, invstd, ss)
         ctx.link = link
@@ -356,7 +422,7 @@ class _Conv3x3BNReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         if dout is None:
-            return (None,) * 12
+            return (None,) * 13
         C = load()
         x, w, y, weight, mean, invstd, ss = ctx.saved_tensors
         need_bn_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
@@ -397,7 +463,7 @@ class _Conv3x3BNReLU(torch.autograd.Function):
             dx = gx if need_x else dx
             dw = gw if need_w else dw
         return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None)
 
 
 def _dgrad(C, g, w, coef, y):
@@ -474,22 +540,30 @@ def conv_bn_supported(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module) -> bool:
             and getattr(bn, "fuses_relu", False))
 
 
-def conv3x3_bn_relu(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module):
-    """``relu(bn(conv3x3(x)))`` on the implicit-GEMM kernel with BN statistics from its epilogue."""
+def conv3x3_bn_relu(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, pending: bool = False):
+    """``relu(bn(conv3x3(x)))`` on the implicit-GEMM kernel with BN statistics from its epilogue.
+
+    pending: the caller feeds the result straight to a 1x1 conv through :func:`conv1x1_bn_act`,
+    which applies this BN in its GEMM prologue (:class:`PendingApply`)."""
+    resolve(x)
     if not (_conv3x3() and conv.kernel_size == (3, 3) and conv_bn_supported(x, conv, bn)):
         return bn(conv(x), relu=True)
     link = BNReLULink(None, None, None) if _epi() else None
+    pend = [] if (pending and _pending_apply()) else None
     out = _Conv3x3BNReLU.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), int(conv.stride[0]),
-                               link)
+                               link, pend)
     if link is not None:
         out._xddp_bnr = link
+    if pend:
+        out._xddp_pend = pend[0]
     return out
 
 
 def conv1x1_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, residual: Optional[torch.Tensor] = None,
                    relu: bool = False, dual_output: bool = False, link_x: Optional[EpiLink] = None,
-                   link_res: Optional[EpiLink] = None, link_ds: Optional[EpiLink] = None, defer: bool = False):
+                   link_res: Optional[EpiLink] = None, link_ds: Optional[EpiLink] = None, defer: bool = False,
+                   pending: bool = False):
     """``relu(bn(conv(x)) [+ residual])`` with BN statistics from the conv epilogue when supported.
 
     link_x / link_res: the :class:`EpiLink` of the block output that is this conv's input /
@@ -497,23 +571,45 @@ def conv1x1_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, residual: Op
     the returned output carries a fresh link for the next block. link_ds: this stride-2 conv is
     the downsample sharing its input with a linked conv1 (compact input gradient to the link).
     defer: return the raw conv output and leave this BN's apply to the consumer that takes the
-    result as its ``residual`` (DeferredBN; only for a BN without ReLU or residual)."""
+    result as its ``residual`` (DeferredBN; only for a BN without ReLU or residual).
+    pending: leave this op's apply (residual + ReLU form) to the next block's conv1, which must be
+    this output's first reader (:class:`PendingApply`). A pending ``x`` is absorbed into this conv's
+    GEMM prologue when the GEMM path allows it, else resolved first."""
+    resolve(residual)
+    pend_in = getattr(x, "_xddp_pend", None)
+    if pend_in is not None and (pend_in.done or not _absorbs(x, conv, bn, pend_in)):
+        pend_in.resolve()
+        pend_in = None
     res_defer = _deferred(residual)
     if conv.kernel_size != (1, 1) or not conv_bn_supported(x, conv, bn) or (residual is not None and not (
             residual.shape[0] == x.shape[0] and residual.dtype == x.dtype
             and residual.is_contiguous(memory_format=torch.channels_last))):
+        if pend_in is not None:
+            pend_in.resolve()
         if res_defer is not None:
             residual = _ApplyDeferred.apply(residual, res_defer.ss, res_defer.nbt)
         return bn(conv(x), residual=residual, relu=relu, dual_output=dual_output)
     dfr = DeferredBN() if (defer and residual is None and not relu and not dual_output) else None
     link_out = EpiLink() if (dual_output and residual is not None and relu and _epi()) else None
     link_in = getattr(x, "_xddp_bnr", None) if conv.stride[0] == 1 else None
+    pend_out = [] if (pending and dual_output and residual is not None and relu and _pending_apply()) else None
     out = _Conv1x1BN.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                            bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), residual, relu,
                            dual_output, int(conv.stride[0]), link_out, link_x, link_res, link_in,
-                           link_ds if conv.stride[0] == 2 else None, dfr, res_defer)
+                           link_ds if conv.stride[0] == 2 else None, dfr, res_defer, pend_in, pend_out)
     if dfr is not None:
         out._xddp_bnss = dfr
     if link_out is not None:
         out[0]._xddp_epi = link_out
+    if pend_out:  # both aliases: whichever a consumer reads first resolves it
+        out[0]._xddp_pend = out[1]._xddp_pend = pend_out[0]
     return out
+
+
+def _absorbs(x, conv, bn, p) -> bool:
+    """Can this 1x1 conv's forward GEMM apply the pending BN in its prologue? Its register-staged
+    GEMM path only (stride 1; not the LDS-DMA or hipBLASLt deep-K forwards), and the pending form
+    must match the tensor (C, 8-channel chunks)."""
+    return (conv.kernel_size == (1, 1) and conv.stride[0] == 1 and conv_bn_supported(x, conv, bn)
+            and not _c1_dma(x, conv.weight) and x.size(1) < _c1_blas_min_k()
+            and p.out.data_ptr() == x.data_ptr() and p.out.shape == x.shape)

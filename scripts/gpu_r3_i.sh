@@ -1,0 +1,12 @@
+#!/bin/bash
+# r3 call I: full GPU suite + smoke with the pending BN applies on, one bench.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+mkdir -p gpurun_out
+export XDDP_NO_AUTOBUILD=1
+step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "$ROOT/gpurun_out/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -3 "$ROOT/gpurun_out/$name.log" | cut -c1-300; if [ $rc -ge 124 ]; then exit $rc; fi; }
+PYT="python -u -m pytest -v --timeout 240 --timeout-method thread"
+step pytest_pend 300 $PYT -s tests/test_pending_apply_gpu.py
+step pytest_all 900 $PYT -m gpu tests
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+step r50 300 python -u bench.py --json-out gpurun_out/r3i_r50.json

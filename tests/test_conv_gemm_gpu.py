@@ -283,6 +283,8 @@ def test_downsample_epilogue_handoff_matches_separate_pass(monkeypatch):
     from distributeddataparallel_amd.ops import FusedBatchNorm2d
 
     monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)  # (see the DeferredBN test)
+    # (bitwise-identical forwards: the pending-apply GEMM's statistics tiles differ from the plain one's)
+    monkeypatch.setenv("XDDP_PENDING_APPLY", "0")
     torch.manual_seed(8)
     m = ResNet(Bottleneck, [1, 1, 2, 1], norm_layer=FusedBatchNorm2d).cuda().to(torch.bfloat16)
     m = m.to(memory_format=torch.channels_last)
@@ -350,6 +352,8 @@ def test_bottleneck_epilogue_handoff_matches_separate_pass(monkeypatch):
     from distributeddataparallel_amd.ops import FusedBatchNorm2d
 
     monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)  # (see the DeferredBN test)
+    # (bitwise-identical forwards: the pending-apply GEMM's statistics tiles differ from the plain one's)
+    monkeypatch.setenv("XDDP_PENDING_APPLY", "0")
     torch.manual_seed(6)
     m = ResNet(Bottleneck, [2, 2, 1, 1], norm_layer=FusedBatchNorm2d).cuda().to(torch.bfloat16)
     m = m.to(memory_format=torch.channels_last)
