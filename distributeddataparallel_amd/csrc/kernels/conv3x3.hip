@@ -24,6 +24,7 @@
 
 #include "common.h"
 #include "kernels/dev_utils.h"
+#include "kernels/norm.h"
 
 namespace xddp {
 namespace kernels {
@@ -325,6 +326,16 @@ std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w
               "conv3x3_forward: 16-B aligned operands required");
   const int64_t OH = (IH - 1) / stride + 1, OW = (IW - 1) / stride + 1, M = B * OH * OW;
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "conv3x3_forward: bad size");
+  // wide layers (N >= XDDP_C3_GEMM_MIN_N, default 256; 0 = never) on the dense GEMM's 4-phase
+  // LDS-DMA pipeline with the im2col addressing (gemm.hip ConvGeo)
+  {
+    static const int min_n = [] {
+      const char* e = std::getenv("XDDP_C3_GEMM_MIN_N");
+      return e ? std::atoi(e) : 256;
+    }();
+    if (min_n > 0 && N >= min_n && N % 128 == 0 && x.numel() < (int64_t(1) << 31) && ((C / 64) & (C / 64 - 1)) == 0)
+      return conv3x3_gemm(x, w, stride, stats, zero_line(x));
+  }
   auto y = at::empty({B, N, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int cfg = tile_choice((int)N);
   const int BM = cfg == 1 || cfg == 3 || cfg == 4 ? 128 : 256, BN = cfg <= 1 ? 128 : 64;

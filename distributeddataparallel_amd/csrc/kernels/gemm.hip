@@ -41,18 +41,30 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 constexpr int kBM = 256, kBK = 64, kWM = 2, kWN = 4, NW = kWM * kWN, kThreads = 64 * NW;
 
-enum Epi : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiResidual = 3, kEpiDGelu = 4 };
+enum Epi : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiResidual = 3, kEpiDGelu = 4, kEpiStats = 5 };
+
+// CONV: A is not a matrix but the implicit im2col of a 3x3 pad-1 convolution (NHWC bf16 input
+// [B, IH, IW, C], weights OHWI [N][3][3][C] = B[N, 9C]): row m = output pixel (b, oh, ow), K-tile
+// kt = tap (kt / (C/64)) x 64-channel block; the DMA source of a row is the input pixel under
+// that tap, or a zero line for padding taps (no branch). Same pipeline as the dense GEMM; this is
+// the ResNet-50 3x3 forward / stride-1 input gradient for N >= 256, where the 4-phase loop beats
+// the 3-stage conv3x3.hip kernel (scripts/conv3x3_ceiling.py).
+struct ConvGeo {
+  int IH, IW, OH, OW, stride, C;
+  const uint16_t* zeros;
+};
 
 
 __device__ __forceinline__ float bf(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
 
-template <int BN, int EPI>
+template <int BN, int EPI, bool CONV = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A,
                                                               const uint16_t* __restrict__ B,
                                                               uint16_t* Y, uint16_t* __restrict__ Y2,
                                                               const uint16_t* __restrict__ bias,
                                                               const uint16_t* res, float* __restrict__ part,
-                                                              int M, int N, int K, int ntiles, int64_t ldr) {
+                                                              int M, int N, int K, int ntiles, int64_t ldr,
+                                                              ConvGeo cg) {
   constexpr int AI = kBM / 8 / NW, BI = BN / 8 / NW;  // DMA wave-instructions per stage (8 rows each)
   static_assert(AI * NW * 8 == kBM && BI * NW * 8 == BN, "tile rows must split evenly over the waves");
   constexpr int WTM = kBM / kWM, WTN = BN / kWN, TM = WTM / 16, TN = WTN / 16;
@@ -79,13 +91,43 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   // needs ~224 for accumulators and fragments). Rows past M re-read row M - 1 (never stored).
   const int drow = wid * 8 + (lane >> 3);                    // + i * 8 NW (A, i < AI) / j * 8 NW (B)
   const int dchunk = 8 * (pos ^ ((drow >> 1) & 7));          // (row >> 1) & 7 is the same for row + 64 i
-  auto issue = [&](int kt, int buf) {
-    uint8_t* As = smem + buf * STAGE;
+  // CONV: per A row, the top-left input pixel of its 3x3 window (packed (ih0 + 2) << 16 | (iw0 + 2))
+  // and that pixel's element offset (may point before the row for padding windows; never
+  // dereferenced then). Host-checked: the input has < 2^31 elements.
+  int vmask[CONV ? AI : 1], cbase[CONV ? AI : 1];  // CONV: taps inside the image (bit t), window offset
+  if constexpr (CONV) {
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int row = min(m0 + drow + i * 8 * NW, M - 1);
-      const uint16_t* src = A + (uint32_t)row * (uint32_t)K + (uint32_t)(dchunk + kt * kBK);
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + (wid * 8 + i * 8 * NW) * 128), 16, 0, 0);
+      const int hw = cg.OH * cg.OW, b = row / hw, rem = row - b * hw, oh = rem / cg.OW, ow = rem - oh * cg.OW;
+      const int st = cg.stride & 0xffff, ih0 = oh * st - 1, iw0 = ow * st - 1;
+      int m = 0;
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+        m |= ((unsigned)(ih0 + t / 3) < (unsigned)cg.IH && (unsigned)(iw0 + t % 3) < (unsigned)cg.IW) << t;
+      vmask[i] = m;
+      cbase[i] = ((b * cg.IH + ih0) * cg.IW + iw0) * cg.C + dchunk;
+    }
+  }
+  auto issue = [&](int kt, int buf) {
+    uint8_t* As = smem + buf * STAGE;
+    if constexpr (CONV) {
+      // C / 64 is a power of two (host-checked): cg.stride's high half carries its log2
+      const int lg = cg.stride >> 16, tap = kt >> lg, cb = kt & ((1 << lg) - 1), r = (tap * 11) >> 5, sx = tap - 3 * r;
+      const int toff = (r * cg.IW + sx) * cg.C + cb * kBK;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const bool ok = (vmask[i] >> tap) & 1;
+        const uint16_t* src = ok ? A + (cbase[i] + toff) : cg.zeros;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + (wid * 8 + i * 8 * NW) * 128), 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int row = min(m0 + drow + i * 8 * NW, M - 1);
+        const uint16_t* src = A + (uint32_t)row * (uint32_t)K + (uint32_t)(dchunk + kt * kBK);
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + (wid * 8 + i * 8 * NW) * 128), 16, 0, 0);
+      }
     }
     uint8_t* Bs = As + kBM * 128;
 #pragma unroll
@@ -253,6 +295,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   u32x4 rb{};
   if (EPI == kEpiResidual && bias) rb = *reinterpret_cast<const u32x4*>(bias + n0 + cc * 8);
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // kEpiDGelu: this thread's column sums
+  // kEpiStats: per-channel shifted sums (shift = the tile's row 0, always valid) for the following
+  // BatchNorm's statistics, as conv3x3.hip's epilogue (csum = sum d, cssq = sum d^2)
+  float cssq[EPI == kEpiStats ? 8 : 1], st_n = 0.f;
+  u32x4 st_k{};
+  if (EPI == kEpiStats) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cssq[e] = 0.f;
+    st_k = *reinterpret_cast<const u32x4*>(Cs + cc * 16);
+  }
 #pragma unroll 4
   for (int q = tid; q < kBM * CPR; q += kThreads) {
     const int row = q / CPR;
@@ -278,6 +329,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
         v[e] = dev::pack_bf16x2(lo, hi);
       }
       *reinterpret_cast<u32x4*>(Y + off) = v;
+    } else if (EPI == kEpiStats) {
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + off));
+      st_n += 1.f;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const float d0 = bf(v[h] & 0xffffu) - bf(st_k[h] & 0xffffu);
+        const float d1 = bf(v[h] >> 16) - bf(st_k[h] >> 16);
+        csum[2 * h] += d0;
+        csum[2 * h + 1] += d1;
+        cssq[2 * h] = fmaf(d0, d0, cssq[2 * h]);
+        cssq[2 * h + 1] = fmaf(d1, d1, cssq[2 * h + 1]);
+      }
     } else if (EPI == kEpiResidual) {
       // y = res + (A·Bᵀ, already rounded to bf16 in the C tile) [+ bias]: one extra rounding of
       // the product against addmm_'s single one (the residual term dominates the sum)
@@ -294,6 +357,46 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
       *reinterpret_cast<u32x4*>(Y + off) = v;
     } else {
       *reinterpret_cast<u32x4*>(Y + off) = v;
+    }
+  }
+  if (EPI == kEpiStats) {
+    // lanes sharing cc (xor over the lane bits above log2(CPR)), then the waves through LDS; one
+    // (count, mean, M2) per channel and tile, group-minor: part[q][N][mtiles] (bn_stats_from_partials)
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1) {
+      st_n += __shfl_xor(st_n, o, 64);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        csum[e] += __shfl_xor(csum[e], o, 64);
+        cssq[e] += __shfl_xor(cssq[e], o, 64);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // C tile reads done: reuse smem
+    float* red = reinterpret_cast<float*>(smem);                      // [NW][2][BN] sums, [NW][CPR] counts
+    float* redn = red + NW * 2 * BN;
+    float* redk = redn + NW * CPR;                                    // [BN] the shifts
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wid * 2 + 0) * BN + cc * 8 + e] = csum[e];
+        red[(wid * 2 + 1) * BN + cc * 8 + e] = cssq[e];
+        if (wid == 0) redk[cc * 8 + e] = (e & 1) ? bf(st_k[e >> 1] >> 16) : bf(st_k[e >> 1] & 0xffffu);
+      }
+      redn[wid * CPR + cc] = st_n;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int G = gridDim.x / ntiles;
+    for (int c = tid; c < BN; c += kThreads) {
+      float tn = 0.f, ts = 0.f, tss = 0.f;
+      for (int w = 0; w < NW; ++w) {
+        tn += redn[w * CPR + c / 8];
+        ts += red[(w * 2 + 0) * BN + c];
+        tss += red[(w * 2 + 1) * BN + c];
+      }
+      const float mean_s = ts / tn;  // tn >= 1: row 0 is always valid
+      part[((int64_t)0 * N + n0 + c) * G + mt] = tn;
+      part[((int64_t)1 * N + n0 + c) * G + mt] = redk[c] + mean_s;
+      part[((int64_t)2 * N + n0 + c) * G + mt] = fmaxf(tss - ts * mean_s, 0.f);
     }
   }
   if (EPI == kEpiDGelu) {
@@ -313,22 +416,23 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   }
 }
 
-template <int BN, int EPI>
+template <int BN, int EPI, bool CONV = false>
 void launch_gemm(const at::Tensor& a, const at::Tensor& b, uint16_t* y, uint16_t* y2, const uint16_t* bias,
-                 const uint16_t* res, float* part, int64_t ldr, int M, int N, int K, hipStream_t stream) {
+                 const uint16_t* res, float* part, int64_t ldr, int M, int N, int K, hipStream_t stream,
+                 const ConvGeo& cg = ConvGeo{}) {
   const int mtiles = (M + kBM - 1) / kBM, ntiles = N / BN;
   // stages | C tile (+ the column-sum exchange of the dGELU epilogue)
   const size_t lds = std::max<size_t>((size_t)2 * (kBM + BN) * 128,
                                       (size_t)kBM * (BN * 2 + 16) + (EPI == kEpiDGelu ? (size_t)2048 * NW : 0));
   static bool attr = false;
   if (!attr) {
-    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI>,
+    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI, CONV>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI>), dim3(mtiles * ntiles), dim3(kThreads), lds, stream,
+  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI, CONV>), dim3(mtiles * ntiles), dim3(kThreads), lds, stream,
                      reinterpret_cast<const uint16_t*>(a.data_ptr()), reinterpret_cast<const uint16_t*>(b.data_ptr()),
-                     y, y2, bias, res, part, M, N, K, ntiles, ldr);
+                     y, y2, bias, res, part, M, N, K, ntiles, ldr, cg);
   XDDP_HIP_CHECK(hipGetLastError());
 }
 
@@ -435,6 +539,35 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
     return {y, db};
   }
   return {y};
+}
+
+// 3x3 pad-1 convolution (stride 1 or 2) on the dense GEMM pipeline (ConvGeo): x [B, C, IH, IW]
+// bf16 channels_last, w [N, C, 3, 3] bf16 channels_last (OHWI). Returns {y [B, N, OH, OW]
+// channels_last, statistics partials [3, N, mtiles] group-minor (empty without stats)}.
+// N % 128 == 0, C % 64 == 0.
+std::vector<at::Tensor> conv3x3_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats,
+                                     const uint16_t* zeros) {
+  const int64_t B = x.size(0), C = x.size(1), IH = x.size(2), IW = x.size(3), N = w.size(0);
+  TORCH_CHECK(C % 64 == 0 && N % 128 == 0 && x.numel() < (int64_t(1) << 31), "conv3x3_gemm: unsupported shape");
+  const int64_t OH = (IH - 1) / stride + 1, OW = (IW - 1) / stride + 1, M = B * OH * OW;
+  auto y = at::empty({B, N, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  // 256 x 128 tiles: the 256-wide tile's conv addressing spills ~60 registers past the 256 the
+  // 4-phase loop leaves (kernel_resources.py), the 128-wide one fits in 186
+  constexpr int BN = 128;
+  const int64_t mtiles = (M + kBM - 1) / kBM;
+  at::Tensor part = stats ? at::empty({3, N, mtiles}, x.options().dtype(at::kFloat))
+                          : at::empty({0}, x.options().dtype(at::kFloat));
+  const int lg = __builtin_ctz((unsigned)(C / 64));
+  TORCH_CHECK((C / 64) == (int64_t(1) << lg), "conv3x3_gemm: C / 64 must be a power of two");
+  // (stride | log2(C / 64) << 16: the kernel splits K-tiles into tap / channel block by shifts)
+  const ConvGeo cg{(int)IH, (int)IW, (int)OH, (int)OW, (int)stride | (lg << 16), (int)C, zeros};
+  auto* yp = reinterpret_cast<uint16_t*>(y.data_ptr());
+  float* pp = stats ? part.data_ptr<float>() : nullptr;
+  const int K = (int)(9 * C);
+  if (stats) launch_gemm<BN, kEpiStats, true>(x, w, yp, nullptr, nullptr, nullptr, pp, N, (int)M, (int)N, K, stream, cg);
+  else launch_gemm<BN, kEpiNone, true>(x, w, yp, nullptr, nullptr, nullptr, pp, N, (int)M, (int)N, K, stream, cg);
+  return {y, part};
 }
 
 }  // namespace kernels

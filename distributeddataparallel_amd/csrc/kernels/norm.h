@@ -56,6 +56,10 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
 std::vector<at::Tensor> conv1x1_dma_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats,
                                             int64_t tile);
 std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats);
+// the same on the dense GEMM pipeline (gemm.hip; N % 128 == 0, input < 2^31 elements); zeros: a
+// 256-B zero line on the device
+std::vector<at::Tensor> conv3x3_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats,
+                                     const uint16_t* zeros);
 at::Tensor conv3x3_rot_weight(const at::Tensor& w);
 at::Tensor conv3x3_dgrad_s2(const at::Tensor& dy, const at::Tensor& w_rot, int64_t H, int64_t W);
 at::Tensor conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like);

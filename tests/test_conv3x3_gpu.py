@@ -22,6 +22,11 @@ def _cl(t):
     (2, 64, 15, 15, 256, 2, 0.0),    # strided, odd input size
     (1, 512, 7, 7, 512, 1, 0.0),     # long reduction (72 steps), one M-tile
     (8, 64, 40, 40, 64, 1, 0.0),     # 100 M-tiles: many stats partials
+    # N >= 256: the dense-GEMM pipeline with im2col addressing (gemm.hip ConvGeo)
+    (3, 256, 14, 14, 256, 1, 30.0),  # layer-3 shape, partial last 256-row tile, |mean| >> std
+    (2, 128, 9, 11, 384, 1, 0.0),    # three 128-wide N tiles, odd spatial size
+    (2, 256, 15, 13, 256, 2, 0.0),   # strided, odd input size
+    (2, 192, 8, 8, 256, 1, 0.0),     # C / 64 = 3 (not a power of two): the conv3x3.hip kernel
 ])
 def test_conv3x3_forward_matches_conv2d(b, cin, h, w, cout, s, off):
     torch.manual_seed(0)
@@ -40,11 +45,12 @@ def test_conv3x3_forward_matches_conv2d(b, cin, h, w, cout, s, off):
     torch.testing.assert_close(1.0 / invstd ** 2 - 1e-5, yf.var(0, unbiased=False), rtol=2e-3, atol=1e-6)
 
 
-def test_conv3x3_rotated_weight_gives_input_gradient():
+@pytest.mark.parametrize("cin,cout", [(128, 64), (256, 256)])
+def test_conv3x3_rotated_weight_gives_input_gradient(cin, cout):
     torch.manual_seed(1)
-    x = torch.randn(2, 128, 10, 11, device="cuda")
-    wt = torch.randn(64, 128, 3, 3, device="cuda") / 34
-    dy = torch.randn(2, 64, 10, 11, device="cuda")
+    x = torch.randn(2, cin, 10, 11, device="cuda")
+    wt = torch.randn(cout, cin, 3, 3, device="cuda") / (9 * cin) ** 0.5
+    dy = torch.randn(2, cout, 10, 11, device="cuda")
     rot = C.conv3x3_rot_weight(_cl(wt))
     torch.testing.assert_close(rot.float(), _cl(wt).float().flip(2, 3).transpose(0, 1), rtol=0, atol=0)
     dx = C.conv3x3_forward(_cl(dy), rot, 1, False)[0]
