@@ -27,6 +27,11 @@ def _cl(t):
     (2, 128, 9, 11, 384, 1, 0.0),    # three 128-wide N tiles, odd spatial size
     (2, 256, 15, 13, 256, 2, 0.0),   # strided, odd input size
     (2, 192, 8, 8, 256, 1, 0.0),     # C / 64 = 3 (not a power of two): the conv3x3.hip kernel
+    # N <= 128, stride 1, W >= 14: the halo kernel (R output rows per block, one staged halo)
+    (2, 64, 56, 56, 64, 1, 30.0),    # layer-1 shape: 4-row bands
+    (2, 128, 28, 28, 128, 1, 0.0),   # layer-2 shape: two 64-channel steps, 7-row bands
+    (3, 128, 17, 23, 64, 1, 0.0),    # ragged: last band shorter, odd width
+    (1, 64, 15, 130, 64, 1, 0.0),    # W > 128: the conv3x3.hip kernel
 ])
 def test_conv3x3_forward_matches_conv2d(b, cin, h, w, cout, s, off):
     torch.manual_seed(0)
@@ -45,12 +50,12 @@ def test_conv3x3_forward_matches_conv2d(b, cin, h, w, cout, s, off):
     torch.testing.assert_close(1.0 / invstd ** 2 - 1e-5, yf.var(0, unbiased=False), rtol=2e-3, atol=1e-6)
 
 
-@pytest.mark.parametrize("cin,cout", [(128, 64), (256, 256)])
-def test_conv3x3_rotated_weight_gives_input_gradient(cin, cout):
+@pytest.mark.parametrize("cin,cout,h,w", [(128, 64, 10, 11), (256, 256, 10, 11), (64, 64, 20, 30), (128, 128, 14, 14)])
+def test_conv3x3_rotated_weight_gives_input_gradient(cin, cout, h, w):
     torch.manual_seed(1)
-    x = torch.randn(2, cin, 10, 11, device="cuda")
+    x = torch.randn(2, cin, h, w, device="cuda")
     wt = torch.randn(cout, cin, 3, 3, device="cuda") / (9 * cin) ** 0.5
-    dy = torch.randn(2, cout, 10, 11, device="cuda")
+    dy = torch.randn(2, cout, h, w, device="cuda")
     rot = C.conv3x3_rot_weight(_cl(wt))
     torch.testing.assert_close(rot.float(), _cl(wt).float().flip(2, 3).transpose(0, 1), rtol=0, atol=0)
     dx = C.conv3x3_forward(_cl(dy), rot, 1, False)[0]

@@ -217,7 +217,9 @@ def test_bottleneck_resnet_conv_bn_fusion_matches_unfused(monkeypatch):
     assert cos(gf) > cos(gu) - 0.02, (cos(gf), cos(gu))
 
 
-@pytest.mark.parametrize("b,cin,h,w,cout", [(2, 64, 14, 14, 256), (3, 64, 9, 7, 128), (2, 128, 7, 7, 64)])
+@pytest.mark.parametrize("b,cin,h,w,cout", [(2, 64, 14, 14, 256), (3, 64, 9, 7, 128), (2, 128, 7, 7, 64),
+                                             # K >= 256: the dense-GEMM pipeline (gemm.hip kEpiBnBwd)
+                                             (2, 256, 14, 14, 1024), (3, 512, 7, 7, 256)])
 def test_dgrad_bn_reduce_epilogue(b, cin, h, w, cout):
     """Input-gradient GEMM with the EPI epilogue: g = mask·(dY·W + add) stored, and per-channel
     (sum g, sum g·(y - mean)) partials, against fp32 PyTorch of the same math."""
@@ -250,7 +252,8 @@ def test_dgrad_bn_reduce_epilogue(b, cin, h, w, cout):
     torch.testing.assert_close(coef, torch.stack([k1, k2, k3]), rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("b,cin,h,w,cout", [(2, 64, 14, 14, 256), (2, 128, 7, 9, 128)])
+@pytest.mark.parametrize("b,cin,h,w,cout", [(2, 64, 14, 14, 256), (2, 128, 7, 9, 128), (2, 256, 14, 14, 512),
+                                             (2, 256, 7, 9, 256)])
 def test_dgrad_bn_reduce_epilogue_stride2_add(b, cin, h, w, cout):
     """EPI epilogue with the compact stride-2 addend (a downsample's input gradient, only at the
     even (h, w) pixels), against fp32 PyTorch of the same math."""
