@@ -468,7 +468,7 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
               "gemm_nt: needs K % 64 == 0 and N % 128 == 0");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
               "gemm_nt: 16-B aligned operands required");
-  TORCH_CHECK(epi >= 0 && epi <= 4, "gemm_nt: epi must be 0..4");
+  TORCH_CHECK(epi >= 0 && epi <= 5, "gemm_nt: epi must be 0..5");
   const bool has_bias = bias.has_value() && bias->defined();
   if (has_bias)
     TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kBFloat16 && bias->numel() == N && bias->is_contiguous() &&
@@ -490,7 +490,7 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
     y = *out;
     TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 2 && y.size(0) == M && y.size(1) == N && y.is_contiguous(),
                 "gemm_nt: out must be a contiguous bf16 [M, N] tensor");
-    TORCH_CHECK(epi != 4, "gemm_nt: epilogue 4 allocates its outputs");
+    TORCH_CHECK(epi < 4, "gemm_nt: epilogues 4 and 5 allocate their outputs");
     TORCH_CHECK(epi != 3 || y.data_ptr() == res.data_ptr() || !(y.data_ptr() < (char*)res.data_ptr() + res.nbytes() &&
                                                                   res.data_ptr() < (char*)y.data_ptr() + y.nbytes()),
                 "gemm_nt: out may alias the residual only exactly");
@@ -515,16 +515,19 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
   auto* yp = reinterpret_cast<uint16_t*>(y.data_ptr());
   auto* y2p = epi == 2 ? reinterpret_cast<uint16_t*>(y2.data_ptr()) : nullptr;
   const auto* bp = has_bias ? reinterpret_cast<const uint16_t*>(bias->data_ptr()) : nullptr;
-  const auto* rp = epi >= 3 ? reinterpret_cast<const uint16_t*>(res.data_ptr()) : nullptr;
-  at::Tensor part = epi == 4 ? at::empty({(M + kBM - 1) / kBM, N}, a.options().dtype(at::kFloat)) : at::Tensor();
-  float* pp = epi == 4 ? part.data_ptr<float>() : nullptr;
+  const auto* rp = (epi == 3 || epi == 4) ? reinterpret_cast<const uint16_t*>(res.data_ptr()) : nullptr;
+  at::Tensor part = epi == 4   ? at::empty({(M + kBM - 1) / kBM, N}, a.options().dtype(at::kFloat))
+                   : epi == 5 ? at::empty({3, N, (M + kBM - 1) / kBM}, a.options().dtype(at::kFloat))
+                              : at::Tensor();
+  float* pp = epi >= 4 ? part.data_ptr<float>() : nullptr;
 #define XDDP_GEMM(BN_)                                                                                    \
   switch (epi) {                                                                                          \
     case 0: launch_gemm<BN_, kEpiNone>(a, w, yp, y2p, bp, rp, pp, ldr, (int)M, (int)N, (int)K, stream); break;     \
     case 1: launch_gemm<BN_, kEpiBias>(a, w, yp, y2p, bp, rp, pp, ldr, (int)M, (int)N, (int)K, stream); break;     \
     case 2: launch_gemm<BN_, kEpiBiasGelu>(a, w, yp, y2p, bp, rp, pp, ldr, (int)M, (int)N, (int)K, stream); break; \
     case 3: launch_gemm<BN_, kEpiResidual>(a, w, yp, y2p, bp, rp, pp, ldr, (int)M, (int)N, (int)K, stream); break; \
-    default: launch_gemm<BN_, kEpiDGelu>(a, w, yp, y2p, bp, rp, pp, ldr, (int)M, (int)N, (int)K, stream); break;   \
+    case 4: launch_gemm<BN_, kEpiDGelu>(a, w, yp, y2p, bp, rp, pp, ldr, (int)M, (int)N, (int)K, stream); break;    \
+    default: launch_gemm<BN_, kEpiStats>(a, w, yp, y2p, bp, rp, pp, ldr, (int)M, (int)N, (int)K, stream); break;   \
   }
   if (BN == 256) {
     XDDP_GEMM(256)
@@ -533,6 +536,7 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const 
   }
 #undef XDDP_GEMM
   if (epi == 2) return {y, y2};
+  if (epi == 5) return {y, part};
   if (epi == 4) {
     at::Tensor db = at::empty({N}, has_bias ? bias->options() : a.options().dtype(at::kFloat));
     colsum_partials(part, db);

@@ -47,7 +47,8 @@ void bind_norm_kernels(py::module_& m) {
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,
         py::arg("residual") = py::none(), py::arg("out") = py::none(),
         "y = a @ w.T (bf16, MFMA LDS-DMA GEMM) with epilogue 0 none | 1 +bias | 2 +bias->GELU | 3 +residual | "
-        "4 GELU backward (residual = h): {(a @ w.T) * gelu'(h), column sums}");
+        "4 GELU backward (residual = h): {(a @ w.T) * gelu'(h), column sums} | 5 BatchNorm statistics: "
+        "{y, partials [3, N, mtiles] group-minor}");
   m.def("flash_attn_forward", &flash_attn_forward, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
         py::arg("scale"));
   m.def("flash_attn_backward", &flash_attn_backward, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),

@@ -184,6 +184,15 @@ def _c1_blas_min_k() -> int:
     return v if v > 0 else 1 << 30
 
 
+def _deep_k_own() -> bool:
+    """The deep-K 1x1 forwards run the own LDS-DMA GEMM with the BN-statistics epilogue (gemm.hip
+    kEpiStats) instead of hipBLASLt + a bn_moments pass: ResNet-50 bs256 12,896-12,917 vs
+    12,695-12,775 img/s interleaved (profiles/README.md r3). XDDP_DEEP_K_OWN=0: hipBLASLt (A/B
+    switch; a block output pending on such a conv is resolved by its own apply pass either way —
+    absorbing it on the register-staged GEMM measured no gain)."""
+    return os.environ.get("XDDP_DEEP_K_OWN", "1") != "0"
+
+
 def _same_tensor(a, b) -> bool:
     return a is not None and b is not None and a.data_ptr() == b.data_ptr() and a.shape == b.shape and \
         a.stride() == b.stride()
@@ -206,15 +215,20 @@ class _Conv1x1BN(torch.autograd.Function):
             p.y = p.res = p.ss = p.rss = None
         elif dma:  # deep-K / few-tile shapes: the 3-stage LDS-DMA pipeline (csrc/kernels/conv3x3.hip TAPS=1)
             y, part = C.conv1x1_dma_forward(x, w, stride, True)
-        elif stride == 1 and x.size(1) >= _c1_blas_min_k():
+        elif stride == 1 and x.size(1) >= _c1_blas_min_k() and (w.size(0) % 128 == 0 or not _deep_k_own()):
             # deep-K, few-tile layers (ResNet-50 layer3/4 conv1: K = 1024 / 2048, 400-800 output
-            # tiles): the register-staged GEMM waits a memory latency per 64-deep K step there and
-            # hipBLASLt's is 30-35 % faster (profiles/r2_gemm_resnet_shapes_vs_hipblaslt.txt); the
-            # outputs are small (26 / 13 MB), so a separate statistics pass costs ~5 us
+            # tiles): the register-staged GEMM waits a memory latency per 64-deep K step there;
+            # the LDS-DMA GEMM (gemm.hip) runs them with the statistics in its epilogue (or
+            # hipBLASLt + a statistics pass, XDDP_DEEP_K_OWN=0)
             B, K, H, W = x.shape
-            y = torch.mm(x.permute(0, 2, 3, 1).reshape(-1, K), w.view(w.size(0), K).t())
-            y = y.view(B, H, W, -1).permute(0, 3, 1, 2)
-            part = C.bn_moments(y).view(1, 3, -1)
+            if _deep_k_own():  # the own LDS-DMA GEMM with the statistics epilogue (gemm.hip kEpiStats)
+                y, part = C.gemm_nt(x.permute(0, 2, 3, 1).reshape(-1, K), w.view(w.size(0), K), None, 5)
+                y = y.view(B, H, W, -1).permute(0, 3, 1, 2)
+                dma = True  # (group-minor partials, as the LDS-DMA kernels leave them)
+            else:
+                y = torch.mm(x.permute(0, 2, 3, 1).reshape(-1, K), w.view(w.size(0), K).t())
+                y = y.view(B, H, W, -1).permute(0, 3, 1, 2)
+                part = C.bn_moments(y).view(1, 3, -1)
         else:
             y, part = C.conv1x1_gemm(x, w, stride, None, True)
         M = y.numel() // y.size(1)

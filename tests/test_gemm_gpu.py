@@ -112,3 +112,25 @@ def test_gemm_nt_dgelu_bias_grad(M, K, N):
     assert _rel(db, hf.grad.sum(0)) < 1e-2
     _, db32 = C.gemm_nt(a, w, None, 4, h)  # no bias: fp32 sums
     assert db32.dtype == torch.float32 and _rel(db32, hf.grad.sum(0)) < 5e-3
+
+
+@pytest.mark.parametrize("M,K,N,off", [(50176 // 8, 1024, 256, 0.0), (777, 2048, 512, 20.0), (300, 192, 384, 0.0)])
+def test_gemm_nt_statistics_epilogue(M, K, N, off):
+    """Epilogue 5: y = a @ w.T plus per-column BatchNorm statistics partials (group-minor
+    [3, N, mtiles]) of the stored bf16 y — the deep-K 1x1 conv forward with its BN's statistics."""
+    from distributeddataparallel_amd import native
+
+    C = native()
+    torch.manual_seed(3)
+    a = (torch.randn(M, K, device="cuda") + off).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    y, part = C.gemm_nt(a, w, None, 5)
+    ref = a.float() @ w.float().t()
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+    assert part.shape == (3, N, (M + 255) // 256)
+    yf = y.float()
+    rm, rv = torch.zeros(N, device="cuda"), torch.ones(N, device="cuda")
+    nbt = torch.zeros((), dtype=torch.long, device="cuda")
+    mean, invstd, _ = C.bn_stats_from_partials(part, M, None, None, rm, rv, nbt, 0.1, False, 1e-5, True)
+    torch.testing.assert_close(mean, yf.mean(0), rtol=1e-5, atol=1e-4 * yf.std(0).max().item())
+    torch.testing.assert_close(1.0 / invstd ** 2 - 1e-5, yf.var(0, unbiased=False), rtol=2e-3, atol=1e-6)
