@@ -88,6 +88,7 @@ std::vector<at::Tensor> ln_backward(const at::Tensor& dy, const at::Tensor& x, c
 void colsum_partials(const at::Tensor& part, at::Tensor& out);
 
 std::vector<at::Tensor> maxpool_forward(const at::Tensor& x, int64_t k, int64_t stride, int64_t pad);
+at::Tensor global_avg_pool_backward(const at::Tensor& g, const at::Tensor& x_like);
 // ResNet stem 7x7/s2 conv (3 -> 64) with BN-statistics partials, and its weight gradient
 // (csrc/kernels/stem_conv.hip)
 std::vector<at::Tensor> stem_conv_forward(const at::Tensor& x, const at::Tensor& w);

@@ -65,6 +65,7 @@ void bind_norm_kernels(py::module_& m) {
   m.def("stem_pool_bn_backward", &stem_pool_bn_backward, py::arg("dy"), py::arg("dy2"), py::arg("idx"), py::arg("x"),
         py::arg("scale_shift"), py::arg("mean"), py::arg("coef") = py::none());
   m.def("maxpool_forward", &maxpool_forward, py::arg("x"), py::arg("kernel"), py::arg("stride"), py::arg("pad"));
+  m.def("global_avg_pool_backward", &global_avg_pool_backward, py::arg("g"), py::arg("x_like"));
   m.def("maxpool_backward", &maxpool_backward, py::arg("dy"), py::arg("idx"), py::arg("x_like"), py::arg("kernel"),
         py::arg("stride"), py::arg("pad"), py::arg("dy2") = py::none());
   m.def("ln_forward", &ln_forward, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("rms"),

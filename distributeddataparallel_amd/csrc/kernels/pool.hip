@@ -392,6 +392,23 @@ __global__ __launch_bounds__(256) void stem_pool_bn_bwd_kernel(
   }
 }
 
+// Global average pool backward, channels_last: dX[b][h][w][c] = g[b][c] / (H·W). One lane per
+// 8 channels of one pixel (a 16-B store), the lane's 8 g values loaded once per pixel run.
+template <typename T, typename G>
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const G* __restrict__ g, T* __restrict__ dx, int64_t nvec,
+                                                       int C, int HW, float inv) {
+  const int cv = C / 8;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pix = v / cv;
+    const int c0 = (int)(v - pix * cv) * 8;
+    const int64_t b = pix / HW;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = dev::Elem<G, float>::ld(g, b * C + c0 + j) * inv;
+    dev::st8_stream(dx + v * 8, o);
+  }
+}
+
 template <typename F>
 void dispatch_pool(at::ScalarType st, F&& f) {
   switch (st) {
@@ -460,6 +477,32 @@ at::Tensor maxpool_backward(const at::Tensor& dy_in, const at::Tensor& idx, cons
                        dy2.defined() ? reinterpret_cast<const T*>(dy2.data_ptr()) : nullptr, idx.data_ptr<uint8_t>(),
                        reinterpret_cast<T*>(dx.data_ptr()), N, H, W, C, OH, OW, (int)k, (int)stride, (int)pad);
     XDDP_HIP_CHECK(hipGetLastError());
+  });
+  return dx;
+}
+
+// [B, C] gradient of a global average pool -> [B, C, H, W] channels_last (dtype of x_like)
+at::Tensor global_avg_pool_backward(const at::Tensor& g, const at::Tensor& x_like) {
+  TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() && x_like.dim() == 4 && g.size(0) == x_like.size(0) &&
+                  g.size(1) == x_like.size(1) && x_like.size(1) % 8 == 0,
+              "global_avg_pool_backward: g [B, C] contiguous, C % 8 == 0");
+  const int64_t B = x_like.size(0), C = x_like.size(1), H = x_like.size(2), W = x_like.size(3);
+  auto dx = at::empty({B, C, H, W}, x_like.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t nvec = B * H * W * (C / 8);
+  if (nvec == 0) return dx;
+  auto stream = c10::hip::getCurrentHIPStream(g.device().index()).stream();
+  dispatch_pool(x_like.scalar_type(), [&](auto tag) {
+    using T = decltype(tag);
+    auto go = [&](auto gtag) {
+      using G = decltype(gtag);
+      hipLaunchKernelGGL((gap_bwd_kernel<T, G>), dim3(grid_for(nvec)), dim3(256), 0, stream,
+                         reinterpret_cast<const G*>(g.data_ptr()), reinterpret_cast<T*>(dx.data_ptr()), nvec, (int)C,
+                         (int)(H * W), 1.f / (float)(H * W));
+      XDDP_HIP_CHECK(hipGetLastError());
+    };
+    if (g.scalar_type() == at::kFloat) go(float{});
+    else if (g.scalar_type() == at::kBFloat16) go(bf16_t{});
+    else TORCH_CHECK(false, "global_avg_pool_backward: g must be float or bf16");
   });
   return dx;
 }

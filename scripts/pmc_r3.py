@@ -1,4 +1,5 @@
-"""Workload for rocprofv3 --pmc passes over the round-2 kernels (VERDICT r2 "Next round" #7):
+"""Workload for rocprofv3 --pmc passes over the hand-written kernels (VERDICT r2 "Next round" #7; r3 adds
+the halo 3x3, the conv-on-gemm_nt path, the pending-apply prologues and the deep-K statistics GEMM):
 3x3 implicit-GEMM forward / stride-1 dgrad, 3x3 patch weight gradient, stem conv forward / weight
 gradient, flash attention forward / backward (dK/dV with fused dQ), and the conv1 input-gradient
 GEMM with the BN-reduce epilogue (EPI), and the transformer GEMM (gemm_nt) beside hipBLASLt.
@@ -48,13 +49,17 @@ def run(label, pattern, flops, nbytes, fn):
 ONLY_GEMM = "--only-gemm" in sys.argv  # stall-counter passes over the transformer GEMMs alone
 B = 256
 # 3x3 forward (+ BN statistics epilogue) and the stride-1 input gradient (same kernel, rotated W)
-for cin, hw in ((64, 56), (128, 28), (256, 14)):
+# (r3 routing: 64/128 channels on the halo kernel, 256/512 on gemm_nt's im2col pipeline)
+for cin, hw in ((64, 56), (128, 28), (256, 14), (512, 7)):
     x, w = bf(B, cin, hw, hw), bf(cin, cin, 3, 3, scale=(9 * cin) ** -0.5)
     m = B * hw * hw
     fl, by = 2.0 * m * cin * 9 * cin, 2.0 * (2 * x.numel() + w.numel())
-    run(f"conv3x3 fwd C{cin} {hw}x{hw}", "conv3x3_fwd_kernel", fl, by, lambda: C.conv3x3_forward(x, w, 1, True))
+    pat = "conv3x3_halo_kernel" if cin <= 128 else "gemm_nt_kernel"
+    run(f"conv3x3 fwd C{cin} {hw}x{hw}", pat, fl, by, lambda: C.conv3x3_forward(x, w, 1, True))
     wr = C.conv3x3_rot_weight(w)
-    run(f"conv3x3 dgrad C{cin} {hw}x{hw}", "conv3x3_fwd_kernel", fl, by, lambda: C.conv3x3_forward(x, wr, 1, False))
+    run(f"conv3x3 dgrad C{cin} {hw}x{hw}", pat, fl, by, lambda: C.conv3x3_forward(x, wr, 1, False))
+    if cin == 512:
+        continue
     run(f"conv3x3 wgrad(patch) C{cin} {hw}x{hw}", "conv3x3_wgrad_kernel", fl, 2.0 * 2 * x.numel() + 4 * w.numel(),
         lambda: C.conv3x3_wgrad_patch(x, x, 1, w))
 # stem 7x7/s2 (3 -> 64, 224 -> 112): forward with BN statistics, weight gradient
@@ -76,6 +81,25 @@ for hw, n, k in ((56, 256, 64), (28, 512, 128), (14, 1024, 256)):
     run(f"EPI dgrad N{n} K{k} {hw}x{hw}", "conv1x1_gemm_kernel", 2.0 * y.numel() * k,
         2.0 * (dy.numel() + 3 * y.numel()) + bits.numel(),
         lambda: C.conv1x1_gemm(dy, w, 1, None, False, None, True, add, y, bits, mean))
+# r3: pending block-output apply in conv1's GEMM prologue (relu(y3·s + t + identity), side output +
+# mask bits) and BN2's apply in conv3's (side output), layer-1 shapes; the deep-K conv1 forward on
+# gemm_nt with the statistics epilogue (layer 3)
+for label, (k, n, res) in (("pending block->conv1 K256 N64 56x56", (256, 64, True)),
+                          ("pending BN2->conv3 K64 N256 56x56", (64, 256, False))):
+    y3, wt = bf(B, k, 56, 56), bf(n, k, 1, 1, scale=k ** -0.5)
+    ss = torch.stack([torch.rand(k, device="cuda") + 0.5, torch.randn(k, device="cuda") * 0.2]).contiguous()
+    ident = bf(B, k, 56, 56) if res else None
+    side = torch.empty_like(y3)
+    bits = torch.empty(y3.numel() // 8, dtype=torch.uint8, device="cuda") if res else None
+    m = B * 56 * 56
+    by = 2.0 * (y3.numel() * (3 if res else 2) + m * n) + (y3.numel() / 8 if res else 0)
+    run(label, "conv1x1_gemm_kernel", 2.0 * m * n * k, by,
+        lambda: C.conv1x1_gemm(y3, wt, 1, ss, True, pro_out=side, pro_bits=bits, pro_res=ident))
+xd, wd = bf(B, 1024, 14, 14), bf(256, 1024, 1, 1, scale=1024 ** -0.5)
+md = B * 14 * 14
+run("deep-K conv1 fwd K1024 N256 14x14 (gemm_nt stats)", "gemm_nt_kernel", 2.0 * md * 256 * 1024,
+    2.0 * (xd.numel() + md * 256 + 256 * 1024), lambda: C.gemm_nt(xd.permute(0, 2, 3, 1).reshape(-1, 1024),
+                                                                  wd.view(256, 1024), None, 5))
 # flash attention, ViT-L/16 (197 tokens, 16 heads x 64) at 64 images, and a Llama-like causal shape
 for (b, s, h, d, causal) in ((64, 197, 16, 64, False), (2, 4096, 32, 128, True)):
     nc = torch.contiguous_format  # [B, S, H, D] row-major (channels_last would move D)

@@ -204,3 +204,20 @@ def test_batchnorm_backward_mask_modes_agree(dt):
     for d in dres_all[1:]:
         torch.testing.assert_close(d, dres_all[0], **tol)
     torch.testing.assert_close(dres_all[0], gsum.float() * (y.float() > 0), **tol)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_global_avg_pool_backward_kernel(dt):
+    """ops.pool.global_avg_pool on the GPU: the backward's broadcast of g / HW (pool.hip
+    gap_bwd_kernel) into a channels_last gradient equals adaptive_avg_pool2d's gradient."""
+    from distributeddataparallel_amd.ops.pool import global_avg_pool
+
+    torch.manual_seed(0)
+    x = torch.randn(4, 2048, 7, 7, device="cuda").to(dt).contiguous(memory_format=torch.channels_last).requires_grad_()
+    x2 = x.detach().clone().requires_grad_()
+    y, y2 = global_avg_pool(x), torch.flatten(torch.nn.functional.adaptive_avg_pool2d(x2, 1), 1)
+    g = torch.randn_like(y)
+    y.backward(g)
+    y2.backward(g)
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(x.grad.float(), x2.grad.float(), rtol=1e-2 if dt == torch.bfloat16 else 1e-6, atol=1e-6)
