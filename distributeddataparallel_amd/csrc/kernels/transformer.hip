@@ -262,10 +262,10 @@ std::vector<at::Tensor> bias_grad(const at::Tensor& g, const c10::optional<at::T
   auto dh = gelu ? at::empty_like(g) : at::Tensor();
   auto db = at::empty({N}, bias_like.options().memory_format(at::MemoryFormat::Contiguous));
   const int cpr = (int)(N / 8);
-  // each thread sums rows / rgroups rows of its column chunk. With GELU the pass also evaluates
-  // erf + exp per element and is latency/ALU-limited at 128K threads (8 waves per CU: 283 us,
-  // 4.4 TB/s on ViT-L/16's [50432, 4096]); 512K threads fill the CUs
-  const int64_t target = gelu ? 524288 : 131072;
+  // each thread sums rows / rgroups rows of its column chunk, one dependent 16-B load after
+  // another: at 128K threads (8 waves per CU) the pass is latency-limited (GELU: 283 us, 4.4 TB/s
+  // on ViT-L/16's [50432, 4096]; plain: 70 us, 1.5 TB/s on [50432, 1024]); 512K threads fill the CUs
+  const int64_t target = 524288;
   const int rgroups = (int)std::max<int64_t>(1, std::min<int64_t>(rows, (target + cpr - 1) / cpr));
   auto part = at::empty({rgroups, N}, g.options().dtype(at::kFloat));
   if (rows == 0) {
