@@ -109,6 +109,7 @@ at::Tensor rope(const at::Tensor& x, const at::Tensor& cosv, const at::Tensor& s
 at::Tensor swiglu_forward(const at::Tensor& a, const at::Tensor& b);
 std::vector<at::Tensor> swiglu_backward(const at::Tensor& g, const at::Tensor& a, const at::Tensor& b);
 at::Tensor gelu_forward(const at::Tensor& h);
+at::Tensor transpose16(const at::Tensor& x);
 std::vector<at::Tensor> bias_grad(const at::Tensor& g, const c10::optional<at::Tensor>& gelu_input,
                                   const at::Tensor& bias_like);
 

@@ -73,6 +73,7 @@ void bind_norm_kernels(py::module_& m) {
   m.def("ln_backward", &ln_backward, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
         py::arg("rms"), py::arg("need_dgamma"), py::arg("need_dbeta"), py::arg("res") = py::none());
   m.def("gelu_forward", &gelu_forward, py::arg("h"));
+  m.def("transpose16", &transpose16, py::arg("x"));
   m.def("bias_grad", &bias_grad, py::arg("grad"), py::arg("gelu_input") = py::none(), py::arg("bias_like"));
 }
 

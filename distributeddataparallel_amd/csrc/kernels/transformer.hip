@@ -145,6 +145,50 @@ __global__ __launch_bounds__(kBlock) void bias_grad_kernel(const T* __restrict__
   *reinterpret_cast<dev::f32x4*>(p + 4) = dev::f32x4{s[4], s[5], s[6], s[7]};
 }
 
+// 16-bit 2-D transpose [R][C] -> [C][R] through 64x64 LDS tiles (padded rows: conflict-free column
+// reads): the K-major copy of a weight a GEMM wants as [N][K] rows (e.g. ViT fc2's Wᵀ for the fused
+// dGELU input-gradient GEMM), at HBM speed instead of torch's strided-copy kernel.
+__global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                          int R, int C) {
+  __shared__ uint16_t tile[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  // full interior tiles (R, C multiples of 8 there) move 16 B per lane each way; edges go by element
+  const bool vec = r0 + 64 <= R && c0 + 64 <= C && (C & 7) == 0 && (R & 7) == 0;
+  if (vec) {
+#pragma unroll
+    for (int i = threadIdx.x; i < 64 * 8; i += 256) {  // 64 rows x 8 chunks of 8 columns
+      const int r = i >> 3, c = (i & 7) * 8;
+      const dev::u32x4 v = *reinterpret_cast<const dev::u32x4*>(in + (int64_t)(r0 + r) * C + c0 + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        tile[r][c + 2 * e] = (uint16_t)(v[e] & 0xffffu);
+        tile[r][c + 2 * e + 1] = (uint16_t)(v[e] >> 16);
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+      const int r = i >> 6, c = i & 63;
+      if (r0 + r < R && c0 + c < C) tile[r][c] = in[(int64_t)(r0 + r) * C + c0 + c];
+    }
+  }
+  __syncthreads();
+  if (vec) {
+#pragma unroll
+    for (int i = threadIdx.x; i < 64 * 8; i += 256) {  // 64 output rows (tile columns) x 8 chunks
+      const int c = i >> 3, r = (i & 7) * 8;
+      dev::u32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (uint32_t)tile[r + 2 * e][c] | ((uint32_t)tile[r + 2 * e + 1][c] << 16);
+      *reinterpret_cast<dev::u32x4*>(out + (int64_t)(c0 + c) * R + r0 + r) = v;
+    }
+  } else {
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+      const int c = i >> 6, r = i & 63;
+      if (c0 + c < C && r0 + r < R) out[(int64_t)(c0 + c) * R + r0 + r] = tile[r][c];
+    }
+  }
+}
+
 template <typename F>
 void dispatch16(at::ScalarType st, F&& f) {
   switch (st) {
@@ -228,6 +272,22 @@ std::vector<at::Tensor> swiglu_backward(const at::Tensor& g, const at::Tensor& a
     XDDP_HIP_CHECK(hipGetLastError());
   });
   return {da, db};
+}
+
+// [R, C] 16-bit contiguous -> its transpose [C, R] contiguous
+at::Tensor transpose16(const at::Tensor& x) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.is_contiguous() && x.element_size() == 2,
+              "transpose16: a contiguous 2-D 16-bit CUDA tensor expected");
+  const int64_t R = x.size(0), C = x.size(1);
+  TORCH_CHECK(R < (int64_t(1) << 31) / 64 && C < (int64_t(1) << 31) / 64, "transpose16: too large");
+  auto out = at::empty({C, R}, x.options());
+  if (R == 0 || C == 0) return out;
+  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
+  hipLaunchKernelGGL(transpose16_kernel, dim3((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64)), dim3(256), 0,
+                     stream, reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(out.data_ptr()),
+                     (int)R, (int)C);
+  XDDP_HIP_CHECK(hipGetLastError());
+  return out;
 }
 
 at::Tensor gelu_forward(const at::Tensor& h) {

@@ -94,7 +94,8 @@ class _EncoderBlockFn(torch.autograd.Function):
         g2 = g.reshape(-1, D).contiguous()
         # MLP
         if _own_gemm(D, w_1.shape[0], backward=True):  # dh = (g·W_2)·gelu'(h), Σ dh in the GEMM epilogue
-            dhid, db_1 = C.gemm_nt(g2, w_2.t().contiguous(), b_1, 4, h)
+            w_2t = C.transpose16(w_2) if w_2.is_contiguous() else w_2.t().contiguous()  # (LDS-tiled transpose)
+            dhid, db_1 = C.gemm_nt(g2, w_2t, b_1, 4, h)
         else:
             db_1, dhid = C.bias_grad(torch.mm(g2, w_2), h, b_1)
         dw_2 = torch.mm(g2.t(), a)

@@ -129,3 +129,12 @@ def test_fused_encoder_block_matches_fp32(own, monkeypatch):
     for n, (ef, eu) in errs.items():
         assert ef < 3e-2, (n, ef, eu)
         assert ef <= 1.5 * eu + 3e-3, (n, ef, eu)
+
+
+@pytest.mark.parametrize("R,Cc", [(1024, 4096), (77, 130), (1, 64), (192, 136)])
+def test_transpose16_matches_torch(R, Cc):
+    """The LDS-tiled 16-bit transpose (transformer.hip) equals torch's .t().contiguous() exactly."""
+    from distributeddataparallel_amd import native
+
+    x = torch.randn(R, Cc, device="cuda").to(torch.bfloat16)
+    assert torch.equal(native().transpose16(x), x.t().contiguous())
