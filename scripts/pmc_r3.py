@@ -36,6 +36,8 @@ def bf(*shape, scale=1.0, fmt=cl):
 def run(label, pattern, flops, nbytes, fn):
     if ONLY_GEMM and "gemm_nt" not in label and "hipBLASLt" not in label:
         return
+    if ONLY and not any(o in label for o in ONLY):
+        return
     fn()  # warm (first-call allocations, tuning) — not part of the plan
     torch.cuda.synchronize()
     plan.append({"label": label, "pattern": pattern, "calls": CALLS, "flops": float(flops), "bytes": float(nbytes)})
@@ -47,6 +49,8 @@ def run(label, pattern, flops, nbytes, fn):
 
 
 ONLY_GEMM = "--only-gemm" in sys.argv  # stall-counter passes over the transformer GEMMs alone
+# --only A,B,...: ops whose label contains one of the substrings (stall passes over a subset)
+ONLY = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
 B = 256
 # 3x3 forward (+ BN statistics epilogue) and the stride-1 input gradient (same kernel, rotated W)
 # (r3 routing: 64/128 channels on the halo kernel, 256/512 on gemm_nt's im2col pipeline)
