@@ -37,6 +37,8 @@
 // MI355X, Llama-3-8B shape (B1 S4096 H32/8 D128 causal): fwd 0.174 ms, fwd+bwd 0.939 ms vs torch
 // SDPA (AOTriton) 0.423 / 2.286 ms; ViT-L/16 (B64 S197 H16 D64): 0.043 / 0.190 vs 0.062 / 0.352 ms
 // (profiles/r2_flash_attn_v3.txt).
+#include <cstdlib>
+
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
@@ -156,14 +158,18 @@ __device__ __forceinline__ void dma_tile(const uint16_t* base, int64_t ss, int r
 // NW waves x 32 query rows per workgroup. At NW = 8 two waves share each SIMD, so one wave's
 // softmax, LDS reads and global-load waits overlap the other's MFMAs (at 4 waves, one per SIMD,
 // the kernel ran ~12K cycles per K/V tile against ~1K of MFMA work).
-template <int D, bool CAUSAL, int NW>
-__global__ __launch_bounds__(64 * NW) void fa_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+// WH (whole K/V, non-causal D = 64 with Sk <= 256: ViT's 197 tokens): every K/V tile of the head
+// is DMA'd up front (64 KB of LDS) and the tile loop runs without barriers; waves whose 32 query
+// rows all lie past Sq skip the math.
+template <int D, bool CAUSAL, int NW, bool WH = false>
+__global__ __launch_bounds__(64 * NW, WH ? 4 : 1) void fa_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                         const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
                                                         float* __restrict__ LSE, int Sq, int Sk, int Hq, int Hkv,
                                                         Strides qs, Strides ks, Strides vs, Strides os,
                                                         float scale_log2, int nqb) {
   constexpr int KS = D / 16, NT = D / 32, BQ = 32 * NW;
-  __shared__ __attribute__((aligned(16))) uint8_t KVs[2][2][kBK * D * 2];  // [stage][K, V]
+  static_assert(!WH || (!CAUSAL && D == 64), "whole-K/V staging is the non-causal D = 64 form");
+  __shared__ __attribute__((aligned(16))) uint8_t KVs[WH ? 4 : 2][2][kBK * D * 2];  // [stage or tile][K, V]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 5;
   const int bh = blockIdx.y, b = bh / Hq, h = bh % Hq, hk = h / (Hq / Hkv);
   const uint16_t* Qb = Q + b * qs.b + h * qs.h;
@@ -193,18 +199,28 @@ __global__ __launch_bounds__(64 * NW) void fa_fwd_kernel(const uint16_t* __restr
 
     const int kend = CAUSAL ? min(Sk, q0 + BQ) : Sk;
     const int ntiles = (kend + kBK - 1) / kBK;
-    dma_tile<D, NW>(Kb, ks.s, 0, Sk, KVs[0][0], w, lane);
-    dma_tile<D, NW>(Vb, vs.s, 0, Sk, KVs[0][1], w, lane);
+    if (WH) {
+      for (int j = 0; j < ntiles; ++j) {
+        dma_tile<D, NW>(Kb, ks.s, j * kBK, Sk, KVs[j][0], w, lane);
+        dma_tile<D, NW>(Vb, vs.s, j * kBK, Sk, KVs[j][1], w, lane);
+      }
+      dma_barrier();
+    } else {
+      dma_tile<D, NW>(Kb, ks.s, 0, Sk, KVs[0][0], w, lane);
+      dma_tile<D, NW>(Vb, vs.s, 0, Sk, KVs[0][1], w, lane);
+    }
     for (int j = 0; j < ntiles; ++j) {
       const int k0 = j * kBK;
-      dma_barrier();
-      if (j + 1 < ntiles) {  // next tile in flight during this tile's math
-        dma_tile<D, NW>(Kb, ks.s, k0 + kBK, Sk, KVs[(j + 1) & 1][0], w, lane);
-        dma_tile<D, NW>(Vb, vs.s, k0 + kBK, Sk, KVs[(j + 1) & 1][1], w, lane);
+      if (!WH) {
+        dma_barrier();
+        if (j + 1 < ntiles) {  // next tile in flight during this tile's math
+          dma_tile<D, NW>(Kb, ks.s, k0 + kBK, Sk, KVs[(j + 1) & 1][0], w, lane);
+          dma_tile<D, NW>(Vb, vs.s, k0 + kBK, Sk, KVs[(j + 1) & 1][1], w, lane);
+        }
       }
-      const uint8_t* Kt = KVs[j & 1][0];
-      const uint8_t* Vt = KVs[j & 1][1];
-      if (!CAUSAL || k0 <= qw + 31) {  // a wave whose rows all precede the tile skips it
+      const uint8_t* Kt = KVs[WH ? j : (j & 1)][0];
+      const uint8_t* Vt = KVs[WH ? j : (j & 1)][1];
+      if (WH ? qw < Sq : (!CAUSAL || k0 <= qw + 31)) {  // a wave whose rows all precede the tile skips it
         f32x16 sc[2];
 #pragma unroll
         for (int t = 0; t < 2; ++t)
@@ -743,7 +759,14 @@ std::vector<at::Tensor> flash_attn_forward(const at::Tensor& q, const at::Tensor
   };
 #define XDDP_FA(D_, C_) \
   if (nw == 8) go(fa_fwd_kernel<D_, C_, 8>); else go(fa_fwd_kernel<D_, C_, 4>)
+  // XDDP_FA_WHOLE=0: the double-buffered tile loop for the short non-causal heads too (A/Bs)
+  static const bool whole_ok = [] {
+    const char* e = std::getenv("XDDP_FA_WHOLE");
+    return !(e && e[0] == '0');
+  }();
+  const bool whole = whole_ok && D == 64 && !causal && Sk <= 4 * kBK;
   if (D == 128) { if (causal) { XDDP_FA(128, true); } else { XDDP_FA(128, false); } }
+  else if (whole) { if (nw == 8) go(fa_fwd_kernel<64, false, 8, true>); else go(fa_fwd_kernel<64, false, 4, true>); }
   else { if (causal) { XDDP_FA(64, true); } else { XDDP_FA(64, false); } }
 #undef XDDP_FA
   return {o, lse};

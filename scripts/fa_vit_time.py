@@ -1,0 +1,32 @@
+"""Time the flash attention forward at the ViT-L/16 bs256 head shape (B256, S197, H16, D64).
+
+usage: python scripts/fa_vit_time.py   (XDDP_FA_WHOLE=0 selects the double-buffered tile loop)
+Prints one JSON line: us per forward call.
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from distributeddataparallel_amd.ops.attention import flash_attention  # noqa: E402
+
+B, S, H, D = 256, 197, 16, 64
+torch.manual_seed(0)
+qkv = torch.randn(B, S, 3, H, D, device="cuda", dtype=torch.bfloat16)
+q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+for _ in range(3):
+    flash_attention(q, k, v)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+iters = 30
+e0.record()
+for _ in range(iters):
+    flash_attention(q, k, v)
+e1.record()
+torch.cuda.synchronize()
+us = e0.elapsed_time(e1) * 1e3 / iters
+tf = 4.0 * B * H * S * S * D / us / 1e6
+print(json.dumps({"shape": [B, S, H, D], "whole": os.environ.get("XDDP_FA_WHOLE", "1"), "fwd_us": round(us, 1),
+                  "tflops": round(tf, 1)}))

@@ -28,6 +28,7 @@ def _ref(q, k, v, causal, scale):
 
 @pytest.mark.parametrize("B,S,H,Hkv,D,causal", [
     (2, 197, 16, 16, 64, False),    # ViT-L/16 head shape (ragged S)
+    (16, 197, 16, 16, 64, False),   # ViT at a full-chip grid: the 8-wave whole-K/V forward
     (1, 512, 8, 2, 128, True),      # Llama-style causal GQA
     (2, 130, 4, 4, 128, True),      # ragged causal
     (1, 64, 2, 1, 64, True),        # one tile
