@@ -1,7 +1,7 @@
 """Time the flash attention forward at the ViT-L/16 bs256 head shape (B256, S197, H16, D64).
 
 usage: python scripts/fa_vit_time.py   (XDDP_FA_WHOLE=0 selects the double-buffered tile loop)
-Prints one JSON line: us per forward call.
+Prints one JSON line: us per forward call and per forward + backward.
 """
 import json
 import os
@@ -28,5 +28,24 @@ e1.record()
 torch.cuda.synchronize()
 us = e0.elapsed_time(e1) * 1e3 / iters
 tf = 4.0 * B * H * S * S * D / us / 1e6
+qkv.requires_grad_(True)
+q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+g = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+
+
+def step():
+    flash_attention(q, k, v).backward(g)
+    qkv.grad = None
+
+
+for _ in range(3):
+    step()
+torch.cuda.synchronize()
+e0.record()
+for _ in range(iters):
+    step()
+e1.record()
+torch.cuda.synchronize()
+fb = e0.elapsed_time(e1) * 1e3 / iters
 print(json.dumps({"shape": [B, S, H, D], "whole": os.environ.get("XDDP_FA_WHOLE", "1"), "fwd_us": round(us, 1),
-                  "tflops": round(tf, 1)}))
+                  "tflops": round(tf, 1), "fwd_bwd_us": round(fb, 1)}))
