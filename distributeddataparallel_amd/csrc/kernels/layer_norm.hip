@@ -7,6 +7,8 @@
 // accumulates dγ/dβ column partials in registers across the rows a block visits
 // (grid-stride), folded through LDS into one partial row per block and reduced by a second
 // small kernel — no float atomics, bitwise reproducible.
+#include <cstdlib>
+
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
@@ -96,7 +98,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 // RES: dx += res (the residual-stream gradient that bypasses this norm, so the caller's add pass
 // disappears), and two more column partials: Σ res and Σ dx — the bias gradients of the linear
 // layers whose outputs fed the residual sums after and before this norm. NP = RES ? 4 : 2.
-template <typename T, typename W, int NV, bool RMS, bool RES>
+// RPF: the narrow-row loop prefetches res with the next row's x / dy (false: res loaded in pass 2)
+template <typename T, typename W, int NV, bool RMS, bool RES, bool RPF = RES>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const W* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, T* __restrict__ dx,
@@ -125,11 +128,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
       if (gamma && c < D) Vec8<W>::ld(gamma + c, gm[k]);
       else for (int j = 0; j < 8; ++j) gm[k][j] = 1.f;
     }
-    // Software-pipelined over this wave's rows: the next row's x / dy (and mean, rstd) are loaded
-    // while the current row is reduced and written, and each row is read once (both passes run
-    // from registers) — the one-row-at-a-time version waited a full memory latency per pass.
+    // Software-pipelined over this wave's rows: the next row's x / dy / res (and mean, rstd) are
+    // loaded while the current row is reduced and written, and each row is read once (both passes
+    // run from registers) — the one-row-at-a-time version waited a full memory latency per pass,
+    // and a res loaded in pass 2 one latency per row (ViT-L/16 rows, residual form: 117 -> 107 us).
+    constexpr int NR = RPF ? NV : 1;
     const int64_t step = (int64_t)gridDim.x * kRowsPerBlock;
-    auto load_row = [&](int64_t r, float (&a)[NV][8], float (&d)[NV][8], float& mu, float& rs) {
+    auto load_row = [&](int64_t r, float (&a)[NV][8], float (&d)[NV][8], float (&rr)[NR][8], float& mu, float& rs) {
       mu = RMS ? 0.f : mean_in[r];
       rs = rstd_in[r];
   #pragma unroll
@@ -138,15 +143,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
         if (c < D) {
           Vec8<T>::ld(x + r * D + c, a[k]);
           Vec8<T>::ld(dy + r * D + c, d[k]);
+          if (RPF) Vec8<T>::ld(res + r * D + c, rr[RPF ? k : 0]);
         }
       }
     };
     int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w;
-    float a[NV][8], d[NV][8], mean = 0.f, rstd = 0.f;
-    if (row < rows) load_row(row, a, d, mean, rstd);
+    float a[NV][8], d[NV][8], rv[NR][8], mean = 0.f, rstd = 0.f;
+    if (row < rows) load_row(row, a, d, rv, mean, rstd);
     for (; row < rows; row += step) {
-      float na[NV][8], nd[NV][8], nmean = 0.f, nrstd = 0.f;
-      if (row + step < rows) load_row(row + step, na, nd, nmean, nrstd);
+      float na[NV][8], nd[NV][8], nr[NR][8], nmean = 0.f, nrstd = 0.f;
+      if (row + step < rows) load_row(row + step, na, nd, nr, nmean, nrstd);
       // pass 1: row reductions
       float s1 = 0.f, s2 = 0.f;
   #pragma unroll
@@ -168,8 +174,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
         const int c = (k * 64 + lane) * 8;
         if (c < D) {
           float o[8];
-          float r[8];
-          if (RES) Vec8<T>::ld(res + row * D + c, r);
+          if (RES && !RPF) Vec8<T>::ld(res + row * D + c, rv[0]);
   #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float xh = (a[k][j] - mean) * rstd;
@@ -180,8 +185,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
           if (RES) {
   #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              o[j] += r[j];
-              sr[RES ? k : 0][j] += r[j];
+              o[j] += rv[RPF ? k : 0][j];
+              sr[RES ? k : 0][j] += rv[RPF ? k : 0][j];
               so[RES ? k : 0][j] += o[j];
             }
           }
@@ -194,6 +199,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
         for (int j = 0; j < 8; ++j) {
           a[k][j] = na[k][j];
           d[k][j] = nd[k][j];
+          if (RPF) rv[RPF ? k : 0][j] = nr[RPF ? k : 0][j];
         }
       mean = nmean;
       rstd = nrstd;
@@ -422,7 +428,21 @@ std::vector<at::Tensor> ln_backward(const at::Tensor& dy_in, const at::Tensor& x
   const int nv = (D / 8 + 63) / 64;
   const bool need_part = dgamma.defined() || dbeta.defined() || hr;
   const int NP = hr ? 4 : 2;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + kRowsPerBlock - 1) / kRowsPerBlock, 1024));
+  // Block cap: the narrow-row (software-pipelined) loop runs at 2 waves per SIMD, so 512 blocks are
+  // exactly one resident round on 256 CUs (ViT-L/16 rows: 107 -> 100 us with the residual form,
+  // 96 -> 90 without, vs 1024 blocks; 2048 / 4096 were slower still). XDDP_LN_BWD_GRID overrides.
+  static const int grid_env = [] {
+    const char* e = std::getenv("XDDP_LN_BWD_GRID");
+    return e ? std::max(1, std::atoi(e)) : 0;
+  }();
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 256;
+  }();
+  const int grid_cap = grid_env ? grid_env : (nv <= 2 ? 2 * cus : 1024);
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + kRowsPerBlock - 1) / kRowsPerBlock, grid_cap));
   auto part = need_part ? at::empty({grid, NP, D}, x.options().dtype(at::kFloat)) : at::Tensor();
   if (rows == 0) return {dx, dgamma, dbeta, sres, sout};
   dispatch_t(x.scalar_type(), [&](auto tt) {
@@ -431,8 +451,14 @@ std::vector<at::Tensor> ln_backward(const at::Tensor& dy_in, const at::Tensor& x
       using W = decltype(tw);
       nv_dispatch<1>(nv, [&](auto nvc) {
         constexpr int NV = decltype(nvc)::value;
+        // XDDP_LN_RESPF=0: res loaded in pass 2 instead of with the prefetched row (A/Bs)
+        static const bool rpf = [] {
+          const char* e = std::getenv("XDDP_LN_RESPF");
+          return !(e && e[0] == '0');
+        }();
         auto k = rms ? ln_bwd_kernel<T, W, NV, true, false>
-                     : (hr ? ln_bwd_kernel<T, W, NV, false, true> : ln_bwd_kernel<T, W, NV, false, false>);
+                     : (hr ? (rpf ? ln_bwd_kernel<T, W, NV, false, true> : ln_bwd_kernel<T, W, NV, false, true, false>)
+                           : ln_bwd_kernel<T, W, NV, false, false>);
         hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, stream, reinterpret_cast<const T*>(dy.data_ptr()),
                            reinterpret_cast<const T*>(x.data_ptr()),
                            hg ? reinterpret_cast<const W*>(gamma->data_ptr()) : nullptr,
