@@ -40,6 +40,8 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
+LR_WARMUP_STEPS = 30  # linear lr warmup (optimizer steps)
+LOSS_GUARD = 1.1  # warn when the final loss ends above 1.1x the first step's
 
 
 def parse(argv=None):
@@ -80,9 +82,11 @@ def parse(argv=None):
                          "results shipped in tuning/tunableop (auto: for transformer models), tune = search "
                          "and write gpurun_out/tunableop_<model>.csv")
     ap.add_argument("--overlap-optim", choices=["auto", "0", "1"], default="auto",
-                    help="run the optimizer per bucket on a side stream during backward "
-                         "(DDP.register_overlapped_optimizer; auto = on for AdamW (transformer) configs at "
-                         "N>1, where it hides the last bucket's all-reduce, off otherwise)")
+                    help="run the optimizer inside backward on a side stream (DDP.register_overlapped_optimizer; "
+                         "auto = on for AdamW (transformer) configs at N>1, off otherwise)")
+    ap.add_argument("--overlap-schedule", choices=["tail", "backward"], default="tail",
+                    help="tail: updates deferred under the chunked tail all-reduce; backward: each bucket's "
+                         "update right after its own all-reduce")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     if a.batch_size is None:
@@ -381,17 +385,18 @@ def main(argv=None):
 
     B = args.batch_size
     micro = max(1, args.no_sync_accum)
-    # auto: at N=1 there is nothing to hide and it measured no gain on one MI355X (Llama-3-8B 16,726
-    # vs 16,779 tok/s, ViT-L/16 1,984 vs 1,970 img/s: hipBLASLt's backward GEMMs occupy every CU, so
-    # the side-stream AdamW interleaves with them). At N>1 the last bucket's all-reduce is exposed
-    # (Llama's 1.05 GB embedding gradient is ready last and forms the tail alone); the other
-    # buckets' updates run under it.
+    # auto: at N=1 there is nothing to hide. At N>1 the last bucket's all-reduce is exposed
+    # (Llama's 1.05 GB embedding gradient is ready last and forms the tail alone); the "tail"
+    # schedule defers every other bucket's AdamW update until the tail's (chunked) collectives are
+    # launched, so the updates run while the links carry the tail. (Updating during backward instead
+    # measured no gain on one MI355X — Llama-3-8B 16,726 vs 16,779 tok/s, ViT-L/16 1,984 vs 1,970
+    # img/s: hipBLASLt's backward GEMMs occupy every CU.)
     overlap_ok = args.impl == "xddp" and hasattr(opt, "step_params") and micro == 1 and not args.graphs
     overlap = args.overlap_optim == "1" or (args.overlap_optim == "auto" and world > 1 and overlap_ok)
     if overlap and not overlap_ok:
         raise SystemExit("--overlap-optim 1 needs the xddp DDP, an AdamW config, one micro-batch and no --graphs")
     if overlap:
-        ddp.register_overlapped_optimizer(opt)
+        ddp.register_overlapped_optimizer(opt, schedule=args.overlap_schedule)
     g = torch.Generator(device=device).manual_seed(1234 + rank)
     ncls = num_classes(args, model)
     if is_lm(args):
@@ -416,7 +421,22 @@ def main(argv=None):
 
         graphed = GraphedTrainStep(ddp, opt, loss_fn, xs[0], ys[0], warmup_steps=3)
 
+    # Linear learning-rate warmup over the first LR_WARMUP_STEPS optimizer steps (Goyal et al.'s
+    # large-batch recipe): lr 0.1 + momentum 0.9 from step 0 on a random-init ResNet-50 fitting a
+    # fixed batch leaves the descent at step ~11 in torch fp32 as well
+    # (profiles/r2_loss_curves_bench_config.txt). Host-side floats only: no kernel, no sync.
+    base_lrs = [grp["lr"] for grp in opt.param_groups]
+    n_opt_steps = [0]
+
+    def set_lr():
+        f = min(1.0, (n_opt_steps[0] + 1) / LR_WARMUP_STEPS)
+        for grp, lr in zip(opt.param_groups, base_lrs):
+            grp["lr"] = lr * f
+        n_opt_steps[0] += 1
+
     def step():
+        if graphed is None:
+            set_lr()
         if graphed is not None:
             return graphed(xs[0], ys[0])
         opt.zero_grad(set_to_none=True)
@@ -430,9 +450,11 @@ def main(argv=None):
         return loss
 
     first_loss = None
+    traj = []  # every step's loss tensor (references only: no copy, no sync in the timed loop)
     for i in range(args.warmup):
         tw = time.perf_counter()
         loss = step()
+        traj.append(loss.detach() if graphed is None else loss.detach().clone())
         if first_loss is None:
             first_loss = float(loss.float().item())
         if rank == 0:
@@ -445,6 +467,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+        traj.append(loss.detach() if graphed is None else loss.detach().clone())
     sync()
     dist.barrier()
     sync()
@@ -453,6 +476,9 @@ def main(argv=None):
     dist.all_reduce(et, op=dist.ReduceOp.MAX)
     elapsed = float(et.item())
     final_loss = float(loss.float().item())
+    lt = torch.stack([t.float().reshape(()) for t in traj]).cpu()
+    loss_min, loss_max = float(lt.min()), float(lt.max())
+    del traj
 
     # ---------------- diagnostics (outside the timed region)
     diag = {}
@@ -507,7 +533,7 @@ def main(argv=None):
                 "norm": args.norm,
                 "optimizer": ("SGD(momentum=0.9, wd=1e-4)" + (" fp32 master weights" if gpu else "")
                               if (conv or args.model == "mlp") else "AdamW(wd=0.1) fp32 master weights"),
-                "optimizer_overlapped_with_backward": bool(overlap),
+                "optimizer_schedule": args.overlap_schedule if overlap else "after backward",
                 "channels_last": bool(args.channels_last),
                 "comm_dtype": args.comm_dtype,
                 "gradient_as_bucket_view": bool(args.grad_as_bucket_view),
@@ -518,11 +544,17 @@ def main(argv=None):
             },
             "initial_loss": round(first_loss, 4) if first_loss is not None else None,
             "final_loss": round(final_loss, 4),
+            "loss_min": round(loss_min, 4),
+            "loss_max": round(loss_max, 4),
+            "lr_warmup_steps": LR_WARMUP_STEPS if graphed is None else 0,
             "scaling_efficiency": eff,
         }
-        if first_loss is not None and (final_loss != final_loss or final_loss > 2.0 * first_loss):
-            # diverging run guard: the number is still a throughput, but say the training blew up
-            out["warning"] = f"loss diverged: final {final_loss:.4g} > 2x first warmup step {first_loss:.4g}"
+        bad = [v for v in (final_loss, loss_max) if v != v or v in (float("inf"), float("-inf"))]
+        if first_loss is not None and (bad or final_loss > LOSS_GUARD * first_loss):
+            # divergence guard: the number is still a throughput, but say the training went wrong
+            # (the run fits one fixed batch, so its loss should not end above where it started)
+            out["warning"] = (f"loss diverged: final {final_loss:.4g} > {LOSS_GUARD}x the first step's "
+                              f"{first_loss:.4g} (min {loss_min:.4g}, max {loss_max:.4g})")
         if flops:
             tf = flops * per_step_samples / (ms * 1e-3) / 1e12
             out["model_tflops_per_gpu"] = round(tf / world, 1)
@@ -550,7 +582,9 @@ def diagnostics(args, ddp, step, sync, dist, device, world, overlap=False):
     out["buckets"] = {"count": len(sizes), "bytes": sizes, **ddp.bucket_plan.as_dict()}
     from distributeddataparallel_amd.parallel.bucket_policy import tail_report
 
-    out["buckets"]["tail"] = tail_report(sizes, ddp.bucket_plan, world, overlap)
+    ost = getattr(ddp, "_overlap_state", None)
+    out["buckets"]["tail"] = tail_report(sizes, ddp.bucket_plan, world, args.overlap_schedule if overlap else None,
+                                         ost["last_chunks"] if ost else 0)
     # what the communicator itself reports (RCCL at N>1: version, ranks, channels and rings parsed
     # from its init log) and every rank's device
     info = pg.comm_info()

@@ -68,26 +68,31 @@ __device__ __forceinline__ void st_release_sys(uint32_t* p, uint32_t v) {
 // would keep LDS-heavy compute kernels — the GEMMs and convolutions running concurrently on the
 // compute stream — off its CU until the peers arrive; when the peers share the GPU (2 processes
 // on one device) that is a deadlock broken only by the timeout.
+// The verdict is workgroup-wide: a wave whose peer timed out writes the call number into the
+// workgroup's own fail word (global memory, not LDS) before the block barrier, and every wave
+// reads it after the barrier, so all waves take the same branch and reach the same later
+// __syncthreads (per-wave verdicts could send some waves into a second barrier and others past it).
 __device__ __forceinline__ bool flag_barrier(const PeerPtrs& pp, int b, int rank, int size, uint32_t val,
-                                             int* status, uint64_t timeout_ticks) {
+                                             int* status, uint64_t timeout_ticks, uint32_t* fail_word,
+                                             uint32_t gen) {
   __threadfence_system();  // every thread's staging stores are visible system-wide before the flags go out
   __syncthreads();
   if (threadIdx.x < size) st_release_sys(pp.flags[threadIdx.x] + b * kPeerMaxRanks + rank, val);
   const int lane = threadIdx.x & 63;
-  bool ok = true;
   if (lane < size) {
     const uint32_t* f = pp.flags[rank] + b * kPeerMaxRanks + lane;
     const uint64_t t0 = wall_clock64();
     while (ld_acquire_sys(f) < val) {
       if (wall_clock64() - t0 > timeout_ticks) {
-        ok = false;
         __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(fail_word, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  ok = __all(ok);
+  __syncthreads();  // (workgroup-scope release/acquire: the fail word is visible to every wave)
+  const bool ok = __hip_atomic_load(fail_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != gen;
   __threadfence_system();  // acquire side for the lanes that did not poll
   return ok;
 }
@@ -131,6 +136,7 @@ __device__ __forceinline__ void copy_range(T* __restrict__ dst, const T* __restr
 template <typename T, int MODE, bool MAXOP = false>
 __global__ __launch_bounds__(kThreads) void peer_kernel(T* __restrict__ io, int64_t n, PeerPtrs pp, int rank,
                                                         int size, int root, uint32_t* __restrict__ gen_dev,
+                                                        uint32_t* __restrict__ fail_dev,
                                                         int* status, float scale, bool do_scale,
                                                         uint64_t timeout_ticks, int64_t slot_bytes, int64_t chunk,
                                                         T* __restrict__ out) {
@@ -149,7 +155,7 @@ __global__ __launch_bounds__(kThreads) void peer_kernel(T* __restrict__ io, int6
   // 1. stage this workgroup's chunk (empty for the workgroups past the end of the message)
   if (!BCAST || rank == root) copy_range(mine, io, lo, hi);
   // 2. cross-rank barrier on this workgroup's flags
-  if (flag_barrier(pp, b, rank, size, 2u * gen, status, timeout_ticks)) {
+  if (flag_barrier(pp, b, rank, size, 2u * gen, status, timeout_ticks, fail_dev + b, gen)) {
     // 3. reduce (or read the root's copy) straight from the peers' slots
     const int64_t nv = (hi - lo) / V;
     if (MODE == 2) {
@@ -194,8 +200,8 @@ __global__ __launch_bounds__(kThreads) void peer_kernel(T* __restrict__ io, int6
 // [lo + s*cs, lo + (s+1)*cs), cs = chunk / W (a multiple of the 16-B vector). Rank r reduces slice r.
 template <typename T, int W>
 __global__ __launch_bounds__(kThreads) void two_shot_kernel(T* __restrict__ io, int64_t n, PeerPtrs pp, int rank,
-                                                            uint32_t* __restrict__ gen_dev, int* status, float scale,
-                                                            bool do_scale, uint64_t timeout_ticks, int64_t slot_bytes,
+                                                            uint32_t* __restrict__ gen_dev, uint32_t* __restrict__ fail_dev,
+                                                            int* status, float scale, bool do_scale, uint64_t timeout_ticks, int64_t slot_bytes,
                                                             int64_t chunk) {
   constexpr int V = 16 / sizeof(T);
   using A = typename Acc<T>::type;
@@ -214,7 +220,7 @@ __global__ __launch_bounds__(kThreads) void two_shot_kernel(T* __restrict__ io, 
   // 1. stage the slices the peers will reduce (not my own: I reduce it from io directly)
   copy_range(mine, io, lo, my_lo);
   copy_range(mine, io, my_hi, hi);
-  if (flag_barrier(pp, b, rank, W, 2u * gen - 1u, status, timeout_ticks)) {
+  if (flag_barrier(pp, b, rank, W, 2u * gen - 1u, status, timeout_ticks, fail_dev + b, gen)) {
     // 2. reduce my slice from every rank, in rank order (every rank gets bitwise the same sum);
     // the result goes to io and to my staging slot, where the peers gather it from
     const T* src[W];
@@ -245,7 +251,7 @@ __global__ __launch_bounds__(kThreads) void two_shot_kernel(T* __restrict__ io, 
       mine[i] = o;
     }
     // 3. gather the other ranks' reduced slices
-    if (flag_barrier(pp, b, rank, W, 2u * gen, status, timeout_ticks)) {
+    if (flag_barrier(pp, b, rank, W, 2u * gen, status, timeout_ticks, fail_dev + b, gen)) {
 #pragma unroll
       for (int r = 0; r < W; ++r) {
         if (r == rank) continue;
@@ -277,8 +283,9 @@ struct PeerLane {
     // uncached: the flags and staged data are read by the peers over xGMI while this GPU writes them
     XDDP_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&own), bytes, hipDeviceMallocUncached));
     XDDP_HIP_CHECK(hipMemset(own, 0, bytes));
-    XDDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&gen_dev), nblocks * sizeof(uint32_t)));
-    XDDP_HIP_CHECK(hipMemset(gen_dev, 0, nblocks * sizeof(uint32_t)));
+    // per workgroup: its call counter, then its fail word (the call number of a timed-out barrier)
+    XDDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&gen_dev), 2 * nblocks * sizeof(uint32_t)));
+    XDDP_HIP_CHECK(hipMemset(gen_dev, 0, 2 * nblocks * sizeof(uint32_t)));
     XDDP_HIP_CHECK(hipDeviceSynchronize());
     hipIpcMemHandle_t h;
     XDDP_HIP_CHECK(hipIpcGetMemHandle(&h, own));
@@ -413,7 +420,8 @@ void PeerAllReduce::launch(at::Tensor t, at::Tensor out, RedOp op, int root, int
   const bool do_scale = op == RedOp::AVG;
   auto go = [&](auto kern, auto* io, auto* o) {
     hipLaunchKernelGGL(kern, dim3((unsigned)L.blocks), dim3(kThreads), 0, s, io, n, L.pp, rank_, size_, root,
-                       L.gen_dev, impl_->status_dev, scale, do_scale, impl_->timeout_ticks, L.slot_bytes, chunk, o);
+                       L.gen_dev, L.gen_dev + L.blocks, impl_->status_dev, scale, do_scale, impl_->timeout_ticks,
+                       L.slot_bytes, chunk, o);
   };
   void* p = t.data_ptr();
   void* q = out.data_ptr();
@@ -453,7 +461,7 @@ void launch_two_shot_w(T* io, int64_t n, PeerLane& L, int rank, int* status, flo
   int64_t chunk = (n + L.blocks - 1) / L.blocks;
   chunk = (chunk + W * V - 1) / (W * V) * (W * V);  // every slice a whole number of vectors
   hipLaunchKernelGGL((two_shot_kernel<T, W>), dim3((unsigned)L.blocks), dim3(kThreads), 0, s, io, n, L.pp, rank,
-                     L.gen_dev, status, scale, do_scale, ticks, L.slot_bytes, chunk);
+                     L.gen_dev, L.gen_dev + L.blocks, status, scale, do_scale, ticks, L.slot_bytes, chunk);
 }
 
 template <typename T>

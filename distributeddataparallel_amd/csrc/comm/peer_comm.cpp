@@ -40,7 +40,7 @@ namespace {
 // Shared error state of one communicator: 0 ok, 1 peer timeout, 3 a peer rank reported an error.
 struct PeerState {
   std::atomic<int> err{0};
-  PeerAllReduce* peer = nullptr;
+  std::shared_ptr<PeerAllReduce> peer;  // shared: a Work may outlive its communicator
   void check() {
     int e = err.load();
     if (e == 0 && peer && peer->status() != 0) {
@@ -109,10 +109,10 @@ class PeerComm : public Comm {
         store_(store),
         device_(device),
         stream_(c10::hip::getStreamFromPool(true, static_cast<c10::DeviceIndex>(device))),
-        peer_(std::make_unique<PeerAllReduce>(std::move(store), rank, size, device, capacity, two_shot_capacity,
+        peer_(std::make_shared<PeerAllReduce>(std::move(store), rank, size, device, capacity, two_shot_capacity,
                                               timeout)),
         st_(std::make_shared<PeerState>()) {
-    st_->peer = peer_.get();
+    st_->peer = peer_;
     const char* m = std::getenv("XDDP_PEER_TWO_SHOT_MIN_BYTES");
     two_shot_min_ = m ? std::atoll(m) : (256 << 10);
     watchdog_ = std::thread([this] { watchdog_loop(); });
@@ -333,7 +333,7 @@ class PeerComm : public Comm {
   std::shared_ptr<Store> store_;
   int device_;
   c10::hip::HIPStream stream_;
-  std::unique_ptr<PeerAllReduce> peer_;
+  std::shared_ptr<PeerAllReduce> peer_;
   std::shared_ptr<PeerState> st_;
   int64_t two_shot_min_ = 0;
   at::Tensor barrier_buf_;

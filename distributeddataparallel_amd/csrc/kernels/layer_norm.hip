@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 // RES: dx += res (the residual-stream gradient that bypasses this norm, so the caller's add pass
 // disappears), and two more column partials: Σ res and Σ dx — the bias gradients of the linear
 // layers whose outputs fed the residual sums after and before this norm. NP = RES ? 4 : 2.
-// RPF: the narrow-row loop prefetches res with the next row's x / dy (false: res loaded in pass 2)
+// With RES the narrow-row loop prefetches res with the next row's x / dy (RPF).
 template <typename T, typename W, int NV, bool RMS, bool RES, bool RPF = RES>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const W* __restrict__ gamma, const float* __restrict__ mean_in,
@@ -430,18 +430,14 @@ std::vector<at::Tensor> ln_backward(const at::Tensor& dy_in, const at::Tensor& x
   const int NP = hr ? 4 : 2;
   // Block cap: the narrow-row (software-pipelined) loop runs at 2 waves per SIMD, so 512 blocks are
   // exactly one resident round on 256 CUs (ViT-L/16 rows: 107 -> 100 us with the residual form,
-  // 96 -> 90 without, vs 1024 blocks; 2048 / 4096 were slower still). XDDP_LN_BWD_GRID overrides.
-  static const int grid_env = [] {
-    const char* e = std::getenv("XDDP_LN_BWD_GRID");
-    return e ? std::max(1, std::atoi(e)) : 0;
-  }();
+  // 96 -> 90 without, vs 1024 blocks; 2048 / 4096 were slower still: profiles/r3_ln_bwd_ab.txt).
   static const int cus = [] {
     int dev = 0, v = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
     return v > 0 ? v : 256;
   }();
-  const int grid_cap = grid_env ? grid_env : (nv <= 2 ? 2 * cus : 1024);
+  const int grid_cap = nv <= 2 ? 2 * cus : 1024;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + kRowsPerBlock - 1) / kRowsPerBlock, grid_cap));
   auto part = need_part ? at::empty({grid, NP, D}, x.options().dtype(at::kFloat)) : at::Tensor();
   if (rows == 0) return {dx, dgamma, dbeta, sres, sout};
@@ -451,14 +447,8 @@ std::vector<at::Tensor> ln_backward(const at::Tensor& dy_in, const at::Tensor& x
       using W = decltype(tw);
       nv_dispatch<1>(nv, [&](auto nvc) {
         constexpr int NV = decltype(nvc)::value;
-        // XDDP_LN_RESPF=0: res loaded in pass 2 instead of with the prefetched row (A/Bs)
-        static const bool rpf = [] {
-          const char* e = std::getenv("XDDP_LN_RESPF");
-          return !(e && e[0] == '0');
-        }();
         auto k = rms ? ln_bwd_kernel<T, W, NV, true, false>
-                     : (hr ? (rpf ? ln_bwd_kernel<T, W, NV, false, true> : ln_bwd_kernel<T, W, NV, false, true, false>)
-                           : ln_bwd_kernel<T, W, NV, false, false>);
+                     : (hr ? ln_bwd_kernel<T, W, NV, false, true> : ln_bwd_kernel<T, W, NV, false, false>);
         hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, stream, reinterpret_cast<const T*>(dy.data_ptr()),
                            reinterpret_cast<const T*>(x.data_ptr()),
                            hg ? reinterpret_cast<const W*>(gamma->data_ptr()) : nullptr,

@@ -359,6 +359,7 @@ void Reducer::prepare_for_forward() {
     }
   }
   harvest_timings();
+  if (!timing_pending_) timed_works_.clear();  // (a backward that raised may have left some)
   num_iterations_++;
   timing_this_iter_ = !timing_pending_ && (num_iterations_ <= 10 || num_iterations_ % sample_rate_ == 0);
   timer_record(0);
@@ -388,7 +389,6 @@ void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs) {
     TORCH_CHECK(false, os.str());
   }
   timer_record(1);
-  if (timing_this_iter_) comm_->set_timing(true);
   expect_hooks_ = true;
   require_finalize_ = true;
   finalize_queued_ = false;
@@ -520,6 +520,24 @@ void Reducer::mark_bucket_ready(int64_t b) {
 }
 
 void Reducer::launch_bucket(int64_t b) {
+  // Comm timing covers exactly the collectives issued for this bucket (the builtin all-reduce, or
+  // whatever a comm hook launches for it), tagged with the bucket index: other users of the
+  // process group during backward (SyncBN, another DDP model) are never counted, and timing is
+  // off again even when the launch throws.
+  if (!timing_this_iter_) return launch_bucket_impl(b);
+  comm_->set_timing(true);
+  try {
+    launch_bucket_impl(b);
+  } catch (...) {
+    comm_->set_timing(false);
+    comm_->drain_timed_works();
+    throw;
+  }
+  comm_->set_timing(false);
+  for (auto& w : comm_->drain_timed_works()) timed_works_.emplace_back(b, std::move(w));
+}
+
+void Reducer::launch_bucket_impl(int64_t b) {
   RECORD_FUNCTION("xddp::reducer::launch_bucket", std::vector<c10::IValue>());
   Range range("xddp::reducer::launch_bucket");
   auto& bk = buckets_[b];
@@ -701,12 +719,7 @@ void Reducer::finalize_backward() {
   for (auto& f : post_bwd_futs_) f->wait();
   post_bwd_futs_.clear();
   timer_record(4);
-  if (timing_this_iter_) {
-    timing_pending_ = true;
-    comm_->set_timing(false);
-    auto ws = comm_->drain_timed_works();
-    for (size_t i = 0; i < ws.size(); ++i) timed_works_.emplace_back(static_cast<int64_t>(i), std::move(ws[i]));
-  }
+  if (timing_this_iter_) timing_pending_ = true;
   timing_this_iter_ = false;
   if (!has_rebuilt_) prev_ready_order_ = ready_order_;
   expect_hooks_ = false;

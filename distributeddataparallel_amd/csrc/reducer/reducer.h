@@ -151,6 +151,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   void mark_variable_ready(int64_t index);
   void mark_bucket_ready(int64_t b);
   void launch_bucket(int64_t b);
+  void launch_bucket_impl(int64_t b);
   void finalize_backward();
   void search_unused_parameters(const std::vector<at::Tensor>& outputs);
   void all_reduce_local_used_map();

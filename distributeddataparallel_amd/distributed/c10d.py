@@ -336,8 +336,13 @@ def _make_comm(backend: str, store, rank: int, size: int, device, timeout: timed
         info = rccl_info.collect(log)
     elif backend == "peer":  # IPC peer memory, one node, device tensors (csrc/comm/peer_comm.cpp)
         mb = lambda k, d: max(0, int(float(os.environ.get(k, d)) * (1 << 20)) // 4096 * 4096)  # noqa: E731
+        # The device-side wait bound of the peer kernels: a rank that died leaves its peers' workgroups
+        # spinning until it expires (the peer watchdog learns of the failure from the status word), so
+        # it is capped at XDDP_PEER_DEVICE_TIMEOUT_S (default 120 s) rather than the group's 30-minute
+        # timeout; XDDP_PEER_TIMEOUT_MS still overrides both.
+        dev_to = min(timeout.total_seconds(), float(os.environ.get("XDDP_PEER_DEVICE_TIMEOUT_S", "120")))
         comm = C.make_peer_comm(store, rank, size, device.index, max(mb("XDDP_PEER_CAPACITY_MB", "16"), 4096),
-                                mb("XDDP_PEER_TWO_SHOT_MB", "64"), timeout.total_seconds())
+                                mb("XDDP_PEER_TWO_SHOT_MB", "64"), dev_to)
     else:
         comm = C.make_cpu_comm(store, rank, size, timeout.total_seconds(), advertise_host(master_addr))
     detail = os.environ.get("XDDP_DEBUG", os.environ.get("TORCH_DISTRIBUTED_DEBUG", "OFF")).upper() == "DETAIL"

@@ -141,8 +141,10 @@ class Bottleneck(nn.Module):
             if ds is not None and link is None:
                 identity = conv1x1_bn_act(xr, ds[0], ds[1], defer=defer)
             out = conv1x1_bn_act(x, self.conv1, self.bn1, relu=True, link_x=link)
-            # BN2's apply happens in conv3's GEMM prologue (ops/conv_bn.py:PendingApply)
-            out = self.act2(conv3x3_bn_relu(out, self.conv2, self.bn2, pending=True))
+            # BN2's apply happens in conv3's GEMM prologue (ops/conv_bn.py:PendingApply) — only
+            # inside ResNet.forward with no hook anywhere in the blocks (a hook on act2 would
+            # otherwise see a tensor conv3's prologue has not written yet)
+            out = self.act2(conv3x3_bn_relu(out, self.conv2, self.bn2, pending=_pending_ok()))
             if ds is None:
                 identity = xr
             elif link is not None:  # issued after conv2: its backward runs before conv1's
@@ -220,14 +222,15 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def _no_block_hooks(self) -> bool:
-        """No forward hook can see a block output (a pending one must not be read before the next
-        block's conv1 writes it): none on the layers, their blocks, or globally."""
+        """No forward hook can see a pending tensor (a block output, or BN2's output inside a block,
+        must not be read before the consuming conv's prologue writes it): none on the layers, any
+        module inside their blocks (act2 included), or globally."""
         from torch.nn.modules import module as _mod
 
         if _mod._global_forward_hooks or _mod._global_forward_pre_hooks:
             return False
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
-            for m in (layer, *layer.children()):
+            for m in layer.modules():
                 if m._forward_hooks or m._forward_pre_hooks:
                     return False
         return True

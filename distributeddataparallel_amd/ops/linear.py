@@ -10,7 +10,7 @@ the same as the eager model's.
 epilogues included), ``bwd`` (default) only the backward GEMM that carries a fused epilogue
 hipBLASLt cannot do (the ViT MLP's dGELU + bias gradient), ``0`` nowhere. On one MI355X the own
 kernel reaches 0.80-0.93x hipBLASLt's plain-GEMM speed on the transformer shapes
-(``profiles/r3_gemm_nt_vs_hipblaslt_v4.txt``), so forward projections stay on hipBLASLt, whose
+(``profiles/r3_gemm_nt_vs_hipblaslt.txt``), so forward projections stay on hipBLASLt, whose
 beta = 1 residual accumulate is free, unless asked for.
 """
 from __future__ import annotations

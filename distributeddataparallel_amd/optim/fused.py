@@ -30,6 +30,16 @@ def _dense_like(p: torch.Tensor) -> torch.Tensor:
     return torch.empty_strided(p.size(), p.stride(), dtype=torch.float32, device=p.device)
 
 
+def _flat_range(t: torch.Tensor, lo: int, hi: int) -> torch.Tensor:
+    """Elements [lo, hi) of a dense (possibly permuted-stride) tensor in memory order, as a 1-D view."""
+    expect = 1
+    for st, sz in sorted((st, sz) for st, sz in zip(t.stride(), t.size()) if sz != 1):
+        if st != expect:
+            raise ValueError("slice updates need dense parameters / gradients / states")
+        expect *= sz
+    return t.as_strided((hi - lo,), (1,), t.storage_offset() + lo)
+
+
 class FusedSGD(Optimizer):
     """SGD with momentum/dampening/Nesterov/weight decay (torch.optim.SGD semantics).
 
@@ -157,38 +167,69 @@ class FusedAdamW(Optimizer):
                     self._cpu_step(ps, gs, m1, m2, masters, group, step, grad_scale)
         return loss
 
+    def _group_index(self, p):
+        if not hasattr(self, "_group_of"):
+            self._group_of = {id(q): gi for gi, grp in enumerate(self.param_groups) for q in grp["params"]}
+        return self._group_of.get(id(p))
+
+    def _init_state(self, p, group):
+        st = self.state[p]
+        if "step" not in st:
+            st["step"] = 0
+            st["exp_avg"] = _dense_like(p).zero_()
+            st["exp_avg_sq"] = _dense_like(p).zero_()
+            if group["master_weights"] and p.dtype in (torch.bfloat16, torch.float16):
+                st["master"] = p.detach().float().clone(memory_format=torch.preserve_format)
+        return st
+
     @torch.no_grad()
     def step_params(self, params, grads):
         """Step only ``params`` with the given gradients (e.g. one DDP bucket's reduced views, from
         an overlapped-optimizer comm hook): same update as ``step`` for those parameters."""
+        live = [(p, g) for p, g in zip(params, grads) if g is not None and self._group_index(p) is not None]
+        self.advance([p for p, _ in live])
+        self.step_slices([(p, g, 0, p.numel()) for p, g in live])
+
+    @torch.no_grad()
+    def advance(self, params):
+        """Start this step for ``params`` (state created on first use, step count + 1) without
+        updating them; :meth:`step_slices` then updates them piecewise with that step count."""
+        for p in params:
+            gi = self._group_index(p)
+            if gi is not None:
+                self._init_state(p, self.param_groups[gi])["step"] += 1
+
+    @torch.no_grad()
+    def step_slices(self, pieces):
+        """Update element ranges of parameters: ``pieces`` = ``[(param, grad, lo, hi)]`` with
+        ``[lo, hi)`` in memory order of the (dense) param; ``grad`` has the param's shape and
+        strides. Uses each param's current step count (:meth:`advance` first). AdamW is elementwise,
+        so updating a param in several slices is bitwise the same as updating it at once — the
+        overlapped optimizer steps a chunked tail bucket this way, chunk by chunk as each chunk's
+        all-reduce lands."""
         C = load()
-        if not hasattr(self, "_group_of"):
-            self._group_of = {id(p): gi for gi, grp in enumerate(self.param_groups) for p in grp["params"]}
         per_group = defaultdict(list)
-        for p, g in zip(params, grads):
-            gi = self._group_of.get(id(p))
-            if gi is not None and g is not None:
-                per_group[gi].append((p, g))
-        for gi, pairs in per_group.items():
+        for p, g, lo, hi in pieces:
+            gi = self._group_index(p)
+            if gi is not None and g is not None and hi > lo:
+                per_group[gi].append((p, g, lo, hi))
+        for gi, items in per_group.items():
             group = self.param_groups[gi]
             b1, b2 = group["betas"]
             buckets = defaultdict(lambda: ([], [], [], [], [], []))
-            for p, g in pairs:
-                st = self.state[p]
-                if "step" not in st:
-                    st["step"] = 0
-                    st["exp_avg"] = _dense_like(p).zero_()
-                    st["exp_avg_sq"] = _dense_like(p).zero_()
-                    if group["master_weights"] and p.dtype in (torch.bfloat16, torch.float16):
-                        st["master"] = p.detach().float().clone(memory_format=torch.preserve_format)
-                st["step"] += 1
+            for p, g, lo, hi in items:
+                st = self._init_state(p, group)
+                if st["step"] == 0:
+                    raise RuntimeError("step_slices before advance() for this step")
                 b = buckets[_group_key(p, g) + (st["step"], "master" in st)]
-                b[0].append(p)
-                b[1].append(g)
-                b[2].append(st["exp_avg"])
-                b[3].append(st["exp_avg_sq"])
+                whole = lo == 0 and hi == p.numel()
+                cut = (lambda t: t) if whole else (lambda t: _flat_range(t, lo, hi))
+                b[0].append(cut(p))
+                b[1].append(cut(g))
+                b[2].append(cut(st["exp_avg"]))
+                b[3].append(cut(st["exp_avg_sq"]))
                 if "master" in st:
-                    b[4].append(st["master"])
+                    b[4].append(cut(st["master"]))
             for (dev, pdt, gdt, step, has_master), (ps, gs, m1, m2, masters, _) in buckets.items():
                 if dev.type == "cuda":
                     C.fused_adam(ps, gs, m1, m2, masters, group["lr"], b1, b2, group["eps"], group["weight_decay"],

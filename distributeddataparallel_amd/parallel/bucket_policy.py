@@ -39,12 +39,15 @@ Decisions, in gradient-ready order (the order buckets launch in):
 At W=1 nothing is communicated and the policy only changes the bucket layout.
 
 A tail bucket cannot split a tensor: when the last-ready gradient is itself large (Llama-3-8B's
-1.05 GB token embedding) the tail IS that tensor and its all-reduce (~5 ms modelled at W=8) is
-exposed whatever the caps. :func:`tail_report` states the modelled exposed time and the
-mitigation in use: with the overlapped optimizer (``DDP.register_overlapped_optimizer``, the
-bench default for transformer configs at W>1) every other bucket's AdamW update runs on a side
-stream while the tail all-reduce is in flight, so the tail hides behind optimizer work that the
-step has to do anyway.
+1.05 GB token embedding) the tail IS that tensor and its all-reduce (~5 ms modelled at W=8) cannot
+overlap backward. What can run under it is the optimizer: with the overlapped optimizer's
+``"tail"`` schedule (``DDP.register_overlapped_optimizer``, the bench default for AdamW configs at
+W>1) every other bucket's update is DEFERRED until the tail's collectives are launched, the tail is
+all-reduced in chunks (``XDDP_TAIL_CHUNK_MB``, default 64 MiB), and the side stream runs the
+deferred updates and then each tail chunk's update as soon as that chunk lands. The GPU then does
+the step's optimizer work while the links carry the tail, and at most one chunk's update remains
+after the last collective. :func:`tail_report` states the modelled exposed time and which of these
+mechanisms the run used.
 
 RCCL knobs (:func:`rccl_env_defaults`): none are forced. RCCL picks its channel count for the
 node's topology; an unmeasured cap could cut large-bucket bandwidth on the 7-link mesh. A cap
@@ -146,23 +149,35 @@ def exposed_tail_us(sizes: List[int], world_size: int, alpha_us: float | None = 
     return alpha + 2.0 * (w - 1) / w * sizes[-1] / (bw * 1e3)
 
 
-def tail_report(sizes: List[int], plan: BucketPlan, world_size: int, overlapped_optimizer: bool) -> dict:
-    """The tail bucket as built, its modelled exposed all-reduce time, and what hides it."""
+def tail_report(sizes: List[int], plan: BucketPlan, world_size: int, overlapped_optimizer=None,
+                tail_chunks: int = 0) -> dict:
+    """The tail bucket as built, its modelled exposed all-reduce time, and what hides it.
+
+    ``overlapped_optimizer``: None/False (optimizer.step() after backward), ``"tail"`` (updates
+    deferred under the chunked tail all-reduce) or ``"backward"``/True (each bucket's update right
+    after its own all-reduce, during backward); ``tail_chunks``: collectives the tail was split into."""
     if not sizes:
         return {}
+    if overlapped_optimizer is True:
+        overlapped_optimizer = "backward"
     exposed = exposed_tail_us(sizes, world_size) if world_size > 1 else 0.0
     over_cap = plan.tail_bytes > 0 and sizes[-1] > plan.tail_bytes
     if world_size <= 1:
         mitigation = "none needed (one rank: nothing is communicated)"
-    elif overlapped_optimizer:
-        mitigation = ("overlapped optimizer: the other buckets' updates run on a side stream while the tail "
-                      "all-reduce is in flight")
+    elif overlapped_optimizer == "tail":
+        mitigation = (f"deferred optimizer: the other buckets' updates run on a side stream concurrently with the "
+                      f"tail all-reduce, issued as {max(1, tail_chunks)} chunk(s); each chunk's update follows its "
+                      f"own collective")
+    elif overlapped_optimizer == "backward":
+        mitigation = ("none for the tail: each bucket's update runs during backward right after its own "
+                      "all-reduce; the tail all-reduce and the tail's update are exposed")
     elif plan.tail_bytes > 0 and not over_cap:
         mitigation = f"tail cap: the last bucket holds <= {plan.tail_bytes} B"
     else:
         mitigation = "none"
     return {"tail_bytes": int(sizes[-1]), "tail_cap_bytes": int(plan.tail_bytes),
             "tail_is_one_tensor_over_cap": bool(over_cap), "exposed_tail_us_model": round(exposed, 1),
+            "optimizer_schedule": overlapped_optimizer or "after backward", "tail_chunks": int(tail_chunks),
             "mitigation": mitigation}
 
 

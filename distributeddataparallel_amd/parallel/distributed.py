@@ -111,6 +111,16 @@ class _CastParams(torch.autograd.Function):
         return (None, *res)
 
 
+def tail_chunks(numel: int, element_size: int, chunk_bytes: int) -> List[tuple]:
+    """Element ranges [lo, hi) splitting a flat bucket into collectives of ~``chunk_bytes``; every
+    boundary is a multiple of 4096 elements (16-B aligned for any dtype). Identical on every rank:
+    it depends on the bucket's size only."""
+    step = max(4096, (chunk_bytes // max(1, element_size)) // 4096 * 4096)
+    if numel <= 2 * step:
+        return [(0, numel)]
+    return [(lo, min(numel, lo + step)) for lo in range(0, numel, step)]
+
+
 def _dense(t: torch.Tensor) -> torch.Tensor:
     if t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last)):
         return t
@@ -703,43 +713,105 @@ class DistributedDataParallel(nn.Module, Joinable):
         else:
             raise ValueError(f"unknown builtin comm hook {comm_hook_type}")
 
-    def register_overlapped_optimizer(self, optimizer):
-        """Run ``optimizer.step_params`` for each bucket as soon as its all-reduce is done, on a side
-        HIP stream, so the (HBM-bound) optimizer update overlaps the (MFMA-bound) backward of the
-        layers whose buckets are still pending; the compute stream waits for the side stream at the
-        end of backward. Do not call ``optimizer.step()`` afterwards (the reference's
-        ``_register_fused_optim`` contract). Needs an optimizer with ``step_params(params, grads)``
-        (``FusedAdamW``, ``FusedAdam``)."""
-        if not hasattr(optimizer, "step_params"):
-            raise TypeError("register_overlapped_optimizer needs an optimizer with step_params (FusedAdamW)")
+    def register_overlapped_optimizer(self, optimizer, schedule: str = "tail",
+                                      tail_chunk_bytes: Optional[int] = None):
+        """Run the optimizer update inside backward, bucket by bucket, on a side HIP stream; the
+        compute stream waits for the side stream at the end of backward. Do not call
+        ``optimizer.step()`` afterwards (the reference's ``_register_fused_optim`` contract,
+        ``pt:nn/parallel/distributed.py:2061-2131``). Needs an optimizer with ``step_params`` /
+        ``advance`` / ``step_slices`` (``FusedAdamW``, ``FusedAdam``).
+
+        ``schedule="tail"`` (default) puts the updates where the GPU is otherwise idle — under the
+        LAST bucket's all-reduce, which nothing in backward can hide:
+
+        * every other bucket's all-reduce is launched as usual when the bucket is ready, but its
+          update is deferred;
+        * the last bucket is all-reduced in chunks of ``tail_chunk_bytes`` (default
+          ``XDDP_TAIL_CHUNK_MB`` = 64 MiB; Llama-3-8B's 1.05 GB token-embedding gradient, which is
+          ready last and forms the tail alone, becomes 16 collectives);
+        * right after those launches the side stream runs the deferred updates (each after its own
+          bucket's collective), then the tail's chunk i update after chunk i's collective — so the
+          tail all-reduce runs concurrently with optimizer work the step has to do anyway, and at
+          most one chunk's update is left after the last chunk's collective.
+
+        ``schedule="backward"`` updates each bucket as soon as its own all-reduce is done, so the
+        (HBM-bound) updates overlap the remaining backward kernels instead; on one MI355X that
+        measured no gain (hipBLASLt's backward GEMMs already occupy every CU) and it leaves the
+        tail all-reduce exposed.
+        """
+        for attr in ("step_params", "advance", "step_slices"):
+            if not hasattr(optimizer, attr):
+                raise TypeError(f"register_overlapped_optimizer needs an optimizer with {attr} (FusedAdamW)")
+        if schedule not in ("tail", "backward"):
+            raise ValueError(f"unknown overlapped-optimizer schedule {schedule!r} (use 'tail' or 'backward')")
+        if tail_chunk_bytes is None:
+            tail_chunk_bytes = int(float(os.environ.get("XDDP_TAIL_CHUNK_MB", "64")) * (1 << 20))
         side = torch.cuda.Stream(self._param_device) if self.device_type == "cuda" else None
-        state = {"opt": optimizer, "side": side, "queued": False, "ddp": weakref.ref(self)}
+        state = {"opt": optimizer, "side": side, "queued": False, "ddp": weakref.ref(self), "deferred": [],
+                 "schedule": schedule, "chunk_bytes": max(1 << 16, int(tail_chunk_bytes)), "last_chunks": 0}
+        self._overlap_state = state
+
+        def run_side(fn):
+            if side is None:
+                fn()
+                return
+            # the side stream starts after everything the compute stream has enqueued (this
+            # bucket's gradients), then each update waits for its own collective
+            side.wait_stream(torch.cuda.current_stream(side.device))
+            with torch.cuda.stream(side):
+                fn()
+
+        def flush_deferred():
+            pending, state["deferred"] = state["deferred"], []
+            for work, ps, gs in pending:
+                work.wait()
+                optimizer.step_params(ps, gs)
 
         def join():
             state["queued"] = False
+            if state["deferred"]:  # the last bucket never reached the hook (e.g. skipped as unused)
+                run_side(flush_deferred)
             if side is not None:
                 torch.cuda.current_stream(side.device).wait_stream(side)
 
-        def hook(st, bucket):
-            ddp = st["ddp"]()
-            buf = bucket.buffer()
-            work = ddp.process_group.allreduce(buf, xdist.ReduceOp.AVG)
-            if st["side"] is None:
-                work.wait()
-                st["opt"].step_params(bucket.parameters(), bucket.gradients())
-            else:
-                # the side stream starts after everything the compute stream has enqueued (this
-                # bucket's gradients), then after the collective
-                st["side"].wait_stream(torch.cuda.current_stream(st["side"].device))
-                with torch.cuda.stream(st["side"]):
-                    work.wait()
-                    st["opt"].step_params(bucket.parameters(), bucket.gradients())
-                if not st["queued"]:
-                    st["queued"] = True
-                    torch.autograd.Variable._execution_engine.queue_callback(join)
+        def done(buf):
             fut = torch.futures.Future()
             fut.set_result(buf)
             return fut
+
+        def hook(st, bucket):
+            ddp = st["ddp"]()
+            pg = ddp.process_group
+            buf = bucket.buffer()
+            if not st["queued"]:
+                st["queued"] = True
+                torch.autograd.Variable._execution_engine.queue_callback(join)
+            if st["schedule"] == "backward":
+                work = pg.allreduce(buf, xdist.ReduceOp.AVG)
+                st["deferred"].append((work, bucket.parameters(), bucket.gradients()))
+                run_side(flush_deferred)
+                return done(buf)
+            if not bucket.is_last():
+                st["deferred"].append((pg.allreduce(buf, xdist.ReduceOp.AVG), bucket.parameters(),
+                                       bucket.gradients()))
+                return done(buf)
+            chunks = tail_chunks(buf.numel(), buf.element_size(), st["chunk_bytes"])
+            works = [pg.allreduce(buf[lo:hi], xdist.ReduceOp.AVG) for lo, hi in chunks]
+            st["last_chunks"] = len(chunks)
+            params, grads = bucket.parameters(), bucket.gradients()
+            spans = list(zip(bucket.offsets(), bucket.lengths()))
+            optimizer.advance(params)
+
+            def updates():
+                flush_deferred()
+                for (lo, hi), work in zip(chunks, works):
+                    work.wait()
+                    pieces = [(p, g, max(lo, o) - o, min(hi, o + n) - o)
+                              for p, g, (o, n) in zip(params, grads, spans) if max(lo, o) < min(hi, o + n)]
+                    optimizer.step_slices(pieces)
+
+            run_side(updates)
+            return done(buf)
 
         self.register_comm_hook(state, hook)
 

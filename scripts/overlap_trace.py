@@ -2,10 +2,11 @@
 """Does the overlapped optimizer hide the tail all-reduce? Reads a rocprofv3 kernel trace of
 ``bench.py --overlap-optim 1`` (forced RCCL launches at W=1: XDDP_RCCL_FORCE_LAUNCH=1, so every
 bucket's all-reduce is a real RCCL kernel on the comm stream) and reports, per iteration, the
-LAST-launched all-reduce (the tail bucket) and the AdamW update kernels that ran while it was in
-flight, plus how much of the AdamW time overlapped any all-reduce at all.
+tail window — the LAST ``--tail-chunks`` all-reduce kernels (the tail bucket, all-reduced in that
+many chunks by the "tail" schedule; 1 for the "backward" schedule) — and the AdamW update kernels
+that ran while it was in flight, plus how much of the AdamW time overlapped any all-reduce at all.
 
-usage: python scripts/overlap_trace.py TRACE_DIR [--out FILE]
+usage: python scripts/overlap_trace.py TRACE_DIR [--tail-chunks K] [--out FILE]
 """
 import argparse
 import csv
@@ -17,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--tail-chunks", type=int, default=1)
     a = ap.parse_args()
     f = sorted(glob.glob(os.path.join(a.trace, "**", "*kernel_trace.csv"), recursive=True))[0]
     rows = list(csv.DictReader(open(f)))
@@ -42,11 +44,13 @@ def main():
     def overlap(x, ys):
         return sum(max(0, min(x[1], e) - max(x[0], s)) for s, e in ys)
 
+    lines.append(f"tail window = the last {a.tail_chunks} all-reduce kernel(s) of each iteration")
     lines.append(f"{'iter':>4s} {'allreduces':>10s} {'tail ms':>8s} {'AdamW kernels during tail':>26s} "
                  f"{'AdamW ms under tail':>20s} {'AdamW before tail start':>24s} {'AdamW after tail end':>21s} "
                  f"{'last AdamW end - tail end ms':>29s}")
     for i, it in enumerate(iters):
-        tail = it[-1]
+        k = min(len(it), a.tail_chunks)
+        tail = (it[-k][0], it[-1][1])
         during = [x for x in adam if x[0] < tail[1] and x[1] > tail[0]]
         before = [x for x in adam if x[1] <= tail[0] and x[0] >= it[0][0]]
         nxt = iters[i + 1][0][0] if i + 1 < len(iters) else float("inf")

@@ -73,8 +73,12 @@ def test_llama3_8b_layout_pinned():
     rep = bp.tail_report(by, plan, 8, overlapped_optimizer=False)
     assert rep["tail_is_one_tensor_over_cap"] and rep["mitigation"] == "none"
     assert rep["exposed_tail_us_model"] > 4000
-    rep = bp.tail_report(by, plan, 8, overlapped_optimizer=True)
-    assert rep["mitigation"].startswith("overlapped optimizer")
+    rep = bp.tail_report(by, plan, 8, overlapped_optimizer="tail", tail_chunks=16)
+    assert rep["mitigation"].startswith("deferred optimizer") and "16 chunk" in rep["mitigation"]
+    assert rep["optimizer_schedule"] == "tail"
+    # updates during backward hide nothing under the tail: the report says so
+    rep = bp.tail_report(by, plan, 8, overlapped_optimizer="backward")
+    assert rep["mitigation"].startswith("none for the tail")
 
 
 def test_tail_report_small_tail_uses_cap():

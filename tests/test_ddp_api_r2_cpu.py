@@ -412,46 +412,72 @@ def test_python_reducer_matches_torch_ddp():
 
 
 # --------------------------------------------------------------------------------------------
-def _w_overlapped_optimizer(rank, world):
+def _w_overlapped_optimizer(rank, world, schedule):
     import distributeddataparallel_amd as xddp
     from distributeddataparallel_amd.optim import FusedAdamW
 
     m1, m2 = _mlp(), _mlp()
     d1 = xddp.DDP(m1, bucket_cap_mb=0.001, first_bucket_cap_mb=0.001)  # several buckets
     d2 = xddp.DDP(m2)
-    d1.register_overlapped_optimizer(o1 := FusedAdamW(m1.parameters(), lr=1e-2, weight_decay=0.1))
+    # tail chunks of 16,384 fp32 elements: the last bucket (fc1's weight + bias, 50,240 elements)
+    # is all-reduced as 4 collectives and updated slice by slice
+    d1.register_overlapped_optimizer(o1 := FusedAdamW(m1.parameters(), lr=1e-2, weight_decay=0.1),
+                                     schedule=schedule, tail_chunk_bytes=16384 * 4)
     o2 = FusedAdamW(m2.parameters(), lr=1e-2, weight_decay=0.1)
-    # event log: every bucket's update is issued right after its own all-reduce, so the updates of
-    # all earlier buckets are already issued (on GPU: running on the side stream) while the LAST
-    # bucket's all-reduce — the exposed tail — is in flight
     log = []
     pg = d1.process_group
-    orig_ar, orig_step = pg.allreduce, o1.step_params
+    orig_ar, orig_slices = pg.allreduce, o1.step_slices
     pg.allreduce = lambda t, *a, **k: (log.append(("ar", t.numel())), orig_ar(t, *a, **k))[1]
-    o1.step_params = lambda ps, gs: (log.append(("step", sum(p.numel() for p in ps))), orig_step(ps, gs))[1]
+    o1.step_slices = lambda pieces: (log.append(("step", sum(hi - lo for _, _, lo, hi in pieces))),
+                                     orig_slices(pieces))[1]
     for x, y in _batches(1, 4, per_rank=4, seed=90 + rank):
         o1.zero_grad()
         log.clear()
-        F.cross_entropy(d1(x), y).backward()  # stepped per bucket inside backward
+        F.cross_entropy(d1(x), y).backward()  # updated inside backward
         o2.zero_grad()
         F.cross_entropy(d2(x), y).backward()
         o2.step()
-    pg.allreduce, o1.step_params = orig_ar, orig_step
-    _assert_params_equal(m1, m2)
+    pg.allreduce, o1.step_slices = orig_ar, orig_slices
+    _assert_params_equal(m1, m2, rtol=0, atol=0)  # bitwise: same all-reduce sums, elementwise AdamW
     nb = len(d1.reducer.bucket_sizes_bytes())
     assert nb >= 2
     ars = [i for i, e in enumerate(log) if e[0] == "ar"]
     steps = [i for i, e in enumerate(log) if e[0] == "step"]
-    assert len(ars) == nb and len(steps) == nb, log
-    for b in range(nb):  # bucket b steps after its all-reduce, before the next bucket's
-        assert ars[b] < steps[b] and (b + 1 == nb or steps[b] < ars[b + 1]), log
-    assert all(s < ars[-1] for s in steps[:-1])  # every other update precedes the tail all-reduce
+    if schedule == "backward":
+        # every bucket's update is issued right after its own all-reduce, one all-reduce per bucket
+        assert len(ars) == nb and len(steps) == nb, log
+        for b in range(nb):
+            assert ars[b] < steps[b] and (b + 1 == nb or steps[b] < ars[b + 1]), log
+    else:
+        # every collective (nb - 1 buckets + 4 tail chunks) is issued before the first update: the
+        # deferred updates run on the side stream while the chunked tail all-reduce is in flight,
+        # then the tail's slices, which add up to the whole tail bucket
+        assert len(ars) == nb - 1 + 4, log
+        assert max(ars) < min(steps), log
+        tail_numel = m1.fc1.weight.numel() + m1.fc1.bias.numel()  # the last bucket: fc1's grads
+        assert [e[1] for e in log[-4:]] == [16384, 16384, 16384, tail_numel - 3 * 16384], log
+        assert d1._overlap_state["last_chunks"] == 4
 
 
 def test_overlapped_optimizer_matches_step_after_backward():
-    """DDP.register_overlapped_optimizer: the per-bucket FusedAdamW.step_params inside backward
-    trains exactly like the usual backward-then-step."""
-    run_ranks(_w_overlapped_optimizer, world=2)
+    """DDP.register_overlapped_optimizer, schedule="backward": the per-bucket FusedAdamW.step_params
+    inside backward trains exactly like the usual backward-then-step."""
+    run_ranks(_w_overlapped_optimizer, world=2, args=("backward",))
+
+
+def test_overlapped_optimizer_tail_schedule_chunked_bitwise():
+    """schedule="tail" (the default): updates deferred under a chunked tail all-reduce, stepped in
+    slices — bitwise equal to the unchunked backward-then-step path."""
+    run_ranks(_w_overlapped_optimizer, world=2, args=("tail",))
+
+
+def test_tail_chunks_ranges():
+    from distributeddataparallel_amd.parallel.distributed import tail_chunks
+
+    assert tail_chunks(1000, 4, 1 << 20) == [(0, 1000)]
+    r = tail_chunks(525_336_576, 2, 64 << 20)  # Llama-3-8B token embedding, bf16
+    assert len(r) == 16 and r[0] == (0, 33_554_432) and r[-1][1] == 525_336_576
+    assert all(lo % 4096 == 0 for lo, _ in r) and all(a[1] == b[0] for a, b in zip(r, r[1:]))
 
 
 def _w_join_buffer_hook(rank, world, location):
