@@ -87,6 +87,9 @@ def parse(argv=None):
     ap.add_argument("--overlap-schedule", choices=["tail", "backward"], default="tail",
                     help="tail: updates deferred under the chunked tail all-reduce; backward: each bucket's "
                          "update right after its own all-reduce")
+    ap.add_argument("--force-rccl-launch", type=int, default=0,
+                    help="issue real RCCL kernels even at N=1 (XDDP_RCCL_FORCE_LAUNCH): the comm-stream "
+                         "schedule becomes visible in a one-GPU kernel trace")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     if a.batch_size is None:
@@ -327,6 +330,8 @@ def main(argv=None):
     os.environ.setdefault("LOCAL_RANK", str(local_rank))
     if "MASTER_PORT" not in os.environ:
         os.environ["MASTER_PORT"] = str(_free_port())
+    if args.force_rccl_launch:
+        os.environ["XDDP_RCCL_FORCE_LAUNCH"] = "1"
     if args.device == "cuda":
         _install_miopen_tuning()
     tunableop = _install_tunableop(args)
