@@ -73,8 +73,13 @@ def parse(argv=None):
     ap.add_argument("--diag-steps", type=int, default=3,
                     help="untimed steps after the timed region with comm timers on every step")
     ap.add_argument("--busbw-iters", type=int, default=5, help="all-reduce bandwidth probe iterations (N>1)")
-    ap.add_argument("--probe-peer", type=int, default=0,
-                    help="N>1: also probe the two-shot peer-memory all-reduce at the bucket sizes")
+    ap.add_argument("--probe-peer", type=int, default=None,
+                    help="N>1: also probe the two-shot peer-memory all-reduce at the bucket sizes with a separate "
+                         "peer instance (default: on at N>1 unless the comm calibration already timed that route)")
+    ap.add_argument("--comm-calibrate", choices=["auto", "0", "1"], default="auto",
+                    help="init-time comm calibration (XDDP_COMM_CALIBRATE; distributed/calibrate.py): peer-path "
+                         "self-check, RCCL vs peer timings at the bucket sizes, fitted alpha / bus bandwidth for the "
+                         "bucket policy, per-size route table. auto = on at N>1 on the rccl / peer backends")
     ap.add_argument("--baseline-json", default=None, help="N=1 result line -> scaling_efficiency")
     ap.add_argument("--launch-timeout", type=float, default=1500.0, help="self-launch: kill children after this")
     ap.add_argument("--tunableop", choices=["auto", "off", "use", "tune"], default="auto",
@@ -357,6 +362,16 @@ def main(argv=None):
             torch.cuda.synchronize()
 
     rccl_env = {}
+    calib = args.comm_calibrate == "1" or (args.comm_calibrate == "auto" and world > 1 and gpu
+                                           and args.backend in ("rccl", "peer") and args.impl == "xddp")
+    if calib:
+        # outside the timed region: runs once in the DDP constructor. The peer lanes are created on
+        # probation and only used if every rank's self-check passes and they measure faster.
+        os.environ.setdefault("XDDP_COMM_CALIBRATE", "1")
+        if args.backend == "rccl":
+            os.environ.setdefault("XDDP_PEER_ALLREDUCE", "auto")
+    if args.probe_peer is None:
+        args.probe_peer = int(world > 1 and not calib)
     if args.impl == "xddp":
         import distributeddataparallel_amd as xddp
         from distributeddataparallel_amd import distributed as dist
@@ -599,6 +614,7 @@ def diagnostics(args, ddp, step, sync, dist, device, world, overlap=False):
         pg.allgather_into_tensor(allv, dev).wait()
         info["rank_devices"] = [int(v) for v in allv.tolist()]
     out["comm_info"] = info
+    out["comm_calibration"] = getattr(ddp, "comm_calibration", None)
     if args.graphs or args.diag_steps <= 0:
         return out
     red.reset_runtime_stats()

@@ -180,6 +180,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("shutdown", &Comm::shutdown, py::call_guard<py::gil_scoped_release>())
       .def("set_timing", &Comm::set_timing)
       .def("timing", &Comm::timing)
+      .def("allreduce_via", &Comm::allreduce_via, py::arg("tensor"), py::arg("op"), py::arg("route"),
+           py::call_guard<py::gil_scoped_release>(),
+           "All-reduce on a named route: 0 auto, 1 base (RCCL ring / peer one-shot chunks), 2 one-shot, 3 two-shot")
+      .def("routes", &Comm::routes)
+      .def("one_shot_capacity", &Comm::one_shot_capacity)
+      .def("set_route_table", &Comm::set_route_table, py::arg("bounds"), py::arg("routes"))
+      .def("route_table", &Comm::route_table)
+      .def("peer_status", &Comm::peer_status)
+      .def("set_peer_timeout_ms", &Comm::set_peer_timeout_ms)
+      .def("finish_peer_probation", &Comm::finish_peer_probation, py::arg("keep"),
+           py::call_guard<py::gil_scoped_release>())
       .def("info", &Comm::info)
       .def("flight_records", [](Comm& c) {
         py::list out;

@@ -145,6 +145,29 @@ class Comm : public std::enable_shared_from_this<Comm> {
     out.swap(timed_log_);
     return out;
   }
+  // ---- route control for comm calibration (distributed/calibrate.py) ----------
+  // Routes of an all-reduce: 0 = the communicator's own choice (route table), 1 = its base path
+  // (the RCCL ring; one-shot chunks on the peer backend), 2 = the one-shot peer kernel, 3 = the
+  // two-shot peer kernel.
+  enum Route { kRouteAuto = 0, kRouteBase = 1, kRouteOneShot = 2, kRouteTwoShot = 3 };
+  virtual std::shared_ptr<Work> allreduce_via(at::Tensor t, RedOp op, int /*route*/) { return allreduce(t, op, 1.0); }
+  // Routes besides auto/base this communicator can run now (RCCL: {2, 3} once the peer lanes exist).
+  virtual std::vector<int> routes() const { return {}; }
+  // Largest message the one-shot lane takes in one launch (0: none).
+  virtual int64_t one_shot_capacity() const { return 0; }
+  // Route table: an all-reduce of nb bytes takes routes[i] for the first bounds[i] >= nb, the
+  // base path beyond the last bound; a route the tensor/op cannot take falls back to the base path.
+  // Must be identical on every rank (it is computed from MAX-reduced timings).
+  virtual void set_route_table(const std::vector<int64_t>& /*bounds*/, const std::vector<int>& /*routes*/) {}
+  virtual std::vector<std::vector<int64_t>> route_table() const { return {}; }
+  // Peer lanes' host-mapped status word: 0 ok, 1 a peer kernel timed out.
+  virtual int peer_status() const { return 0; }
+  // Device-side wait bound of the peer kernels from now on (calibration uses a short one).
+  virtual void set_peer_timeout_ms(double /*ms*/) {}
+  // End of the peer lanes' probation: keep=false closes them (everything takes the base path);
+  // keep=true arms them (their failures become communicator errors from now on).
+  virtual void finish_peer_probation(bool /*keep*/) {}
+
   // Backend facts for logs/benchmarks (RCCL: version, channel count seen at init, ...).
   virtual std::map<std::string, std::string> info() const { return {{"backend", backend()}}; }
 

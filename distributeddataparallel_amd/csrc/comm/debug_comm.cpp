@@ -59,6 +59,17 @@ class DebugComm : public Comm {
     inner_->set_timing(on);
   }
   std::map<std::string, std::string> info() const override { return inner_->info(); }
+  std::shared_ptr<Work> allreduce_via(at::Tensor t, RedOp op, int route) override {
+    pre("allreduce", t, static_cast<int64_t>(op), true);
+    return inner_->allreduce_via(t, op, route);
+  }
+  std::vector<int> routes() const override { return inner_->routes(); }
+  int64_t one_shot_capacity() const override { return inner_->one_shot_capacity(); }
+  void set_route_table(const std::vector<int64_t>& b, const std::vector<int>& r) override { inner_->set_route_table(b, r); }
+  std::vector<std::vector<int64_t>> route_table() const override { return inner_->route_table(); }
+  int peer_status() const override { return inner_->peer_status(); }
+  void set_peer_timeout_ms(double ms) override { inner_->set_peer_timeout_ms(ms); }
+  void finish_peer_probation(bool keep) override { inner_->finish_peer_probation(keep); }
   std::vector<std::shared_ptr<Work>> drain_timed_works() override { return inner_->drain_timed_works(); }
   std::shared_ptr<Comm> inner() const { return inner_; }
   FlightRecorder& flight() override { return inner_->flight(); }

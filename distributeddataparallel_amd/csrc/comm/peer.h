@@ -61,6 +61,8 @@ class PeerAllReduce {
   int64_t capacity() const { return cap_; }
   int64_t two_shot_capacity() const { return cap2_; }
   double timeout_ms() const { return timeout_ms_; }
+  // Wait bound of the launches issued from now on (kernel argument: no effect on queued ones).
+  void set_timeout_ms(double ms);
 
  private:
   void launch(at::Tensor t, at::Tensor out, RedOp op, int root, int mode, hipStream_t s);

@@ -322,6 +322,7 @@ struct PeerAllReduce::Impl {
   int* status_host = nullptr;  // host-mapped, coherent
   int* status_dev = nullptr;
   uint64_t timeout_ticks = 0;
+  int khz = 100000;
 };
 
 PeerAllReduce::PeerAllReduce(std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity,
@@ -351,7 +352,8 @@ PeerAllReduce::PeerAllReduce(std::shared_ptr<Store> store, int rank, int size, i
   XDDP_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
   const char* t = std::getenv("XDDP_PEER_TIMEOUT_MS");
   timeout_ms_ = t ? std::atof(t) : static_cast<double>(timeout.count());
-  impl_->timeout_ticks = (uint64_t)(timeout_ms_ * (khz > 0 ? khz : 100000));
+  impl_->khz = khz > 0 ? khz : 100000;
+  impl_->timeout_ticks = (uint64_t)(timeout_ms_ * impl_->khz);
   // every rank mapped every buffer before the first call raises a flag in it
   store->set("peer/ok/" + std::to_string(rank), "1");
   for (int r = 0; r < size; ++r) store->get("peer/ok/" + std::to_string(r));
@@ -512,6 +514,11 @@ void PeerAllReduce::allreduce_two_shot(at::Tensor t, RedOp op, hipStream_t s) {
     }
     XDDP_HIP_CHECK(hipGetLastError());
   }
+}
+
+void PeerAllReduce::set_timeout_ms(double ms) {
+  timeout_ms_ = ms;
+  impl_->timeout_ticks = (uint64_t)(ms * impl_->khz);
 }
 
 int PeerAllReduce::status() const {

@@ -132,7 +132,7 @@ class PeerComm : public Comm {
     TORCH_CHECK(op == RedOp::SUM || op == RedOp::AVG || op == RedOp::MAX || op == RedOp::PREMUL_SUM,
                 "peer backend: all-reduce supports SUM, AVG, MAX and PREMUL_SUM");
     const RedOp kop = op == RedOp::PREMUL_SUM ? RedOp::SUM : op;
-    const bool two = (int64_t)t.nbytes() >= two_shot_min_ && peer_->supports_two_shot(t, kop);
+    const bool two = use_two_shot(t, kop);
     return launch(two ? "allreduce_two_shot" : "allreduce", t, {t}, [&](hipStream_t s) {
       if (two) {
         peer_->allreduce_two_shot(t, kop, s);
@@ -141,6 +141,41 @@ class PeerComm : public Comm {
       }
       if (op == RedOp::PREMUL_SUM) t.mul_(premul);  // (on the comm stream: the guard below)
     });
+  }
+
+  // Routes: base / one-shot = one-shot chunks, two-shot = the two-shot lane. The route table
+  // (calibration) replaces the XDDP_PEER_TWO_SHOT_MIN_BYTES threshold; dropping the two-shot lane
+  // after a failed self-check (finish_peer_probation(false)) leaves the one-shot chunks.
+  std::shared_ptr<Work> allreduce_via(at::Tensor t, RedOp op, int route) override {
+    if (route == kRouteAuto) return allreduce(t, op, 1.0);
+    TORCH_CHECK(op == RedOp::SUM || op == RedOp::AVG || op == RedOp::MAX, "peer backend: allreduce_via op");
+    const bool two = route == kRouteTwoShot;
+    TORCH_CHECK(!two || (two_shot_ok_ && peer_->supports_two_shot(t, op)), "peer backend: two-shot route unavailable");
+    return launch(two ? "allreduce_two_shot" : "allreduce", t, {t}, [&](hipStream_t s) {
+      if (two) peer_->allreduce_two_shot(t, op, s);
+      else for_chunks(t, [&](at::Tensor c) { peer_->allreduce(c, op, s); });
+    });
+  }
+  std::vector<int> routes() const override {
+    if (two_shot_ok_ && peer_->two_shot_capacity() > 0) return {kRouteOneShot, kRouteTwoShot};
+    return {kRouteOneShot};
+  }
+  int64_t one_shot_capacity() const override { return peer_->capacity(); }
+  void set_route_table(const std::vector<int64_t>& bounds, const std::vector<int>& routes) override {
+    TORCH_CHECK(bounds.size() == routes.size(), "route table: bounds and routes differ in length");
+    route_bounds_ = bounds;
+    route_ids_ = routes;
+  }
+  std::vector<std::vector<int64_t>> route_table() const override {
+    return {route_bounds_, std::vector<int64_t>(route_ids_.begin(), route_ids_.end())};
+  }
+  int peer_status() const override { return peer_->status(); }
+  void set_peer_timeout_ms(double ms) override { peer_->set_timeout_ms(ms); }
+  void finish_peer_probation(bool keep) override {
+    if (keep) return;
+    two_shot_ok_ = false;
+    route_bounds_.clear();
+    route_ids_.clear();
   }
 
   std::shared_ptr<Work> broadcast(at::Tensor t, int root) override {
@@ -205,6 +240,15 @@ class PeerComm : public Comm {
   }
 
  private:
+  bool use_two_shot(const at::Tensor& t, RedOp op) const {
+    if (!two_shot_ok_ || !peer_->supports_two_shot(t, op)) return false;
+    const int64_t nb = static_cast<int64_t>(t.nbytes());
+    if (route_bounds_.empty()) return nb >= two_shot_min_;
+    for (size_t i = 0; i < route_bounds_.size(); ++i)
+      if (nb <= route_bounds_[i]) return route_ids_[i] == kRouteTwoShot;
+    return false;
+  }
+
   int64_t chunk_elems(const at::Tensor& t) const {
     const int64_t esz = t.element_size();
     return std::max<int64_t>(16 / esz, (peer_->capacity() / esz) / (16 / esz) * (16 / esz));
@@ -336,6 +380,9 @@ class PeerComm : public Comm {
   std::shared_ptr<PeerAllReduce> peer_;
   std::shared_ptr<PeerState> st_;
   int64_t two_shot_min_ = 0;
+  bool two_shot_ok_ = true;
+  std::vector<int64_t> route_bounds_;
+  std::vector<int> route_ids_;
   at::Tensor barrier_buf_;
   std::thread watchdog_;
   std::atomic<bool> wd_stop_{false};

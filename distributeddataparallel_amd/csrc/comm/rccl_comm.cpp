@@ -259,6 +259,71 @@ class RcclComm : public Comm {
     });
   }
 
+  std::shared_ptr<Work> allreduce_via(at::Tensor t, RedOp op, int route) override {
+    check_tensor(t);
+    if (route == kRouteAuto) return allreduce(t, op, 1.0);
+    if (size_ == 1 && !force_launch_) return local_noop("allreduce", t);
+    auto pr = std::atomic_load(&peer_);
+    if (route == kRouteOneShot) {
+      TORCH_CHECK(pr && pr->supports(t, op, false), "xddp rccl: one-shot route unavailable for this tensor");
+      return launch_peer("allreduce_peer", t, {t}, [&](hipStream_t s) { pr->allreduce(t, op, s); });
+    }
+    if (route == kRouteTwoShot) {
+      TORCH_CHECK(pr && pr->supports_two_shot(t, op), "xddp rccl: two-shot route unavailable for this tensor");
+      return launch_peer("allreduce_two_shot", t, {t}, [&](hipStream_t s) { pr->allreduce_two_shot(t, op, s); });
+    }
+    TORCH_CHECK(op != RedOp::PREMUL_SUM, "allreduce_via: PREMUL_SUM takes the auto route");
+    return launch("allreduce", t, {t}, [&](hipStream_t s) {
+      XDDP_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()),
+                                    to_nccl(op, t.scalar_type()), comm_, s));
+    });
+  }
+
+  std::vector<int> routes() const override {
+    auto pr = std::atomic_load(&peer_);
+    if (!pr) return {};
+    std::vector<int> r{kRouteOneShot};
+    if (pr->two_shot_capacity() > 0) r.push_back(kRouteTwoShot);
+    return r;
+  }
+  int64_t one_shot_capacity() const override {
+    auto pr = std::atomic_load(&peer_);
+    return pr ? pr->capacity() : 0;
+  }
+  void set_route_table(const std::vector<int64_t>& bounds, const std::vector<int>& routes) override {
+    TORCH_CHECK(bounds.size() == routes.size(), "route table: bounds and routes differ in length");
+    route_bounds_ = bounds;
+    route_ids_ = routes;
+  }
+  std::vector<std::vector<int64_t>> route_table() const override {
+    return {route_bounds_, std::vector<int64_t>(route_ids_.begin(), route_ids_.end())};
+  }
+  int peer_status() const override {
+    auto pr = std::atomic_load(&peer_);
+    return pr ? pr->status() : 0;
+  }
+  void set_peer_timeout_ms(double ms) override {
+    if (auto pr = std::atomic_load(&peer_)) pr->set_timeout_ms(ms);
+  }
+  void finish_peer_probation(bool keep) override {
+    auto pr = std::atomic_load(&peer_);
+    if (!pr) return;
+    if (keep && pr->status() == 0) {
+      probation_ = false;
+      return;
+    }
+    // every launched peer kernel drains (its grid always exits, also after a timeout); then the
+    // lanes go away and every collective takes the RCCL ring
+    c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
+    XDDP_HIP_CHECK(hipStreamSynchronize(stream_.stream()));
+    route_bounds_.clear();
+    route_ids_.clear();
+    peer_mode_ = 0;
+    std::atomic_store(&peer_, std::shared_ptr<PeerAllReduce>());
+    pr->close();
+    probation_ = false;
+  }
+
   std::shared_ptr<Work> broadcast(at::Tensor t, int root) override {
     check_tensor(t);
     if (size_ == 1 && !force_launch_) return local_noop("broadcast", t);
@@ -367,9 +432,14 @@ class RcclComm : public Comm {
   // The route depends only on facts identical on every rank (size, dtype, op) — never on group
   // state — so all ranks issue the same sequence. Every rank must agree the path works: each
   // posts whether its IPC mapping succeeded and the path is used only if all did.
+  //   XDDP_PEER_ALLREDUCE=auto: both lanes are created but on probation — nothing is routed to them
+  //     and their timeouts are not communicator errors — until comm calibration
+  //     (distributed/calibrate.py) has self-checked them on every rank and installed a route table
+  //     from measured timings (finish_peer_probation: keep them or close them).
   void init_peer(const std::shared_ptr<Store>& store) {
     const char* e = std::getenv("XDDP_PEER_ALLREDUCE");
-    const int mode = e ? std::atoi(e) : 0;
+    const bool autom = e && std::string(e) == "auto";
+    const int mode = autom ? 2 : (e ? std::atoi(e) : 0);
     if (mode <= 0 || size_ < 2 || size_ > kPeerMaxRanks) return;
     auto env_i64 = [](const char* k, int64_t d) {
       const char* v = std::getenv(k);
@@ -395,13 +465,24 @@ class RcclComm : public Comm {
     bool all = true;
     for (int r = 0; r < size_; ++r) all = all && store->get("peer/use/" + std::to_string(r)) == "1";
     if (!all) peer_.reset();
-    peer_mode_ = peer_ ? mode : 0;
+    peer_mode_ = peer_ && !autom ? mode : 0;
+    probation_ = peer_ && autom;
   }
 
   enum class PeerRoute { kRccl, kOneShot, kTwoShot };
   PeerRoute peer_route(const at::Tensor& t, RedOp op, bool bcast) const {
     if (!peer_) return PeerRoute::kRccl;
     const int64_t nb = static_cast<int64_t>(t.nbytes());
+    if (!route_bounds_.empty()) {  // calibrated: the measured fastest route for this size
+      for (size_t i = 0; i < route_bounds_.size(); ++i) {
+        if (nb > route_bounds_[i]) continue;
+        if (route_ids_[i] == kRouteOneShot && peer_->supports(t, op, bcast)) return PeerRoute::kOneShot;
+        if (route_ids_[i] == kRouteTwoShot && !bcast && peer_->supports_two_shot(t, op)) return PeerRoute::kTwoShot;
+        return PeerRoute::kRccl;
+      }
+      return PeerRoute::kRccl;
+    }
+    if (probation_) return PeerRoute::kRccl;
     if (nb <= peer_bytes_ && peer_->supports(t, op, bcast)) return PeerRoute::kOneShot;
     if (!bcast && peer_mode_ >= 2 && nb >= two_shot_min_ && nb <= two_shot_max_ && peer_->supports_two_shot(t, op))
       return PeerRoute::kTwoShot;
@@ -419,7 +500,9 @@ class RcclComm : public Comm {
             {"high_priority_stream", high_priority_ ? "1" : "0"},
             {"peer_mode", std::to_string(peer_mode_)},
             {"peer_one_shot_max_bytes", std::to_string(peer_ ? peer_bytes_ : 0)},
-            {"peer_two_shot_min_bytes", std::to_string(peer_mode_ >= 2 ? two_shot_min_ : 0)}};
+            {"peer_two_shot_min_bytes", std::to_string(peer_mode_ >= 2 ? two_shot_min_ : 0)},
+            {"peer_probation", probation_ ? "1" : "0"},
+            {"route_table_entries", std::to_string(route_bounds_.size())}};
   }
 
   hipStream_t stream() const { return stream_.stream(); }
@@ -451,7 +534,7 @@ class RcclComm : public Comm {
     XDDP_HIP_CHECK(hipEventRecord(pre, cur.stream()));
     XDDP_HIP_CHECK(hipStreamWaitEvent(stream_.stream(), pre, 0));
     pool_->put(pre);
-    auto w = std::make_shared<RcclWork>(pool_, device_, err_, peer_);
+    auto w = std::make_shared<RcclWork>(pool_, device_, err_, probation_ ? nullptr : std::atomic_load(&peer_));
     w->seq = flight_.record(name, meta.numel(), meta.scalar_type());
     const bool timed = timing_.load() && !capturing_;
     // Inside a group the RCCL kernels are enqueued at ncclGroupEnd: the group is timed there.
@@ -524,7 +607,7 @@ class RcclComm : public Comm {
   // One-rank collectives that are identities: no RCCL launch, a Work that is already ordered.
   std::shared_ptr<Work> local_noop(const char* name, const at::Tensor& t) {
     TORCH_CHECK(err_->load() == 0, "xddp rccl: communicator is in error state");
-    auto w = std::make_shared<RcclWork>(pool_, device_, err_, peer_);
+    auto w = std::make_shared<RcclWork>(pool_, device_, err_, probation_ ? nullptr : std::atomic_load(&peer_));
     w->seq = flight_.record(name, t.numel(), t.scalar_type());
     XDDP_HIP_CHECK(hipEventRecord(w->ev, c10::hip::getCurrentHIPStream(device_).stream()));
     flight_.finish(w->seq, "completed");
@@ -588,10 +671,11 @@ class RcclComm : public Comm {
         } catch (...) {
         }
       }
-      if ((err_->load() == 0 || err_->load() == 4) && reason.empty() && peer_ && peer_->status() != 0) {
+      auto pr = std::atomic_load(&peer_);
+      if ((err_->load() == 0 || err_->load() == 4) && reason.empty() && pr && !probation_ && pr->status() != 0) {
         // (a Work query may have flagged it first; the watchdog still dumps, posts and aborts)
         reason = "peer-memory collective: a rank did not arrive within " +
-                 std::to_string(static_cast<int64_t>(peer_->timeout_ms())) + " ms (XDDP_PEER_TIMEOUT_MS)";
+                 std::to_string(static_cast<int64_t>(pr->timeout_ms())) + " ms (XDDP_PEER_TIMEOUT_MS)";
         std::cerr << "[xddp rank " << rank_ << "] watchdog: " << reason << "; aborting communicator\n";
         int z = 0;
         err_->compare_exchange_strong(z, 4);
@@ -653,6 +737,9 @@ class RcclComm : public Comm {
   bool destroyed_ = false;
   std::shared_ptr<PeerAllReduce> peer_;
   int peer_mode_ = 0;
+  std::atomic<bool> probation_{false};
+  std::vector<int64_t> route_bounds_;
+  std::vector<int> route_ids_;
   int64_t peer_bytes_ = 0;
   int64_t two_shot_min_ = 0;
   int64_t two_shot_max_ = 0;

@@ -218,6 +218,7 @@ class ProcessGroup:
         self.group_name = name
         self.timeout = timeout
         self._coalescing = 0
+        self.comm_calibration = None  # distributed/calibrate.py report, once measured
 
     # torch.distributed.ProcessGroup-style accessors
     def rank(self) -> int:

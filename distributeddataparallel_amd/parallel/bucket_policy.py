@@ -8,13 +8,17 @@ buckets from a two-term cost model of one all-reduce of S bytes over W ranks::
 
     t(S) = alpha + 2 (W-1)/W * S / B
 
-* ``alpha``  - fixed cost per RCCL all-reduce launch (kernel launch + ring latency). ASSUMED
-  30 us at W=8 (not yet measured on an 8-GPU node; ``XDDP_RCCL_ALPHA_US`` overrides);
+* ``alpha``  - fixed cost per RCCL all-reduce launch (kernel launch + ring latency);
 * ``B``      - achieved all-reduce BUS bandwidth for large messages, i.e. what RCCL's rings
   sustain over the node, not one link: bounded below by one xGMI link (~153 GB/s, a single ring)
-  and above by all seven (~1,071 GB/s). ASSUMED 350 GB/s (RCCL spreads several rings over the
-  links); ``bench.py`` measures the per-bucket busbw at N>1 so a measurement can replace it
-  (``XDDP_RCCL_BUSBW_GBPS``). docs/ARCHITECTURE.md uses the same two constants.
+  and above by all seven (~1,071 GB/s).
+
+Where they come from, first match wins: explicit arguments; ``XDDP_RCCL_ALPHA_US`` /
+``XDDP_RCCL_BUSBW_GBPS``; the job's own init-time measurement (``distributed/calibrate.py``, run
+by the DDP constructor when ``XDDP_COMM_CALIBRATE=1`` — the bench default at N>1 — which times the
+communicator at the planned bucket sizes and installs the fit with :func:`set_calibration`); and
+only then the unmeasured defaults alpha = 30 us, B = 350 GB/s (RCCL spreading several rings over
+the links). :func:`calibration_source` says which one a plan used.
 
 Decisions, in gradient-ready order (the order buckets launch in):
 
@@ -78,12 +82,41 @@ class BucketPlan:
 
     def as_dict(self):
         return {"policy": self.policy, "first_bytes": self.first_bytes, "cap_bytes": self.cap_bytes,
-                "tail_bytes": self.tail_bytes}
+                "tail_bytes": self.tail_bytes, "alpha_busbw_source": calibration_source()}
 
 
-def _env_float(name: str, default: float) -> float:
-    v = os.environ.get(name)
-    return float(v) if v else default
+_CALIBRATION = None  # (alpha_us, busbw_GBps) measured by distributed/calibrate.py
+
+
+def set_calibration(alpha_us: float, busbw_gbps: float) -> None:
+    """Install the job's measured alpha / B (identical on every rank: fitted from MAX-reduced timings)."""
+    global _CALIBRATION
+    _CALIBRATION = (float(alpha_us), float(busbw_gbps))
+
+
+def clear_calibration() -> None:
+    global _CALIBRATION
+    _CALIBRATION = None
+
+
+def calibration_source() -> str:
+    if os.environ.get("XDDP_RCCL_ALPHA_US") or os.environ.get("XDDP_RCCL_BUSBW_GBPS"):
+        return "env"
+    return "measured" if _CALIBRATION is not None else "assumed defaults"
+
+
+def _alpha_us() -> float:
+    v = os.environ.get("XDDP_RCCL_ALPHA_US")
+    if v:
+        return float(v)
+    return _CALIBRATION[0] if _CALIBRATION is not None else DEFAULT_ALPHA_US
+
+
+def _busbw_gbps() -> float:
+    v = os.environ.get("XDDP_RCCL_BUSBW_GBPS")
+    if v:
+        return float(v)
+    return _CALIBRATION[1] if _CALIBRATION is not None else DEFAULT_BUSBW_GBPS
 
 
 def reference_plan(bucket_cap_mb: float = 25, first_bucket_cap_mb: float = 1) -> BucketPlan:
@@ -93,8 +126,8 @@ def reference_plan(bucket_cap_mb: float = 25, first_bucket_cap_mb: float = 1) ->
 def xgmi_plan(total_bytes: int, world_size: int, alpha_us: float | None = None,
               busbw_gbps: float | None = None) -> BucketPlan:
     """Bucket caps for one DDP job from (total gradient bytes, world size)."""
-    alpha = (alpha_us if alpha_us is not None else _env_float("XDDP_RCCL_ALPHA_US", DEFAULT_ALPHA_US)) * 1e-6
-    bw = (busbw_gbps if busbw_gbps is not None else _env_float("XDDP_RCCL_BUSBW_GBPS", DEFAULT_BUSBW_GBPS)) * 1e9
+    alpha = (alpha_us if alpha_us is not None else _alpha_us()) * 1e-6
+    bw = (busbw_gbps if busbw_gbps is not None else _busbw_gbps()) * 1e9
     w = max(2, int(world_size))  # W=1 communicates nothing; size as for a pair
     f = 2.0 * (w - 1) / w
     s_alpha = alpha * bw / f      # bytes whose transfer time equals alpha
@@ -143,8 +176,8 @@ def bucket_bytes(sizes_bytes: Sequence[int], layout: List[List[int]]) -> List[in
 def exposed_tail_us(sizes: List[int], world_size: int, alpha_us: float | None = None,
                     busbw_gbps: float | None = None) -> float:
     """Modelled time of the last bucket's all-reduce (the part of comm backward cannot hide)."""
-    alpha = alpha_us if alpha_us is not None else _env_float("XDDP_RCCL_ALPHA_US", DEFAULT_ALPHA_US)
-    bw = busbw_gbps if busbw_gbps is not None else _env_float("XDDP_RCCL_BUSBW_GBPS", DEFAULT_BUSBW_GBPS)
+    alpha = alpha_us if alpha_us is not None else _alpha_us()
+    bw = busbw_gbps if busbw_gbps is not None else _busbw_gbps()
     w = max(2, world_size)
     return alpha + 2.0 * (w - 1) / w * sizes[-1] / (bw * 1e3)
 

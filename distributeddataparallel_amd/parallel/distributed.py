@@ -290,6 +290,17 @@ class DistributedDataParallel(nn.Module, Joinable):
         total_bytes = sum(p.numel() * p.element_size() for p in self._module_parameters)
         if comm_dtype is not None:
             total_bytes = sum(p.numel() for p in self._module_parameters) * torch.empty(0, dtype=comm_dtype).element_size()
+        from ..distributed import calibrate as _cal
+
+        if self.device_type == "cuda" and _cal.enabled(self.process_group):
+            # XDDP_COMM_CALIBRATE=1: measure alpha / B and the per-size route (RCCL ring vs the peer
+            # kernels) at the sizes this job's buckets will have, before the plan is fixed
+            plan0, _ = _bp.resolve_plan(bucket_policy, bucket_cap_mb, first_bucket_cap_mb, total_bytes,
+                                        self.process_group.size(), self.process_group.backend)
+            sizes = _cal.probe_sizes(plan0.first_bytes, plan0.cap_bytes, plan0.tail_bytes, total_bytes)
+            cdt = comm_dtype or (self._module_parameters or self._delay_all_reduce_params)[0].dtype
+            _cal.calibrate(self.process_group, sizes, cdt)
+        self.comm_calibration = getattr(self.process_group, "comm_calibration", None)
         self.bucket_plan, _ = _bp.resolve_plan(bucket_policy, bucket_cap_mb, first_bucket_cap_mb, total_bytes,
                                                self.process_group.size(), self.process_group.backend)
         self.bucket_bytes_cap = self.bucket_plan.cap_bytes
