@@ -274,37 +274,58 @@ struct PeerLane {
   int blocks = 0;
   int64_t slot_bytes = 0;
 
-  void open(const std::shared_ptr<Store>& store, const std::string& tag, int rank, int size, int nblocks,
-            int64_t slot) {
+  // Every rank publishes its handle — or an error marker — before it looks at the others', so a
+  // rank whose allocation or export failed never leaves its peers waiting on a key that will not
+  // come; returns "" on success, else the first failure (this rank's or a peer's marker).
+  std::string open(const std::shared_ptr<Store>& store, const std::string& tag, int rank, int size, int nblocks,
+                   int64_t slot) {
     blocks = nblocks;
     slot_bytes = slot;
     const int64_t flag_bytes = ((int64_t)nblocks * kPeerMaxRanks * 4 + 4095) / 4096 * 4096;
     const size_t bytes = flag_bytes + 2 * (size_t)slot;
-    // uncached: the flags and staged data are read by the peers over xGMI while this GPU writes them
-    XDDP_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&own), bytes, hipDeviceMallocUncached));
-    XDDP_HIP_CHECK(hipMemset(own, 0, bytes));
-    // per workgroup: its call counter, then its fail word (the call number of a timed-out barrier)
-    XDDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&gen_dev), 2 * nblocks * sizeof(uint32_t)));
-    XDDP_HIP_CHECK(hipMemset(gen_dev, 0, 2 * nblocks * sizeof(uint32_t)));
-    XDDP_HIP_CHECK(hipDeviceSynchronize());
-    hipIpcMemHandle_t h;
-    XDDP_HIP_CHECK(hipIpcGetMemHandle(&h, own));
-    store->set("peer/h/" + tag + "/" + std::to_string(rank),
-               std::string(reinterpret_cast<const char*>(&h), sizeof(h)));
+    std::string err, mine;
+    try {
+      // uncached: the flags and staged data are read by the peers over xGMI while this GPU writes them
+      XDDP_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&own), bytes, hipDeviceMallocUncached));
+      XDDP_HIP_CHECK(hipMemset(own, 0, bytes));
+      // per workgroup: its call counter, then its fail word (the call number of a timed-out barrier)
+      XDDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&gen_dev), 2 * nblocks * sizeof(uint32_t)));
+      XDDP_HIP_CHECK(hipMemset(gen_dev, 0, 2 * nblocks * sizeof(uint32_t)));
+      XDDP_HIP_CHECK(hipDeviceSynchronize());
+      hipIpcMemHandle_t h;
+      XDDP_HIP_CHECK(hipIpcGetMemHandle(&h, own));
+      mine = std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+    } catch (const std::exception& e) {
+      err = std::string("rank ") + std::to_string(rank) + ": " + e.what();
+      mine = "ERR";
+    }
+    store->set("peer/h/" + tag + "/" + std::to_string(rank), mine);
     for (int r = 0; r < size; ++r) {
       uint8_t* base = own;
       if (r != rank) {
         std::string s = store->get("peer/h/" + tag + "/" + std::to_string(r));
-        TORCH_CHECK(s.size() == sizeof(hipIpcMemHandle_t), "peer all-reduce: bad IPC handle from rank ", r);
+        if (!err.empty()) continue;  // (still read every key: the exchange stays symmetric)
+        if (s.size() != sizeof(hipIpcMemHandle_t)) {
+          err = "rank " + std::to_string(r) + " could not export its staging buffer";
+          continue;
+        }
         hipIpcMemHandle_t ph;
         std::memcpy(&ph, s.data(), sizeof(ph));
         void* p = nullptr;
-        XDDP_HIP_CHECK(hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess));
+        const hipError_t e = hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+          err = "rank " + std::to_string(rank) + ": hipIpcOpenMemHandle of rank " + std::to_string(r) + " failed (" +
+                hipGetErrorString(e) + ")";
+          continue;
+        }
         base = static_cast<uint8_t*>(p);
       }
-      pp.flags[r] = reinterpret_cast<uint32_t*>(base);
-      pp.data[r] = base + flag_bytes;
+      if (err.empty()) {
+        pp.flags[r] = reinterpret_cast<uint32_t*>(base);
+        pp.data[r] = base + flag_bytes;
+      }
     }
+    return err;
   }
 
   void close(int rank, int size) {
@@ -337,7 +358,7 @@ PeerAllReduce::PeerAllReduce(std::shared_ptr<Store> store, int rank, int size, i
                                hipHostMallocMapped | hipHostMallocCoherent));
   *impl_->status_host = 0;
   XDDP_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&impl_->status_dev), impl_->status_host, 0));
-  impl_->one.open(store, "1", rank, size, kPeerMaxBlocks, capacity);
+  std::string err = impl_->one.open(store, "1", rank, size, kPeerMaxBlocks, capacity);
   if (two_shot_capacity > 0) {
     // XDDP_PEER_TWO_SHOT_BLOCKS: workgroups of the two-shot grid (8..256, default 64). Every
     // workgroup of a launch is resident while it waits for its peers, and a CU holding one cannot
@@ -346,7 +367,8 @@ PeerAllReduce::PeerAllReduce(std::shared_ptr<Store> store, int rank, int size, i
     // GEMMs run concurrently stalled every launch until the timeout (scripts/peer_stress.py).
     int nb = kPeerTwoShotDefaultBlocks;
     if (const char* e = std::getenv("XDDP_PEER_TWO_SHOT_BLOCKS")) nb = std::max(8, std::min(kPeerTwoShotBlocks, std::atoi(e)));
-    impl_->two.open(store, "2", rank, size, nb, two_shot_capacity);
+    const std::string e2 = impl_->two.open(store, "2", rank, size, nb, two_shot_capacity);
+    if (err.empty()) err = e2;
   }
   int khz = 0;
   XDDP_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
@@ -354,9 +376,16 @@ PeerAllReduce::PeerAllReduce(std::shared_ptr<Store> store, int rank, int size, i
   timeout_ms_ = t ? std::atof(t) : static_cast<double>(timeout.count());
   impl_->khz = khz > 0 ? khz : 100000;
   impl_->timeout_ticks = (uint64_t)(timeout_ms_ * impl_->khz);
-  // every rank mapped every buffer before the first call raises a flag in it
-  store->set("peer/ok/" + std::to_string(rank), "1");
-  for (int r = 0; r < size; ++r) store->get("peer/ok/" + std::to_string(r));
+  // every rank mapped every buffer before the first call raises a flag in it; a failure anywhere
+  // fails the construction on EVERY rank (all of them read every rank's verdict)
+  store->set("peer/ok/" + std::to_string(rank), err.empty() ? "1" : "0");
+  std::string first_bad;
+  for (int r = 0; r < size; ++r)
+    if (store->get("peer/ok/" + std::to_string(r)) != "1" && first_bad.empty()) first_bad = std::to_string(r);
+  if (!err.empty() || !first_bad.empty()) {
+    close();
+    TORCH_CHECK(false, "peer all-reduce: IPC setup failed (", err.empty() ? "rank " + first_bad + " failed" : err, ")");
+  }
 }
 
 PeerAllReduce::~PeerAllReduce() {
@@ -365,7 +394,7 @@ PeerAllReduce::~PeerAllReduce() {
 }
 
 void PeerAllReduce::close() {
-  if (!impl_ || !impl_->one.own) return;
+  if (!impl_ || (!impl_->one.own && !impl_->two.own && !impl_->status_host)) return;
   c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
   (void)hipDeviceSynchronize();  // best effort: close() also runs on error paths
   impl_->one.close(rank_, size_);

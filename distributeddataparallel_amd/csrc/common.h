@@ -6,8 +6,10 @@
 
 #include <chrono>
 #include <cstdint>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 
 #define XDDP_HIP_CHECK(expr)                                                          \
   do {                                                                                \
@@ -22,6 +24,20 @@ inline int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(
              std::chrono::steady_clock::now().time_since_epoch())
       .count();
+}
+
+// Opt a kernel in to `lds` bytes (> 64 KiB) of dynamic LDS, once per kernel: the attribute is a
+// property of the function, so the cache is keyed by the kernel pointer (one static per launch
+// site would skip the call for a second kernel launched from the same site with less LDS).
+inline void ensure_dyn_lds(const void* kern, size_t lds) {
+  if (lds <= 65536) return;
+  static std::mutex mu;
+  static std::unordered_map<const void*, size_t> done;
+  std::lock_guard<std::mutex> g(mu);
+  size_t& cur = done[kern];
+  if (lds <= cur) return;
+  XDDP_HIP_CHECK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  cur = lds;
 }
 
 // Reduction ops, numbered like c10d::ReduceOp::RedOpType so Python enums line up.

@@ -519,11 +519,7 @@ std::vector<at::Tensor> conv3x3_halo(const at::Tensor& x, const at::Tensor& w, b
   const int BN = (int)N;
   const size_t lds = std::max<size_t>((size_t)hrows * 128 + 3 * (size_t)BN * 128, (size_t)256 * (BN * 2 + 16));
   auto go = [&](auto kern, int nt) {
-    static size_t lds_set = 0;
-    if (lds > 65536 && lds > lds_set) {
-      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      lds_set = lds;
-    }
+    ensure_dyn_lds((const void*)kern, lds);
     hipLaunchKernelGGL(kern, dim3((unsigned)mtiles), dim3(nt), lds, stream,
                        reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()), zeros, (int)N, hg,
@@ -581,11 +577,7 @@ std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w
   Geo3 geo{(int)IH, (int)IW, (int)OH, (int)OW, (int)stride};
   const uint16_t* zeros = zero_line(x);
   auto go = [&](auto kern, int nt, size_t lds) {
-    static size_t lds_set = 0;
-    if (lds > 65536 && lds > lds_set) {
-      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      lds_set = lds;
-    }
+    ensure_dyn_lds((const void*)kern, lds);
     hipLaunchKernelGGL(kern, dim3(mtiles * ntiles), dim3(nt), lds, stream,
                        reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()), zeros, (int)M, (int)N, (int)C, geo,
@@ -638,11 +630,7 @@ std::vector<at::Tensor> conv1x1_dma_forward(const at::Tensor& x, const at::Tenso
   Geo3 geo{(int)IH, (int)IW, (int)OH, (int)OW, (int)stride};
   const uint16_t* zeros = zero_line(x);
   auto go = [&](auto kern, int nt, size_t lds) {
-    static size_t lds_set = 0;
-    if (lds > 65536 && lds > lds_set) {
-      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      lds_set = lds;
-    }
+    ensure_dyn_lds((const void*)kern, lds);
     hipLaunchKernelGGL(kern, dim3(mtiles * ntiles), dim3(nt), lds, stream,
                        reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(wc.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()), zeros, (int)M, (int)N, (int)C, geo,
@@ -679,6 +667,10 @@ at::Tensor conv3x3_dgrad_s2(const at::Tensor& dy, const at::Tensor& w_rot, int64
                   (reinterpret_cast<uintptr_t>(w_rot.data_ptr()) % 16) == 0,
               "conv3x3_dgrad_s2: 16-B aligned operands required");
   TORCH_CHECK(B * H * W < (int64_t(1) << 31) && dy.numel() < (int64_t(1) << 40), "conv3x3_dgrad_s2: bad size");
+  // even input sizes (every ResNet stride-2 3x3): the four phase GEMMs on the dense GEMM's 4-phase
+  // LDS-DMA pipeline, one launch, written straight to the strided pixels (gemm.hip DGS2)
+  if (H == 2 * OH && W == 2 * OW && C % 128 == 0 && ((N / 64) & (N / 64 - 1)) == 0 && dy.numel() < (int64_t(1) << 31))
+    return conv3x3_dgrad_s2_gemm(dy, w_rot, H, W, zero_line(dy));
   auto dx = at::empty({B, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int cfg = tile_choice((int)C);
   const int BM = cfg == 1 || cfg == 3 || cfg == 4 ? 128 : 256, BN = cfg <= 1 ? 128 : 64;
@@ -695,11 +687,7 @@ at::Tensor conv3x3_dgrad_s2(const at::Tensor& dy, const at::Tensor& w_rot, int64
   Geo3 geo{(int)OH, (int)OW, (int)OH, (int)OW, 1};
   const uint16_t* zeros = zero_line(dy);
   auto go = [&](auto kern, int nt, size_t lds) {
-    static size_t lds_set = 0;
-    if (lds > 65536 && lds > lds_set) {
-      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      lds_set = lds;
-    }
+    ensure_dyn_lds((const void*)kern, lds);
     hipLaunchKernelGGL(kern, dim3(total), dim3(nt), lds, stream, reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                        reinterpret_cast<const uint16_t*>(w_rot.data_ptr()), reinterpret_cast<uint16_t*>(dx.data_ptr()),
                        zeros, 0, (int)C, (int)N, geo, nullptr, ntiles, dg);

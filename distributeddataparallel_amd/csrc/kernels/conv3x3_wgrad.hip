@@ -50,18 +50,23 @@ __device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
 // XOR applied to a row's 32-B chunk-pair index (0..3), from the pixel's 2-D LDS coordinates
 __device__ __forceinline__ int swp(int y, int x) { return (x & 3) ^ (y & 1); }
 
-template <int ST>
+// NB = output channels (n) per block: 64 (4 waves, one 16-channel c slice each) or 128 (stride 2:
+// 8 waves, wave w owns n half w >> 2 and c slice w & 3). At stride 2 the staged X halo (289
+// pixels per 64 output pixels) dominates the bytes per stage; sharing it between two n halves
+// halves the staging per MFMA and puts two waves on each SIMD.
+template <int ST, int NB = 64>
 struct Halo {
+  static constexpr int NW = NB / 16;                     // waves: 4 | 8
   // phases: 1 (stride 1) or 4 (stride 2: (row parity, column parity)); each phase an IYN x 10 grid
   static constexpr int PHASES = ST == 1 ? 1 : 4;
   static constexpr int IYN = ST == 1 ? kP + 2 : kP + 1;  // 10 | 9 (valid columns: the same)
   static constexpr int IXW = 10;                         // row pitch of a phase grid (even: see swp)
   static constexpr int ROWS = PHASES * IYN * IXW;        // 100 | 360 LDS rows
   static constexpr int INSTR = (ROWS + 7) / 8;           // DMA wave-instructions (8 rows each)
-  static constexpr int PER_WAVE = (INSTR + 3) / 4;       // 4 | 12
-  static constexpr int BROWS = PER_WAVE * 32;            // 128 | 384 rows reserved
+  static constexpr int PER_WAVE = (INSTR + NW - 1) / NW; // 4 | 12 (NB 64), 6 (NB 128)
+  static constexpr int BROWS = PER_WAVE * NW * 8;        // 128 | 384 rows reserved
   static constexpr int STAGES = ST == 1 ? 3 : 2;
-  static constexpr int STAGE = (64 + BROWS) * 128;       // bytes per stage
+  static constexpr int STAGE = (NB + BROWS) * 128;       // bytes per stage (dY rows: NB / 64 images)
   // LDS row of halo pixel (hy, hx) (0 <= hy < (kP-1)·ST+3)
   __device__ static int row(int hy, int hx) {
     if (ST == 1) return hy * IXW + hx;
@@ -71,20 +76,21 @@ struct Halo {
   __device__ static int xcoord(int hx) { return ST == 1 ? hx : hx >> 1; }
 };
 
-template <int ST>
-__global__ __launch_bounds__(256, ST == 1 ? 2 : 1) void conv3x3_wgrad_kernel(
+template <int ST, int NB = 64>
+__global__ __launch_bounds__(NB * 4, ST == 1 ? 2 : 1) void conv3x3_wgrad_kernel(
     const uint16_t* __restrict__ dY, const uint16_t* __restrict__ X, float* __restrict__ ws,
     const uint16_t* __restrict__ zeros, int N, int C, int IH, int IW, int OH, int OW, int pgh, int pgw,
     int npatch, int ntiles, int splits) {
-  using H = Halo<ST>;
+  using H = Halo<ST, NB>;
   constexpr int STG = H::STAGES, LPS = 2 + H::PER_WAVE;  // DMA instructions per stage per wave
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nh = wid >> 2, cw = wid & 3;  // this wave's n half (NB = 128) and 16-channel c slice
   const int wg = dev::xcd_remap(blockIdx.x, gridDim.x);
   const int tile = wg % ntiles, sidx = wg / ntiles;  // XCD neighbours: same pixels, other tiles
   const int ctiles = C >> 6;
-  const int n0 = (tile / ctiles) * 64, c0 = (tile % ctiles) * 64;
+  const int n0 = (tile / ctiles) * NB, c0 = (tile % ctiles) * 64;
   const int p_begin = (int)((int64_t)npatch * sidx / splits), p_end = (int)((int64_t)npatch * (sidx + 1) / splits);
 
   // per-lane DMA row decode (patch-relative), fixed for the whole kernel
@@ -92,7 +98,7 @@ __global__ __launch_bounds__(256, ST == 1 ? 2 : 1) void conv3x3_wgrad_kernel(
   int a_py[2], a_px[2], a_chunk[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int r = (wid * 2 + i) * 8 + (lane >> 3);  // patch pixel 0..63
+    const int r = (cw * 2 + i) * 8 + (lane >> 3);  // patch pixel 0..63 (of n half nh)
     a_py[i] = r >> 3;
     a_px[i] = r & 7;
     a_chunk[i] = pos ^ (2 * swp(a_py[i], a_px[i]));
@@ -113,15 +119,15 @@ __global__ __launch_bounds__(256, ST == 1 ? 2 : 1) void conv3x3_wgrad_kernel(
 
   auto issue = [&](int p, int buf) {
     uint8_t* A = smem + buf * H::STAGE;
-    uint8_t* B = A + 64 * 128;
+    uint8_t* B = A + NB * 128;
     const int per_img = pgh * pgw;
     const int b = p / per_img, pr = p - b * per_img, oy0 = (pr / pgw) * kP, ox0 = (pr % pgw) * kP;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int oy = oy0 + a_py[i], ox = ox0 + a_px[i];
       const bool ok = oy < OH && ox < OW;
-      const uint16_t* src = ok ? dY + (((int64_t)b * OH + oy) * OW + ox) * N + n0 + a_chunk[i] * 8 : zeros;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(A + (wid * 2 + i) * 1024), 16, 0, 0);
+      const uint16_t* src = ok ? dY + (((int64_t)b * OH + oy) * OW + ox) * N + n0 + 64 * nh + a_chunk[i] * 8 : zeros;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(A + nh * 8192 + (cw * 2 + i) * 1024), 16, 0, 0);
     }
     const int gy0 = oy0 * ST - 1, gx0 = ox0 * ST - 1;
 #pragma unroll
@@ -151,8 +157,8 @@ __global__ __launch_bounds__(256, ST == 1 ? 2 : 1) void conv3x3_wgrad_kernel(
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (k + STG - 1 < np) issue(p_begin + k + STG - 1, (k + STG - 1) % STG);
-    const uint8_t* A = smem + (k % STG) * H::STAGE;
-    const uint8_t* B = A + 64 * 128;
+    const uint8_t* A = smem + (k % STG) * H::STAGE + nh * 8192;
+    const uint8_t* B = smem + (k % STG) * H::STAGE + NB * 128;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int py = ks * 4 + g;
@@ -169,15 +175,15 @@ __global__ __launch_bounds__(256, ST == 1 ? 2 : 1) void conv3x3_wgrad_kernel(
         const int r = t / 3, s = t % 3;
         const int hy = py * ST + r, hx0 = q4 * ST + s, hx1 = (4 + q4) * ST + s;
         const int y = H::ycoord(hy), x0 = H::xcoord(hx0), x1 = H::xcoord(hx1);
-        const v4s v8[2] = {lds_tr16(B + H::row(hy, hx0) * 128 + ((wid ^ swp(y, x0)) * 32) + 8 * p4),
-                           lds_tr16(B + H::row(hy, hx1) * 128 + ((wid ^ swp(y, x1)) * 32) + 8 * p4)};
+        const v4s v8[2] = {lds_tr16(B + H::row(hy, hx0) * 128 + ((cw ^ swp(y, x0)) * 32) + 8 * p4),
+                           lds_tr16(B + H::row(hy, hx1) * 128 + ((cw ^ swp(y, x1)) * 32) + 8 * p4)};
         const bf16x8 b = __builtin_bit_cast(bf16x8, v8);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][t], 0, 0, 0);
       }
     }
   }
-  // fp32 slab ws[sidx][n][tap][c]: lane holds n = n0 + 16i + 4(lane >> 4) + r, c = c0 + 16·wid + (lane & 15)
+  // fp32 slab ws[sidx][n][tap][c]: lane holds n = n0 + 64 nh + 16i + 4(lane >> 4) + r, c = c0 + 16 cw + (lane & 15)
   float* out = ws + (int64_t)sidx * N * 9 * C;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -185,8 +191,8 @@ __global__ __launch_bounds__(256, ST == 1 ? 2 : 1) void conv3x3_wgrad_kernel(
     for (int t = 0; t < 9; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int n = n0 + 16 * i + 4 * (lane >> 4) + r;
-        out[((int64_t)n * 9 + t) * C + c0 + 16 * wid + (lane & 15)] = acc[i][t][r];
+        const int n = n0 + 64 * nh + 16 * i + 4 * (lane >> 4) + r;
+        out[((int64_t)n * 9 + t) * C + c0 + 16 * cw + (lane & 15)] = acc[i][t][r];
       }
 }
 
@@ -260,28 +266,27 @@ at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_
   const int64_t npatch64 = B * pgh * pgw;
   TORCH_CHECK(npatch64 > 0 && npatch64 < (int64_t(1) << 31), "conv3x3_wgrad_patch: bad patch count");
   const int npatch = (int)npatch64;
-  const int ntiles = (int)((N / 64) * (C / 64));
-  const int per_cu = stride == 1 ? 2 : 1;  // resident blocks per CU (LDS: 72 KB | 112 KB per block)
+  // stride 2 with N % 128 == 0: 128-channel n tiles (8 waves sharing one staged halo)
+  const int nb = stride == 2 && N % 128 == 0 ? 128 : 64;
+  const int ntiles = (int)((N / nb) * (C / 64));
+  const int per_cu = stride == 1 ? 2 : 1;  // resident blocks per CU (LDS: 72 KB | 112 / 128 KB per block)
   int splits = std::max(1, std::min(npatch, (cu_count() * per_cu + ntiles - 1) / ntiles));
   if (splits_req > 0) splits = (int)std::min<int64_t>(npatch, splits_req);
   auto ws = at::empty({splits, N, 9, C}, dy.options().dtype(at::kFloat));
   auto dw = at::empty({N, C, 3, 3}, dy.options().dtype(w_like.scalar_type()).memory_format(at::MemoryFormat::ChannelsLast));
   auto stream = c10::hip::getCurrentHIPStream(dy.device().index()).stream();
   const uint16_t* zeros = zero_line_w(x);
-  auto go = [&](auto kern, size_t lds) {
-    static size_t lds_set = 0;
-    if (lds > 65536 && lds > lds_set) {
-      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      lds_set = lds;
-    }
-    hipLaunchKernelGGL(kern, dim3(ntiles * splits), dim3(256), lds, stream,
+  auto go = [&](auto kern, size_t lds, int threads) {
+    ensure_dyn_lds((const void*)kern, lds);
+    hipLaunchKernelGGL(kern, dim3(ntiles * splits), dim3(threads), lds, stream,
                        reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
                        ws.data_ptr<float>(), zeros, (int)N, (int)C, (int)IH, (int)IW, (int)OH, (int)OW, pgh, pgw,
                        npatch, ntiles, splits);
     XDDP_HIP_CHECK(hipGetLastError());
   };
-  if (stride == 1) go(conv3x3_wgrad_kernel<1>, (size_t)Halo<1>::STAGES * Halo<1>::STAGE);
-  else go(conv3x3_wgrad_kernel<2>, (size_t)Halo<2>::STAGES * Halo<2>::STAGE);
+  if (stride == 1) go(conv3x3_wgrad_kernel<1>, (size_t)Halo<1>::STAGES * Halo<1>::STAGE, 256);
+  else if (nb == 128) go(conv3x3_wgrad_kernel<2, 128>, (size_t)Halo<2, 128>::STAGES * Halo<2, 128>::STAGE, 512);
+  else go(conv3x3_wgrad_kernel<2>, (size_t)Halo<2>::STAGES * Halo<2>::STAGE, 256);
   const int64_t nk = N * 9 * C;
   const int grid = (int)((nk / 4 + 63) / 64);
   auto red = [&](auto tag) {

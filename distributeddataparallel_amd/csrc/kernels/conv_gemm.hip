@@ -1028,11 +1028,7 @@ void launch_gemm(int pro, bool stats, bool bt, dim3 grid, size_t lds, hipStream_
                  const uint16_t* w, uint16_t* y, int64_t M, int N, int K, RowMap rm, const float* pss, float* part,
                  int mt, int nt, int groups, const uint16_t* x2, const EpiBN& epi, const ProOut& po) {
   auto go = [&](auto kern) {
-    static size_t lds_set = 0;  // per kernel instantiation: opt in to > 64 KB of dynamic LDS once
-    if (lds > 65536 && lds > lds_set) {
-      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      lds_set = lds;
-    }
+    ensure_dyn_lds((const void*)kern, lds);
     hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, s, x, w, y, M, N, K, rm, pss, part, mt, nt, groups, x2,
                        epi, po);
   };
@@ -1198,11 +1194,7 @@ std::vector<at::Tensor> conv1x1_gemm(const at::Tensor& x, const at::Tensor& w, i
                                         mtiles, ntiles, groups, x2p, epi, po)
   if (pro >= 4) {
     auto go = [&](auto kern) {
-      static size_t lds_set = 0;
-      if (lds > 65536 && lds > lds_set) {
-        XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        lds_set = lds;
-      }
+      ensure_dyn_lds((const void*)kern, lds);
       hipLaunchKernelGGL(kern, grid, dim3(512), lds, stream, xp, wp, yp, M, (int)N, (int)K, rm, pss, pp, mtiles, ntiles,
                          groups, x2p, epi, po);
     };
@@ -1265,11 +1257,7 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stri
   RowMap rm{(int)OH, (int)OW, (int)IH, (int)IW, (int)stride};
   const size_t lds = 2 * (size_t)64 * ((TN * 2 + 32) + (TK * 2 + 32));
   auto go = [&](auto kern) {
-    static size_t lds_set = 0;
-    if (lds > 65536 && lds > lds_set) {
-      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      lds_set = lds;
-    }
+    ensure_dyn_lds((const void*)kern, lds);
     hipLaunchKernelGGL(kern, dim3(S * tiles), dim3(256), lds, stream,
                        reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
                        ws.data_ptr<float>(), (int)M, (int)N, (int)K, rm, ntiles, ktiles, (int)mchunk, y2p, cfp,
@@ -1336,11 +1324,7 @@ std::vector<at::Tensor> conv1x1_bwd_fused(const at::Tensor& g, const at::Tensor&
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
   const size_t lds = 2 * (size_t)64 * ((N * 2 + 32) + (K * 2 + 32)) + (size_t)N * (K * 2 + 32);
   auto go = [&](auto kern) {
-    static size_t lds_set = 0;
-    if (lds > 65536 && lds > lds_set) {
-      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      lds_set = lds;
-    }
+    ensure_dyn_lds((const void*)kern, lds);
     hipLaunchKernelGGL(kern, dim3(S), dim3(256), lds, stream, reinterpret_cast<const uint16_t*>(g.data_ptr()),
                        reinterpret_cast<const uint16_t*>(y2.data_ptr()), coef.data_ptr<float>(),
                        reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
@@ -1382,11 +1366,7 @@ at::Tensor conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stri
   RowMap rm{(int)OH, (int)OW, (int)IH, (int)IW, (int)stride};
   const size_t lds = 2 * (size_t)64 * ((TN * 2 + 32) + (TK * 2 + 32));
   auto go = [&](auto kern) {
-    static size_t lds_set = 0;
-    if (lds > 65536 && lds > lds_set) {
-      XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      lds_set = lds;
-    }
+    ensure_dyn_lds((const void*)kern, lds);
     hipLaunchKernelGGL(kern, dim3(S * tiles), dim3(256), lds, stream,
                        reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
                        ws.data_ptr<float>(), (int)M, (int)N, (int)K, rm, ntiles, ktiles, (int)mchunk, nullptr, nullptr,

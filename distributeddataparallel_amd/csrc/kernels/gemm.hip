@@ -49,15 +49,30 @@ enum Epi : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiResidual = 3,
 // that tap, or a zero line for padding taps (no branch). Same pipeline as the dense GEMM; this is
 // the ResNet-50 3x3 forward / stride-1 input gradient for N >= 256, where the 4-phase loop beats
 // the 3-stage conv3x3.hip kernel (scripts/conv3x3_ceiling.py).
+//
+// DGS2 (MODE 2): the input gradient of a stride-2 3x3 pad-1 convolution as four phase GEMMs in one
+// launch. dX pixel (2i + ph, 2j + pw) only receives the taps whose stride-2 window lands on it:
+// with the 180-degree-rotated weight wr[ci][a][b][co] = w[co][2-a][2-b][ci],
+//   dX[2i+ph][2j+pw] = sum over a in A(ph), b in A(pw) of dY[i + r(a)][j + s(b)] · wr[a][b]
+// where A(0) = {1} (offset 0) and A(1) = {0 (offset 0), 2 (offset +1)}: phases of 1, 2, 2 and 4
+// taps, K = taps x Cout. Row m of phase p = dY-grid pixel (b, i, j); its K-tiles DMA the dY pixels
+// under the phase's taps (zero line past the bottom / right edge) and the matching Cout block of
+// wr's tap (B = wr viewed [Cin, 9 Cout], ldb = 9 Cout); the C tile is written straight to the
+// strided dX pixels — every dX pixel exactly once, no zero-fill, no scatter pass. Blocks are
+// phase-major, heaviest phase first (4 taps, then the two 2-tap phases, then the 1-tap one), and
+// the XCD remap / grouped tile order run inside each phase.
 struct ConvGeo {
   int IH, IW, OH, OW, stride, C;
   const uint16_t* zeros;
+  int XH = 0, XW = 0;  // DGS2: dX spatial size (even); IH/IW = OH/OW = the dY grid
 };
+
+constexpr int kModeDense = 0, kModeConv = 1, kModeDgS2 = 2;
 
 
 __device__ __forceinline__ float bf(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
 
-template <int BN, int EPI, bool CONV = false>
+template <int BN, int EPI, int MODE = kModeDense>
 __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A,
                                                               const uint16_t* __restrict__ B,
                                                               uint16_t* Y, uint16_t* __restrict__ Y2,
@@ -71,6 +86,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   constexpr int STAGE = (kBM + BN) * 128;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
+  constexpr bool CONV = MODE != kModeDense;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / kWN, wn = wid % kWN;
   // Tile order: the XCD remap gives each XCD a contiguous run of logical tiles (32 at a time on
   // its 32 CUs); logical tiles go through groups of GM m-tiles, M fastest inside a group, so such
@@ -78,13 +94,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   // XCD's L2 — instead of one A panel and 32 B panels (a full row of N tiles), which made every
   // XCD stream all of B (2.6x hipBLASLt's HBM bytes on 8192^3, profiles/r3_pmc_kernels.txt).
   constexpr int GM = BN == 256 ? 8 : 4;  // 8 x 4 tiles of 256 x 256, 4 x 8 of 256 x 128
-  const int wg = dev::xcd_remap(blockIdx.x, gridDim.x);
-  const int mtiles = gridDim.x / ntiles, grp = wg / (GM * ntiles), first_m = grp * GM;
+  // DGS2: phase-major blocks (heaviest first), each phase a full M x N tile grid
+  const int tiles = MODE == kModeDgS2 ? gridDim.x / 4 : gridDim.x;
+  const int pidx = MODE == kModeDgS2 ? blockIdx.x / tiles : 0;
+  const int ph = pidx == 0 || pidx == 2, pw = pidx <= 1;  // phase order (1,1) (0,1) (1,0) (0,0)
+  const int wg = dev::xcd_remap(blockIdx.x - pidx * tiles, tiles);
+  const int mtiles = tiles / ntiles, grp = wg / (GM * ntiles), first_m = grp * GM;
   const int gm = min(mtiles - first_m, GM), local = wg - grp * GM * ntiles;
   const int mt = first_m + local % gm, nt = local / gm;
   const int n0 = nt * BN, m0 = mt * kBM;
   const int pos = lane & 7;  // 16-B slot this lane fills in its 128-B LDS row
-  const int nk = K / kBK;
+  // DGS2: the phase's tap count (1 << (ph + pw)) times the Cout blocks; ldb = 9 Cout
+  const int nk = MODE == kModeDgS2 ? ((cg.C / kBK) << (ph + pw)) : K / kBK;
+  const int ldb = MODE == kModeDgS2 ? 9 * cg.C : K;
 
   // DMA sources: lane l of wave w fills 16-B slot (l & 7) of rows (w*AI + i)*8 + (l >> 3); the
   // offsets are recomputed per issue from two per-lane values (few live VGPRs: the 4-phase loop
@@ -95,7 +117,22 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   // and that pixel's element offset (may point before the row for padding windows; never
   // dereferenced then). Host-checked: the input has < 2^31 elements.
   int vmask[CONV ? AI : 1], cbase[CONV ? AI : 1];  // CONV: taps inside the image (bit t), window offset
-  if constexpr (CONV) {
+  if constexpr (MODE == kModeDgS2) {
+    // row = dY-grid pixel (b, i, j); tap t of the phase reads dY (i + r_t, j + s_t), r_t, s_t in {0, 1}
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int row = min(m0 + drow + i * 8 * NW, M - 1);
+      const int hw = cg.OH * cg.OW, b = row / hw, rem = row - b * hw, y = rem / cg.OW, x = rem - y * cg.OW;
+      int m = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int r = ph ? (t >> pw) : 0, sx = pw ? (t & 1) : 0;
+        m |= (y + r < cg.IH && x + sx < cg.IW) << t;
+      }
+      vmask[i] = m;
+      cbase[i] = ((b * cg.IH + y) * cg.IW + x) * cg.C + dchunk;
+    }
+  } else if constexpr (CONV) {
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int row = min(m0 + drow + i * 8 * NW, M - 1);
@@ -111,7 +148,20 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   }
   auto issue = [&](int kt, int buf) {
     uint8_t* As = smem + buf * STAGE;
-    if constexpr (CONV) {
+    int boff = kt * kBK;  // B's K offset (DGS2: the tap's block of wr)
+    if constexpr (MODE == kModeDgS2) {
+      const int lg = cg.stride >> 16, tap = kt >> lg, cb = kt & ((1 << lg) - 1);
+      const int tr = pw ? tap >> 1 : tap, tc = pw ? tap & 1 : 0;  // row / column tap of the phase
+      const int r = ph ? tr : 0, sx = pw ? tc : 0, a = ph ? 2 * tr : 1, bb = pw ? 2 * tc : 1;
+      const int toff = (r * cg.IW + sx) * cg.C + cb * kBK;
+      boff = (a * 3 + bb) * cg.C + cb * kBK;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const bool ok = (vmask[i] >> tap) & 1;
+        const uint16_t* src = ok ? A + (cbase[i] + toff) : cg.zeros;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + (wid * 8 + i * 8 * NW) * 128), 16, 0, 0);
+      }
+    } else if constexpr (CONV) {
       // C / 64 is a power of two (host-checked): cg.stride's high half carries its log2
       const int lg = cg.stride >> 16, tap = kt >> lg, cb = kt & ((1 << lg) - 1), r = (tap * 11) >> 5, sx = tap - 3 * r;
       const int toff = (r * cg.IW + sx) * cg.C + cb * kBK;
@@ -132,7 +182,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
     uint8_t* Bs = As + kBM * 128;
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
-      const uint16_t* src = B + (uint32_t)(n0 + drow + j * 8 * NW) * (uint32_t)K + (uint32_t)(dchunk + kt * kBK);
+      const uint16_t* src = B + (uint32_t)(n0 + drow + j * 8 * NW) * (uint32_t)ldb + (uint32_t)(dchunk + boff);
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(Bs + (wid * 8 + j * 8 * NW) * 128), 16, 0, 0);
     }
   };
@@ -309,7 +359,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
     const int row = q / CPR;
     if (row >= rows_valid) continue;
     u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
-    const int64_t off = (int64_t)(m0 + row) * N + n0 + cc * 8;
+    int64_t off = (int64_t)(m0 + row) * N + n0 + cc * 8;
+    if constexpr (MODE == kModeDgS2) {  // dY-grid pixel (b, i, j) -> dX pixel (b, 2i + ph, 2j + pw)
+      const int m = m0 + row, hw = cg.OH * cg.OW, b = m / hw, rem = m - b * hw, y = rem / cg.OW, x = rem - y * cg.OW;
+      off = (((int64_t)b * cg.XH + 2 * y + ph) * cg.XW + 2 * x + pw) * N + n0 + cc * 8;
+    }
     if (EPI == kEpiBiasGelu) {
       *reinterpret_cast<u32x4*>(Y + off) = v;  // pre-activation (the backward's dGELU input)
       u32x4 g;
@@ -416,21 +470,21 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   }
 }
 
-template <int BN, int EPI, bool CONV = false>
+template <int BN, int EPI, int MODE = kModeDense>
 void launch_gemm(const at::Tensor& a, const at::Tensor& b, uint16_t* y, uint16_t* y2, const uint16_t* bias,
                  const uint16_t* res, float* part, int64_t ldr, int M, int N, int K, hipStream_t stream,
                  const ConvGeo& cg = ConvGeo{}) {
-  const int mtiles = (M + kBM - 1) / kBM, ntiles = N / BN;
+  const int mtiles = (M + kBM - 1) / kBM, ntiles = N / BN, phases = MODE == kModeDgS2 ? 4 : 1;
   // stages | C tile (+ the column-sum exchange of the dGELU epilogue)
   const size_t lds = std::max<size_t>((size_t)2 * (kBM + BN) * 128,
                                       (size_t)kBM * (BN * 2 + 16) + (EPI == kEpiDGelu ? (size_t)2048 * NW : 0));
   static bool attr = false;
   if (!attr) {
-    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI, CONV>,
+    XDDP_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_nt_kernel<BN, EPI, MODE>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI, CONV>), dim3(mtiles * ntiles), dim3(kThreads), lds, stream,
+  hipLaunchKernelGGL((gemm_nt_kernel<BN, EPI, MODE>), dim3(phases * mtiles * ntiles), dim3(kThreads), lds, stream,
                      reinterpret_cast<const uint16_t*>(a.data_ptr()), reinterpret_cast<const uint16_t*>(b.data_ptr()),
                      y, y2, bias, res, part, M, N, K, ntiles, ldr, cg);
   XDDP_HIP_CHECK(hipGetLastError());
@@ -569,9 +623,32 @@ std::vector<at::Tensor> conv3x3_gemm(const at::Tensor& x, const at::Tensor& w, i
   auto* yp = reinterpret_cast<uint16_t*>(y.data_ptr());
   float* pp = stats ? part.data_ptr<float>() : nullptr;
   const int K = (int)(9 * C);
-  if (stats) launch_gemm<BN, kEpiStats, true>(x, w, yp, nullptr, nullptr, nullptr, pp, N, (int)M, (int)N, K, stream, cg);
-  else launch_gemm<BN, kEpiNone, true>(x, w, yp, nullptr, nullptr, nullptr, pp, N, (int)M, (int)N, K, stream, cg);
+  if (stats) launch_gemm<BN, kEpiStats, kModeConv>(x, w, yp, nullptr, nullptr, nullptr, pp, N, (int)M, (int)N, K, stream, cg);
+  else launch_gemm<BN, kEpiNone, kModeConv>(x, w, yp, nullptr, nullptr, nullptr, pp, N, (int)M, (int)N, K, stream, cg);
   return {y, part};
+}
+
+// Input gradient of a stride-2 3x3 pad-1 convolution (DGS2, four phase GEMMs in one launch):
+// dy [B, Cout, OH, OW] bf16 channels_last, wr = the rotated weight [Cin, Cout, 3, 3] channels_last
+// (OHWI memory: wr[ci][a][b][co] = w[co][2-a][2-b][ci], conv3x3_rot_weight) -> dx [B, Cin, XH, XW]
+// channels_last with XH = 2 OH, XW = 2 OW (even input sizes). Cin % 128 == 0, Cout / 64 a power of two.
+at::Tensor conv3x3_dgrad_s2_gemm(const at::Tensor& dy, const at::Tensor& wr, int64_t XH, int64_t XW,
+                                 const uint16_t* zeros) {
+  const int64_t B = dy.size(0), Co = dy.size(1), OH = dy.size(2), OW = dy.size(3), Ci = wr.size(0);
+  TORCH_CHECK(wr.size(1) == Co && XH == 2 * OH && XW == 2 * OW, "conv3x3_dgrad_s2_gemm: even input sizes only");
+  TORCH_CHECK(Co % 64 == 0 && Ci % 128 == 0 && dy.numel() < (int64_t(1) << 31) && B * XH * XW * Ci < (int64_t(1) << 40),
+              "conv3x3_dgrad_s2_gemm: unsupported shape");
+  const int lg = __builtin_ctz((unsigned)(Co / 64));
+  TORCH_CHECK((Co / 64) == (int64_t(1) << lg), "conv3x3_dgrad_s2_gemm: Cout / 64 must be a power of two");
+  const int64_t M = B * OH * OW;
+  auto dx = at::empty({B, Ci, XH, XW}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto stream = c10::hip::getCurrentHIPStream(dy.device().index()).stream();
+  ConvGeo cg{(int)OH, (int)OW, (int)OH, (int)OW, 2 | (lg << 16), (int)Co, zeros};
+  cg.XH = (int)XH;
+  cg.XW = (int)XW;
+  launch_gemm<128, kEpiNone, kModeDgS2>(dy, wr, reinterpret_cast<uint16_t*>(dx.data_ptr()), nullptr, nullptr, nullptr,
+                                        nullptr, Ci, (int)M, (int)Ci, (int)(4 * Co), stream, cg);
+  return dx;
 }
 
 }  // namespace kernels

@@ -69,9 +69,14 @@ def test_conv3x3_rotated_weight_gives_input_gradient(cin, cout, h, w):
     (3, 64, 15, 15, 128),    # odd input: the last dY row/column feeds the even phase only
     (2, 128, 28, 28, 128),   # ResNet-50 layer2 entry shape (reduced batch), 256x128 tiles
     (1, 512, 14, 14, 512),   # layer4 entry shape, long reduction
+    (2, 256, 28, 28, 256),   # layer3 entry shape
+    (1, 128, 56, 56, 128),   # layer2 entry spatial size
+    (1, 128, 6, 10, 64),     # 15 dY pixels: one partial m-tile per phase, Cout 64 (1-K-tile phase)
 ])
 def test_conv3x3_dgrad_s2_matches_conv2d(b, cin, h, w, cout):
-    """Stride-2 input gradient over the four phase grids (conv3x3.hip DG2) vs fp32 autograd."""
+    """Stride-2 input gradient over the four phase grids vs fp32 autograd: even input sizes with
+    Cin % 128 == 0 run the four phase GEMMs on the dense GEMM pipeline (gemm.hip DGS2), the odd
+    ones the phase-grid kernel (conv3x3.hip DG2)."""
     torch.manual_seed(3)
     x = torch.randn(b, cin, h, w, device="cuda")
     wt = torch.randn(cout, cin, 3, 3, device="cuda") / (9 * cin) ** 0.5
@@ -124,7 +129,9 @@ def test_conv3x3_bn_relu_forward_backward(stride):
     (3, 64, 14, 14, 128, 1),    # partial patches (14 = 8 + 6), 2 n-tiles
     (2, 128, 9, 7, 64, 1),      # odd spatial size, 2 c-tiles
     (2, 64, 15, 15, 64, 2),     # strided, odd input size (phase-split halo)
-    (2, 128, 28, 28, 128, 2),   # strided, ResNet-50 layer2 entry shape (reduced batch)
+    (2, 128, 28, 28, 128, 2),   # strided, ResNet-50 layer2 entry shape (reduced batch): 128-channel n tiles
+    (2, 256, 14, 14, 256, 2),   # strided, layer3 entry shape: 2 x 4 tiles of 128 x 64
+    (1, 64, 16, 16, 128, 2),    # strided, N = 128 over a 64-channel input
     (1, 512, 7, 7, 512, 1),     # one partial patch per image, 64 tiles
     (4, 64, 56, 56, 64, 1),     # ResNet-50 layer1 shape (reduced batch): many splits
 ])
