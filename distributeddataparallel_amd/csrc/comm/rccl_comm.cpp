@@ -440,7 +440,8 @@ class RcclComm : public Comm {
     const char* e = std::getenv("XDDP_PEER_ALLREDUCE");
     const bool autom = e && std::string(e) == "auto";
     const int mode = autom ? 2 : (e ? std::atoi(e) : 0);
-    if (mode <= 0 || size_ < 2 || size_ > kPeerMaxRanks) return;
+    // (one rank: only with XDDP_RCCL_FORCE_LAUNCH, so a one-GPU box runs the peer / calibration path)
+    if (mode <= 0 || size_ > kPeerMaxRanks || (size_ < 2 && !force_launch_)) return;
     auto env_i64 = [](const char* k, int64_t d) {
       const char* v = std::getenv(k);
       return v ? static_cast<int64_t>(std::atof(v)) : d;

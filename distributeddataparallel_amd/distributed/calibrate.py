@@ -199,7 +199,9 @@ def calibrate(pg, sizes: Sequence[int], dtype=torch.bfloat16, iters: int = 5) ->
     ``pg.comm_calibration``. No-op report for one rank or a backend without device collectives."""
     from ..parallel import bucket_policy as bp
 
-    if pg.size() <= 1 or pg.backend not in ("rccl", "peer"):
+    one_rank_forced = (pg.size() == 1 and pg.backend == "rccl" and os.environ.get("XDDP_RCCL_FORCE_LAUNCH") == "1"
+                       and os.environ.get("XDDP_CALIBRATE_ONE_RANK") == "1")  # (one-GPU test of the RCCL path)
+    if (pg.size() <= 1 and not one_rank_forced) or pg.backend not in ("rccl", "peer"):
         rep = {"skipped": f"{pg.backend} backend with {pg.size()} rank(s): nothing to calibrate"}
         pg.comm_calibration = rep
         return rep

@@ -55,3 +55,38 @@ def test_calibration_peer_backend_self_check_and_routes():
 
 def test_calibration_corrupted_self_check_falls_back_on_every_rank():
     run_ranks(_w_calibrate, world=2, backend="peer", args=(False,), env={"XDDP_CALIBRATE_CORRUPT_RANK": "1"})
+
+
+def _w_calibrate_rccl_one_rank(rank, world, corrupt):
+    """The RCCL communicator's side of the calibration on one GPU: forced RCCL launches at W = 1
+    with the peer lanes on probation (XDDP_PEER_ALLREDUCE=auto), allreduce_via on every route, the
+    route table, and the probation verdict (kept, or closed after a failed self-check)."""
+    from distributeddataparallel_amd import distributed as xdist
+    from distributeddataparallel_amd.distributed import calibrate as cal
+    from distributeddataparallel_amd.parallel import bucket_policy as bp
+
+    pg = xdist.get_default_group()
+    assert pg.backend == "rccl" and set(pg.comm.routes()) == {2, 3}
+    assert pg.comm_info()["peer_probation"] == "1"
+    try:
+        rep = cal.calibrate(pg, [64 << 10, MiB, 8 * MiB], torch.bfloat16, iters=3)
+        assert rep["self_check"]["ok"] is (not corrupt), rep
+        if corrupt:
+            assert list(pg.comm.routes()) == [] and rep["route_table"] == [{"max_bytes": None, "route": "base"}]
+        else:
+            assert pg.comm_info()["peer_probation"] == "0" and set(rep["timings_ms"]) == {"base", "one_shot", "two_shot"}
+        for n in (1000, MiB // 2 + 3):  # every route the table picks still reduces exactly (W = 1: identity)
+            x = torch.arange(n, device="cuda", dtype=torch.float32)
+            pg.allreduce(x, xdist.ReduceOp.SUM).wait()
+            torch.cuda.synchronize()
+            assert torch.equal(x.cpu(), torch.arange(n, dtype=torch.float32))
+    finally:
+        bp.clear_calibration()
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_calibration_rccl_communicator_one_rank(corrupt):
+    env = {"XDDP_RCCL_FORCE_LAUNCH": "1", "XDDP_PEER_ALLREDUCE": "auto", "XDDP_CALIBRATE_ONE_RANK": "1"}
+    if corrupt:
+        env["XDDP_CALIBRATE_CORRUPT_RANK"] = "0"
+    run_ranks(_w_calibrate_rccl_one_rank, world=1, backend="rccl", args=(corrupt,), env=env)
