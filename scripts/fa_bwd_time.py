@@ -45,6 +45,7 @@ def main():
         dq, dk, dv = run()
         print(json.dumps({"shape": name, "bwd_us": round(us, 1), "tflops": round(flops / us / 1e6, 1),
                           "dq_stages": os.environ.get("XDDP_FA_DQ_STAGES", "3"),
+                          "dkdv_stages": os.environ.get("XDDP_FA_DKDV_STAGES", "2"),
                           "finite": bool(torch.isfinite(dq).all() and torch.isfinite(dk).all())}), flush=True)
 
 
