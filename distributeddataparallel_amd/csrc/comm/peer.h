@@ -25,6 +25,20 @@ constexpr int kPeerMaxBlocks = 64;
 constexpr int kPeerTwoShotBlocks = 256;
 constexpr int kPeerTwoShotDefaultBlocks = 64;
 
+// Before a rank frees its peer lanes at shutdown: a peer may still be reading this rank's staging
+// slot (a two-shot peer gathers the reduced slices after this rank's own kernel has finished), so
+// every rank posts "closing" and waits — bounded, a shutdown on an error path is not collective —
+// until all ranks have posted it: then no rank runs a peer kernel any more.
+inline void peer_quiesce(const std::shared_ptr<Store>& store, int rank, int size, std::chrono::milliseconds timeout) {
+  try {
+    store->set("peer/closing/" + std::to_string(rank), "1");
+    std::vector<std::string> keys;
+    for (int r = 0; r < size; ++r) keys.push_back("peer/closing/" + std::to_string(r));
+    store->wait(keys, timeout);
+  } catch (...) {
+  }
+}
+
 class PeerAllReduce {
  public:
   // Collective over `size` ranks of one node (all must construct it; IPC handles go through

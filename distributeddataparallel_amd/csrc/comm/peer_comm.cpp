@@ -236,6 +236,11 @@ class PeerComm : public Comm {
 
   void shutdown() override {
     stop_watchdog();
+    {
+      c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device_));
+      (void)hipStreamSynchronize(stream_.stream());
+    }
+    peer_quiesce(store_, rank_, size_, std::chrono::seconds(10));
     peer_->close();
   }
 

@@ -418,7 +418,10 @@ class RcclComm : public Comm {
       ncclCommDestroy(comm_);
       destroyed_ = true;
     }
-    if (peer_) peer_->close();
+    if (auto pr = std::atomic_load(&peer_)) {
+      peer_quiesce(store_, rank_, size_, std::chrono::seconds(10));
+      pr->close();
+    }
   }
 
   // Peer-memory routing (comm/peer_allreduce.hip), node-local groups of 2..8 ranks:
