@@ -12,9 +12,8 @@ GEMM over the strided pixels (compact), handed to the next consumer's epilogue o
 
 The ResNet bottleneck's 3x3 conv + BN + ReLU (``conv3x3_bn_relu``) runs on the implicit-GEMM
 kernel of ``csrc/kernels/conv3x3.hip`` with the same statistics epilogue; its stride-1 input
-gradient is that kernel on (dY, rot180(W)ᵀ) (the stride-2 one: the same kernel over four phase
-grids of dX, opt-in, MIOpen is faster there); the stride-1 weight gradient is
-``conv3x3_wgrad.hip``, the stride-2 one stays on MIOpen.
+gradient is that kernel on (dY, rot180(W)ᵀ) (the stride-2 one: four phase GEMMs of 1/2/2/4 taps
+on the dense GEMM pipeline, ``gemm.hip`` DGS2); both weight gradients are ``conv3x3_wgrad.hip``.
 
 Parameters and buffers stay in the original ``nn.Conv2d`` / ``FusedBatchNorm2d`` modules, so
 state_dict layout and DDP bucketing are unchanged.
@@ -464,11 +463,12 @@ class _Conv3x3BNReLU(torch.autograd.Function):
             # four phase grids of the strided dX, 1/2/2/4 taps each, one launch (conv3x3.hip DG2)
             dx = C.conv3x3_dgrad_s2(dy, C.conv3x3_rot_weight(w), x.size(2), x.size(3))
             need_x = False
-        if need_w and _wgrad3() and (s == 1 or os.environ.get("XDDP_CONV3X3_WGRAD_S2", "0") == "1"):
+        if need_w and _wgrad3() and (s == 1 or os.environ.get("XDDP_CONV3X3_WGRAD_S2", "1") != "0"):
             # 8x8 output patches sharing one staged X halo across the 9 taps (conv3x3_wgrad.hip):
-            # 96-98 us vs MIOpen's 120-182 us per stride-1 ResNet-50 shape (bs256); the stride-2
-            # variant (phase-split halo) loses (175-193 vs 120-134 us), MIOpen keeps those
-            # (scripts/wgrad3_bench.py, profiles/r2_wgrad3_bench.txt)
+            # 96-98 us vs MIOpen's 120-182 us per stride-1 ResNet-50 shape (bs256); at stride 2 the
+            # phase-split halo is shared by 128 output channels (8 waves): 127 / 118 / 108 vs
+            # MIOpen's 150 / 139 / 145 us (profiles/r4_s2_bwd_vs_miopen.txt; XDDP_CONV3X3_WGRAD_S2=0
+            # hands it back to MIOpen)
             dw = C.conv3x3_wgrad_patch(dy, x, s, w)
             need_w = False
         if need_x or need_w:
@@ -496,12 +496,11 @@ def _conv3x3() -> bool:
 
 
 def _dgrad3_s2() -> bool:
-    """XDDP_CONV3X3_DGRAD_S2=1 runs the stride-2 3x3 input gradient on the phase-grid kernel
-    (conv3x3.hip DG2). Off by default: MIOpen is faster on all three ResNet-50 shapes, zero-fill
-    included (177/149/139 vs 185/168/169 us at bs256, r2 measurement,
-    profiles/r2_dg2_vs_miopen.txt) — the 1- and 2-tap phases are too short to fill the 3-stage
-    pipeline of a one-block-per-CU tile."""
-    return os.environ.get("XDDP_CONV3X3_DGRAD_S2", "0") == "1"
+    """The stride-2 3x3 input gradient as four phase GEMMs on the 4-phase LDS-DMA GEMM pipeline
+    (gemm.hip DGS2: 1/2/2/4 taps per phase, written straight to the strided pixels, no zero-fill):
+    142 / 97 / 86 us vs MIOpen's 170 / 141 / 136 us on the three ResNet-50 bs256 shapes
+    (profiles/r4_s2_bwd_vs_miopen.txt). XDDP_CONV3X3_DGRAD_S2=0 hands it back to MIOpen."""
+    return os.environ.get("XDDP_CONV3X3_DGRAD_S2", "1") != "0"
 
 
 def _epi() -> bool:
