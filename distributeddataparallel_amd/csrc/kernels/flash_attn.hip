@@ -328,20 +328,15 @@ __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(const uint16_t* __restr
 
 // dQ: one workgroup = NW waves x 32 query rows of one (batch, q head); S^T and dP^T with the
 // query on the lane (as the forward), dQ^T += K^T · dS^T. NW = 8 pairs two waves per SIMD.
-template <int D, bool CAUSAL, int NW, int STG = 3>
+template <int D, bool CAUSAL, int NW>
 __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
     uint16_t* __restrict__ dQ, int Sq, int Sk, int Hq, int Hkv, Strides qs, Strides ks, Strides vs, Strides dos,
     Strides dqs, float scale_log2, float scale, int nqb) {
   constexpr int KS = D / 16, NT = D / 32, BQ = 32 * NW;
-  // STG K/V stages (2 or 3): tile j + STG - 1's DMA goes out right after tile j's barrier, so with
-  // three stages each tile's load has two tiles of compute to land in. Per wave and tile: 2 PER
-  // DMA instructions (K and V), the count per tile the barrier's vmcnt leaves in flight.
-  static_assert(STG == 2 || STG == 3, "2 or 3 K/V stages");
-  constexpr int PER = (kBK / (512 / D)) / NW;
   // [stage][K (row reads for S^T, transposed reads for dQ), V (row reads for dP^T)]
-  __shared__ __attribute__((aligned(16))) uint8_t KVs[STG][2][kBK * D * 2];
+  __shared__ __attribute__((aligned(16))) uint8_t KVs[2][2][kBK * D * 2];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 5;
   const int bh = blockIdx.y, b = bh / Hq, h = bh % Hq, hk = h / (Hq / Hkv);
   const uint16_t* Kb = K + b * ks.b + hk * ks.h;
@@ -373,26 +368,15 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_kernel(
     const int ntiles = (kend + kBK - 1) / kBK;
     dma_tile<D, NW>(Kb, ks.s, 0, Sk, KVs[0][0], w, lane);
     dma_tile<D, NW>(Vb, vs.s, 0, Sk, KVs[0][1], w, lane);
-    if (STG == 3 && ntiles > 1) {
-      dma_tile<D, NW>(Kb, ks.s, kBK, Sk, KVs[1][0], w, lane);
-      dma_tile<D, NW>(Vb, vs.s, kBK, Sk, KVs[1][1], w, lane);
-    }
-    int stc = 0;  // stage of tile j (j % STG, rotated: no division in the loop)
     for (int j = 0; j < ntiles; ++j) {
       const int k0 = j * kBK;
-      // tile j landed (with 3 stages tile j + 1 may stay in flight) and every wave is done with
-      // tile j - 1, whose stage the next DMA overwrites
-      if (STG == 3 && j + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();
-      const int stn = STG == 2 ? 1 - stc : (stc == 0 ? 2 : stc - 1);  // (j + STG - 1) % STG
-      if (j + STG - 1 < ntiles) {
-        dma_tile<D, NW>(Kb, ks.s, k0 + (STG - 1) * kBK, Sk, KVs[stn][0], w, lane);
-        dma_tile<D, NW>(Vb, vs.s, k0 + (STG - 1) * kBK, Sk, KVs[stn][1], w, lane);
+      dma_barrier();
+      if (j + 1 < ntiles) {
+        dma_tile<D, NW>(Kb, ks.s, k0 + kBK, Sk, KVs[(j + 1) & 1][0], w, lane);
+        dma_tile<D, NW>(Vb, vs.s, k0 + kBK, Sk, KVs[(j + 1) & 1][1], w, lane);
       }
-      const uint8_t* Kt = KVs[stc][0];
-      const uint8_t* Vt = KVs[stc][1];
-      stc = stc == STG - 1 ? 0 : stc + 1;
+      const uint8_t* Kt = KVs[j & 1][0];
+      const uint8_t* Vt = KVs[j & 1][1];
       if (!CAUSAL || k0 <= qw + 31) {
         const bool masked = k0 + kBK > Sk || (CAUSAL && k0 + kBK - 1 > qw);  // wave-uniform
         // one 32-key half at a time keeps S^T / dP^T at 32 live registers
@@ -866,14 +850,8 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
                          strides_of(dq), sl2, sc, nqb);
       XDDP_HIP_CHECK(hipGetLastError());
     };
-    // XDDP_FA_DQ_STAGES=2: the two-stage K/V ring (A/B of the three-stage default)
-    static const int dq_stages = [] {
-      const char* e = std::getenv("XDDP_FA_DQ_STAGES");
-      return e && e[0] == '2' ? 2 : 3;
-    }();
-#define XDDP_FA(D_, C_)                                                                          \
-  if (dq_stages == 2) { if (nw == 8) go(fa_bwd_dq_kernel<D_, C_, 8, 2>); else go(fa_bwd_dq_kernel<D_, C_, 4, 2>); } \
-  else if (nw == 8) go(fa_bwd_dq_kernel<D_, C_, 8>); else go(fa_bwd_dq_kernel<D_, C_, 4>)
+#define XDDP_FA(D_, C_) \
+  if (nw == 8) go(fa_bwd_dq_kernel<D_, C_, 8>); else go(fa_bwd_dq_kernel<D_, C_, 4>)
     if (D == 128) { if (causal) { XDDP_FA(128, true); } else { XDDP_FA(128, false); } }
     else { if (causal) { XDDP_FA(64, true); } else { XDDP_FA(64, false); } }
 #undef XDDP_FA
