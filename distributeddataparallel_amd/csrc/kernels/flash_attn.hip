@@ -162,7 +162,7 @@ __device__ __forceinline__ void dma_tile(const uint16_t* base, int64_t ss, int r
 // is DMA'd up front (64 KB of LDS) and the tile loop runs without barriers; waves whose 32 query
 // rows all lie past Sq skip the math.
 template <int D, bool CAUSAL, int NW, bool WH = false>
-__global__ __launch_bounds__(64 * NW, WH ? 4 : 1) void fa_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+__global__ __launch_bounds__(64 * NW, WH && NW == 8 ? 4 : 1) void fa_fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                         const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
                                                         float* __restrict__ LSE, int Sq, int Sk, int Hq, int Hkv,
                                                         Strides qs, Strides ks, Strides vs, Strides os,
@@ -451,7 +451,7 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_kernel(
 // one 16 x 16 tile of that item's dQ^T = K^T · dS^T on mfma_f32_16x16x32_bf16 over all 256 keys
 // (d = 16 (w & 3).., q = 16 (w >> 2)..): no cross-wave reduction, no atomics. Both LDS images are [row][256] bf16 with the 16-B chunk index XOR'd by
 // row & 15, so the 16 rows a b128 lane group reads sit in 16 distinct bank groups.
-template <int D, bool CAUSAL, int KW, bool FQ = false, int STG = 2>
+template <int D, bool CAUSAL, int KW, bool FQ = false>
 __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
@@ -470,12 +470,9 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
   static_assert(KW >= 2 && KW * NG == 8 && NIT % NI == 0 && (NIT < KW || NI * KW == NIT), "wave split");
   static_assert((NG - 1) * KW * ACC * 4 <= VBLK + 2 * NG * STAGE, "group reduction must fit the LDS");
   static_assert(!FQ || (KW == 8 && D == 64 && !CAUSAL), "fused dQ: one 256-key block, D = 64, non-causal");
-  // STG item stages per group (2, or 3: item k + 2's Q / dO DMA leaves right after item k's
-  // barrier, two items ahead of its use); 3 needs every wave to issue Q and dO pieces (NIT >= KW)
-  static_assert(STG == 2 || (STG == 3 && !FQ && NIT >= KW), "three stages: D = 128 / KW = 4 layout");
   constexpr int DSB = QB * BK * 2;                   // (FQ) one dS [QB][BK] bf16 buffer
   constexpr int FQB = FQ ? D * BK * 2 + 2 * DSB : 0;  // K^T [D][BK] + two dS buffers
-  __shared__ __attribute__((aligned(16))) uint8_t smem[VBLK + STG * NG * STAGE + FQB];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[VBLK + 2 * NG * STAGE + FQB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wq = w % KW, G = w / KW, g = lane >> 5;
   // blockIdx.x = (batch, kv head, head split), blockIdx.y = key block: the dispatcher walks x
   // first, so every workgroup of key block 0 (the heaviest under a causal mask) starts first.
@@ -506,7 +503,7 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
                       : bf16x8{};
   // (FQ) byte offset of element [row][col] of a [row][BK] bf16 LDS image, chunk-swizzled
   auto fq_off = [](int row, int col) { return row * (BK * 2) + (((col >> 3) ^ (row & 15)) << 4) + (col & 7) * 2; };
-  uint8_t* KT = smem + VBLK + STG * NG * STAGE;
+  uint8_t* KT = smem + VBLK + 2 * NG * STAGE;
   uint8_t* DSl = KT + D * BK * 2;
   const int kl = 32 * wq + (lane & 31);  // this lane's key within the block
   if constexpr (FQ) {  // K^T image from the K registers (zero rows past Sk come along)
@@ -526,7 +523,7 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
   const int qstart = CAUSAL ? (k0 / QB) * QB : 0;
   const int nqt = (Sq - qstart + QB - 1) / QB;
   const int total = hpw * nqt, niter = (total + NG - 1) / NG;
-  uint8_t* gsm = smem + VBLK + G * STG * STAGE;
+  uint8_t* gsm = smem + VBLK + G * 2 * STAGE;
   auto issue = [&](int it, int st) {  // rows past Sq read row Sq - 1 (masked below)
     const int h = hk * grp + split * hpw + it / nqt, qt0 = qstart + (it % nqt) * QB;
     uint8_t* S = gsm + st * STAGE;
@@ -569,28 +566,17 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
     }
   };
   if (G < total) issue(G, 0);
-  if (STG == 3 && G + NG < total) issue(G + NG, 1);
-  int stc = 0;  // stage of item k (k % STG, rotated)
   for (int k = 0; k < niter; ++k) {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     const int it = G + NG * k;
-    if (STG == 3 && it + NG < total) {
-      // item k landed; item k + 1's pieces (2 NI, + the lse / delta row on waves 0 and 1) stay in flight
-      if (wq < 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI + 1) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-    const int stn = STG == 2 ? 1 - stc : (stc == 0 ? 2 : stc - 1);  // (k + STG - 1) % STG
-    // into the stage item k - 1 was computed from
-    if (it + (STG - 1) * NG < total) issue(it + (STG - 1) * NG, stn);
+    if (it + NG < total) issue(it + NG, (k + 1) & 1);  // into the stage item k - 1 was computed from
     // (FQ: one group, non-causal, so every item is computed) item k - 1's dQ: its dS landed before
     // the barrier above; the buffer is rewritten at item k + 1, after the next barrier
     if constexpr (FQ)
       if (k > 0) dq_tile(it - 1, DSl + ((k - 1) & 1) * DSB);
     const int qt0 = qstart + (it % nqt) * QB;
     if (it < total && (!CAUSAL || qt0 + QB - 1 >= kw)) {
-      const uint8_t* Qt = gsm + stc * STAGE;
+      const uint8_t* Qt = gsm + (k & 1) * STAGE;
       const uint8_t* Dt = Qt + TILE;
       const float* lse_s = reinterpret_cast<const float*>(Qt + 2 * TILE);
       const float* dl_s = lse_s + QB;
@@ -636,7 +622,6 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
         }
       }
     }
-    stc = stc == STG - 1 ? 0 : stc + 1;
   }
   if constexpr (FQ) {  // the last item's dQ
     if (niter > 0) {
@@ -880,14 +865,7 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
                          strides_of(dq));
       XDDP_HIP_CHECK(hipGetLastError());
     };
-    // XDDP_FA_DKDV_STAGES=3: three Q / dO item stages per group at D = 128 (A/B)
-    static const int kv_stages = [] {
-      const char* e = std::getenv("XDDP_FA_DKDV_STAGES");
-      return e && e[0] == '3' ? 3 : 2;
-    }();
-    if (D == 128 && kv_stages == 3) {
-      if (causal) go(fa_bwd_dkdv_kernel<128, true, 4, false, 3>); else go(fa_bwd_dkdv_kernel<128, false, 4, false, 3>);
-    } else if (D == 128) { if (causal) go(fa_bwd_dkdv_kernel<128, true, 4>); else go(fa_bwd_dkdv_kernel<128, false, 4>); }
+    if (D == 128) { if (causal) go(fa_bwd_dkdv_kernel<128, true, 4>); else go(fa_bwd_dkdv_kernel<128, false, 4>); }
     else if (kwv == 8) go(fa_bwd_dkdv_kernel<64, false, 8, true>);
     else { if (causal) go(fa_bwd_dkdv_kernel<64, true, 4>); else go(fa_bwd_dkdv_kernel<64, false, 4>); }
     if (nsplit > 1) {  // the split-sum writes dense [B, Sk, Hkv, D]: strided outputs get a copy

@@ -266,9 +266,44 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(const T* __restrict_
 constexpr int kStrip = 14;
 
 template <typename T>
+struct Raw8 {  // 8 channel values as loaded: packed pairs for 16-bit dtypes, fp32 as is
+  static constexpr bool kPacked = !__is_same(T, float);
+  uint32_t w[kPacked ? 4 : 8];
+  __device__ __forceinline__ void load(const T* p) {
+    const dev::u32x4 a = *reinterpret_cast<const dev::u32x4*>(p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = a[j];
+    if constexpr (!kPacked) {
+      const dev::u32x4 b = *reinterpret_cast<const dev::u32x4*>(p + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[4 + j] = b[j];
+    }
+  }
+  __device__ __forceinline__ void set(const float (&v)[8]) {  // round to T
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (__is_same(T, bf16_t)) w[j] = dev::pack_bf16x2(v[2 * j], v[2 * j + 1]);
+      else if constexpr (__is_same(T, f16_t)) w[j] = dev::pack_f16x2(v[2 * j], v[2 * j + 1]);
+    }
+    if constexpr (!kPacked) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = __float_as_uint(v[j]);
+    }
+  }
+  __device__ __forceinline__ float get(int j) const {
+    if constexpr (__is_same(T, bf16_t)) return __uint_as_float((j & 1) ? (w[j >> 1] & 0xffff0000u) : (w[j >> 1] << 16));
+    else if constexpr (__is_same(T, f16_t))
+      return dev::f16_to_f32((uint16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xffffu)));
+    else return __uint_as_float(w[j]);
+  }
+};
+
+template <typename T>
 struct PoolWin {  // two adjacent pooling windows (u, u+1) of one window row, dy + dy2 summed
+  // the summed gradient is kept at storage precision (4 registers per window for 16-bit dtypes):
+  // the unfused stack stores dy + dy2 in T too (autograd sums the two uses of the pool output)
   uint64_t packed[2];
-  float g[2][8];
+  Raw8<T> g8[2];
   __device__ __forceinline__ void load(const T* dy, const T* dy2, const uint8_t* idx, int n, int oh, int u, int OH,
                                        int OW, int C, int c0) {
     const int ohc = min(oh, OH - 1);
@@ -276,40 +311,59 @@ struct PoolWin {  // two adjacent pooling windows (u, u+1) of one window row, dy
     for (int d = 0; d < 2; ++d) {
       const int64_t o = (((int64_t)n * OH + ohc) * OW + min(u + d, OW - 1)) * C + c0;
       packed[d] = *reinterpret_cast<const uint64_t*>(idx + o);
-      Vec8<T>::ld(dy + o, g[d]);
       if (dy2) {
-        float g2[8];
+        float g[8], g2[8];
+        Vec8<T>::ld(dy + o, g);
         Vec8<T>::ld(dy2 + o, g2);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[d][j] += g2[j];
+        for (int j = 0; j < 8; ++j) g[j] += g2[j];
+        g8[d].set(g);
+      } else {
+        g8[d].load(dy + o);
       }
       if (oh >= OH || u + d >= OW) packed[d] = ~0ull;  // no window: matches no position
     }
   }
+  __device__ __forceinline__ float g(int d, int j) const { return g8[d].get(j); }
 };
 
 template <typename T, bool ELEM>
-__global__ __launch_bounds__(256) void stem_pool_bn_bwd_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ELEM && __is_same(T, bf16_t) ? 4 : 1)))
+void stem_pool_bn_bwd_kernel(
     const T* __restrict__ dy, const T* __restrict__ dy2, const uint8_t* __restrict__ idx, const T* __restrict__ y,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
     const float* __restrict__ coef, float* __restrict__ part, T* __restrict__ dx, int N, int H, int W, int C, int OH,
     int OW) {
+  // Per-channel constants live in LDS, not in 40-48 registers per lane: the kernel streams (every
+  // input read once, every output written once), so its speed is the number of waves in flight
+  // (bf16 dX pass: 128 VGPRs, 4 waves per SIMD; it was 178, 2 waves). ELEM folds the mean into the
+  // bias (dX = k1·g + k2·y + k3', k3' = k3 - k2·mean); each of the quad's four input pixels takes
+  // its window contributions, masks and emits before the next one (one 8-wide accumulator).
+  // cst rows: ELEM (scale, shift, k1, k3'), partials (scale, shift, mean); ck2 = k2 (ELEM only).
+  __shared__ float cst[4][64 * 8];  // C <= 512
+  __shared__ float ck2[ELEM ? 64 * 8 : 1];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    cst[0][c] = scale[c];
+    cst[1][c] = shift[c];
+    if (ELEM) {
+      cst[2][c] = coef[c];
+      cst[3][c] = fmaf(-coef[C + c], mean[c], coef[2 * C + c]);  // stem_conv_wgrad_fused: the same fma
+      ck2[c] = coef[C + c];
+    } else {
+      cst[2][c] = mean[c];
+    }
+  }
+  __syncthreads();
   const int cv = C / 8;
   const int QH = (H + 1) / 2, QW = (W + 1) / 2, NS = (QH + kStrip - 1) / kStrip;
   const int64_t total = (int64_t)N * NS * QW * cv;
   const int64_t q = (int64_t)dev::xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int c0 = (int)(threadIdx.x % cv) * 8;
-  float sc[8], sh[8], mu[8], k1[8], k2[8], k3[8], s1[8], s2[8];
-  Vec8<float>::ld(scale + c0, sc);
-  Vec8<float>::ld(shift + c0, sh);
-  Vec8<float>::ld(mean + c0, mu);
-  if (ELEM) {
-    Vec8<float>::ld(coef + c0, k1);
-    Vec8<float>::ld(coef + C + c0, k2);
-    Vec8<float>::ld(coef + 2 * C + c0, k3);
-  }
+  float s1[ELEM ? 1 : 8], s2[ELEM ? 1 : 8];
+  if (!ELEM) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+    for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  }
   if (q < total) {
     int64_t r = q / cv;
     const int u = (int)(r % QW);
@@ -320,54 +374,57 @@ __global__ __launch_bounds__(256) void stem_pool_bn_bwd_kernel(
     PoolWin<T> top, bot;
     top.load(dy, dy2, idx, n, t0, u, OH, OW, C, c0);
     for (int t = t0; t < t1; ++t) {
+      // re-read the LDS constants each quad row (an LDS read is cheap; 40 hoisted registers are not)
+      asm volatile("" ::: "memory");
       bot.load(dy, dy2, idx, n, t + 1, u, OH, OW, C, c0);
-      float yq[4][8];
+      // the quad's four y pixels are fetched together (clamped at the odd edge), outside the
+      // per-pixel branches, so their latencies overlap; 16-bit values stay packed until used
+      Raw8<T> yq[4];
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const int h = min(2 * t + (d >> 1), H - 1), w = min(2 * u + (d & 1), W - 1);
-        Vec8<T>::ld(y + (((int64_t)n * H + h) * W + w) * C + c0, yq[d]);
+        yq[d].load(y + (((int64_t)n * H + h) * W + w) * C + c0);
       }
-      float acc[4][8];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[a][j] = 0.f;
-#pragma unroll
-      for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-        for (int dw = 0; dw < 2; ++dw) {
-          const PoolWin<T>& win = dh ? bot : top;
-#pragma unroll
-          for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-              // input (2t + a, 2u + b) sits at offset (1 + a - 2dh, 1 + b - 2dw) of window (t + dh, u + dw)
-              const int kh = 1 + a - 2 * dh, kw = 1 + b - 2 * dw;
-              if (kh < 0 || kw < 0) continue;  // compile-time after unrolling
-              const int pos = kh * 3 + kw;
-#pragma unroll
-              for (int j = 0; j < 8; ++j)
-                if ((int)((win.packed[dw] >> (8 * j)) & 0xff) == pos) acc[a * 2 + b][j] += win.g[dw][j];
-            }
-        }
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
+          // input (2t + a, 2u + b) sits at offset (1 + a - 2dh, 1 + b - 2dw) of window (t + dh, u + dw)
+          float acc[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+            for (int dw = 0; dw < 2; ++dw) {
+              const int kh = 1 + a - 2 * dh, kw = 1 + b - 2 * dw;
+              if (kh < 0 || kw < 0) continue;  // compile-time after unrolling
+              const PoolWin<T>& win = dh ? bot : top;
+              const int pos = kh * 3 + kw;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const uint32_t word = (uint32_t)(win.packed[dw] >> (32 * (j >> 2)));
+                if (__builtin_amdgcn_ubfe(word, 8 * (j & 3), 8) == (uint32_t)pos) acc[j] += win.g(dw, j);
+              }
+            }
           const int h = 2 * t + a, w = 2 * u + b;
           if (h >= H || w >= W) continue;
-          const float* yv = yq[a * 2 + b];
+          float yv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) yv[j] = yq[a * 2 + b].get(j);
           float out[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
+            // constants are read four channels at a time (the barrier keeps the compiler from
+            // issuing all 40 LDS reads at once, which set the kernel's register peak)
+            if (j == 4) asm volatile("" ::: "memory");
             // g at the precision the unfused maxpool backward stores it, masked by the ReLU
-            const float g = fmaf(yv[j], sc[j], sh[j]) > 0.f ? rnd<T>(acc[a * 2 + b][j]) : 0.f;
-            const float dd = yv[j] - mu[j];
+            const float g = fmaf(yv[j], cst[0][c0 + j], cst[1][c0 + j]) > 0.f ? rnd<T>(acc[j]) : 0.f;
             if (ELEM) {
-              out[j] = fmaf(k1[j], g, fmaf(k2[j], dd, k3[j]));
+              out[j] = fmaf(cst[2][c0 + j], g, fmaf(ck2[c0 + j], yv[j], cst[3][c0 + j]));
             } else {
               s1[j] += g;
-              s2[j] = fmaf(g, dd, s2[j]);
+              s2[j] = fmaf(g, yv[j] - cst[2][c0 + j], s2[j]);
             }
           }
           if (ELEM) dev::st8_stream(dx + (((int64_t)n * H + h) * W + w) * C + c0, out);
@@ -552,7 +609,7 @@ at::Tensor stem_pool_bn_backward(const at::Tensor& dy_in, const c10::optional<at
   const int64_t lanes = (int64_t)N * (((H + 1) / 2 + kStrip - 1) / kStrip) * ((W + 1) / 2) * (C / 8);
   TORCH_CHECK(lanes < ((int64_t)1 << 31) - 256, "stem_pool_bn_backward: input too large");
   const int grid = (int)((lanes + 255) / 256);
-  TORCH_CHECK(256 % (C / 8) == 0, "stem_pool_bn_backward: C / 8 must divide 256");
+  TORCH_CHECK(256 % (C / 8) == 0 && C <= 512, "stem_pool_bn_backward: C / 8 must divide 256, C <= 512");
   at::Tensor out = elem ? at::empty_like(x, at::MemoryFormat::ChannelsLast)
                         : at::empty({grid, C, 2}, x.options().dtype(at::kFloat));
   dispatch_pool(x.scalar_type(), [&](auto tag) {

@@ -272,7 +272,7 @@ struct PoolBwd {
   const uint16_t* dyp2;  // second consumer's gradient (or null)
   const uint8_t* idx;    // byte argmax [N, OHp, OWp, 64]
   const uint16_t* y;     // conv output (BN input) [N, OH, OW, 64]
-  const float* coef6;    // [6][64]: scale, shift, mean, k1, k2, k3 (unfolded BN-backward coefficients)
+  const float* coef6;    // [6][64]: scale, shift, mean, k1, k2, k3 - k2·mean (dY = k1·g + k2·y + k3')
   int OHp, OWp;
 };
 
@@ -291,7 +291,8 @@ __global__ __launch_bounds__(256, FUSED ? 1 : 2) void stem_conv_wgrad_kernel(con
   const int cp = wv & 1, nh = wv >> 1;
   const int ntiles = N * tiles_h * tiles_w;
   if (FUSED) {
-    for (int i = tid; i < 6 * 64; i += 256) Cf[i] = pb.coef6[i];
+    for (int i = tid; i < 6 * 64; i += 256)  // k3' = k3 - k2·mean, the fma stem_pool_bn_backward uses
+      Cf[i] = i < 320 ? pb.coef6[i] : fmaf(-pb.coef6[i - 64], pb.coef6[i - 192], pb.coef6[i]);
   }
 
   auto tile_pos = [&](int tile, int& n, int& oh0, int& ow0) {
@@ -346,6 +347,15 @@ __global__ __launch_bounds__(256, FUSED ? 1 : 2) void stem_conv_wgrad_kernel(con
       const int h = min(2 * t + (d >> 1), OH - 1), w = min(2 * u + (d & 1), OW - 1);
       pk_y[d] = *reinterpret_cast<const dev::u32x4*>(pb.y + (((int64_t)n * OH + h) * OW + w) * 64 + c8 * 8);
     }
+    // dy + dy2 at storage precision, as autograd sums the pool output's two uses in the unfused
+    // stack (and as the materializing stem_pool_bn_backward does)
+    if (pb.dyp2) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          pk_g[d][e] = dev::pack_bf16x2(bfx(pk_g[d][e], 0) + bfx(pk_g2[d][e], 0), bfx(pk_g[d][e], 1) + bfx(pk_g2[d][e], 1));
+    }
     // one pixel of the quad at a time (8 live sums): pixel (2t + a, 2u + b) sits at offset
     // (1 + a - 2dh, 1 + b - 2dw) of window (t + dh, u + dw)
 #pragma unroll
@@ -364,7 +374,7 @@ __global__ __launch_bounds__(256, FUSED ? 1 : 2) void stem_conv_wgrad_kernel(con
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const uint32_t am = (pk_idx[d][j >> 2] >> (8 * (j & 3))) & 0xffu;
-            if (win && am == pos) acc[j] += bfx(pk_g[d][j >> 1], j & 1) + bfx(pk_g2[d][j >> 1], j & 1);
+            if (win && am == pos) acc[j] += bfx(pk_g[d][j >> 1], j & 1);
           }
         }
         const int row = (2 * qr + a) * 16 + 2 * qc + b;  // pixel index inside the 8 x 16 tile
@@ -379,7 +389,7 @@ __global__ __launch_bounds__(256, FUSED ? 1 : 2) void stem_conv_wgrad_kernel(con
             const float yv = bfx(pk_y[a * 2 + b][e], hh);
             // g at the precision the unfused maxpool backward stores it, masked by the ReLU
             const float g = fmaf(yv, Cf[c], Cf[64 + c]) > 0.f ? bf16r(acc[j]) : 0.f;
-            r2[hh] = valid ? fmaf(Cf[192 + c], g, fmaf(Cf[256 + c], yv - Cf[128 + c], Cf[320 + c])) : 0.f;
+            r2[hh] = valid ? fmaf(Cf[192 + c], g, fmaf(Cf[256 + c], yv, Cf[320 + c])) : 0.f;
           }
           o4[e] = dev::pack_bf16x2(r2[0], r2[1]);
         }

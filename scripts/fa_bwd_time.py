@@ -2,7 +2,7 @@
 """Flash-attention backward (own HIP kernels) per call at the BASELINE transformer shapes:
 Llama-3-8B (B2 S4096 H32/8 D128 causal, the PMC table's shape) and ViT-L/16 (B256 S197 H16 D64).
 Prints analytic TF/s (5 GEMMs of the backward with one recompute; causal counts half), so
-variants selected by environment switches (e.g. XDDP_FA_DKDV_STAGES) can be A/B'd in one box.
+variants selected by environment switches can be A/B'd in one box.
 
 usage: python scripts/fa_bwd_time.py [--iters 20]
 """
@@ -44,7 +44,6 @@ def main():
         flops = 5 * 2.0 * B * H * S * S * D * (0.5 if causal else 1.0)
         dq, dk, dv = run()
         print(json.dumps({"shape": name, "bwd_us": round(us, 1), "tflops": round(flops / us / 1e6, 1),
-                          "dkdv_stages": os.environ.get("XDDP_FA_DKDV_STAGES", "2"),
                           "finite": bool(torch.isfinite(dq).all() and torch.isfinite(dk).all())}), flush=True)
 
 
