@@ -146,8 +146,27 @@ __global__ __launch_bounds__(NB * 4, ST == 1 ? 2 : 1) void conv3x3_wgrad_kernel(
     for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // transposed-read addressing: group g (lane >> 4) = patch row within the k-step, lane (4q + p)
-  // supplies pixel column q (+4 for the second read) and bytes 8p of its 32-B chunk pair
+  // supplies pixel column q (+4 for the second read) and bytes 8p of its 32-B chunk pair. The
+  // swizzle depends on the lane only through (q + dx) & 3 and (g + dy) & 1, so each read is a
+  // per-lane base (4 for A, 6 | 4 for the halo) plus a compile-time offset the ds_read absorbs.
   const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  constexpr int DXN = ST == 1 ? 3 : 2;
+  int a_off[4], b_off[DXN][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a_off[i] = (g * 8 + q4) * 128 + ((i ^ swp(g, q4)) * 32) + 8 * p4;
+#pragma unroll
+  for (int dx = 0; dx < DXN; ++dx)
+#pragma unroll
+    for (int dp = 0; dp < 2; ++dp)
+      b_off[dx][dp] = (g * H::IXW + q4 + dx) * 128 + ((cw ^ ((q4 + dx) & 3) ^ ((g + dp) & 1)) * 32) + 8 * p4;
+  auto read_b = [&](const uint8_t* B, int ks, int t) {
+    const int r = t / 3, s = t % 3;
+    const int dy = ST == 1 ? r : r >> 1, dx = ST == 1 ? s : s >> 1;
+    const int phase = ST == 1 ? 0 : (r & 1) * 2 + (s & 1);
+    const uint8_t* p = B + b_off[dx][dy & 1] + (phase * H::IYN * H::IXW + (ks * 4 + dy) * H::IXW) * 128;
+    const v4s v8[2] = {lds_tr16(p), lds_tr16(p + 4 * 128)};
+    return __builtin_bit_cast(bf16x8, v8);
+  };
   const int np = p_end - p_begin;
   for (int k = 0; k < STG - 1 && k < np; ++k) issue(p_begin + k, k);
   for (int k = 0; k < np; ++k) {
@@ -159,28 +178,33 @@ __global__ __launch_bounds__(NB * 4, ST == 1 ? 2 : 1) void conv3x3_wgrad_kernel(
     if (k + STG - 1 < np) issue(p_begin + k + STG - 1, (k + STG - 1) % STG);
     const uint8_t* A = smem + (k % STG) * H::STAGE + nh * 8192;
     const uint8_t* B = smem + (k % STG) * H::STAGE + NB * 128;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int py = ks * 4 + g;
-      bf16x8 a[4];
+    auto read_a = [&](int ks, bf16x8 (&a)[4]) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int x0 = q4, x1 = 4 + q4;
-        const v4s v8[2] = {lds_tr16(A + (py * 8 + x0) * 128 + ((i ^ swp(py, x0)) * 32) + 8 * p4),
-                           lds_tr16(A + (py * 8 + x1) * 128 + ((i ^ swp(py, x1)) * 32) + 8 * p4)};
+        const uint8_t* p = A + a_off[i] + ks * 4 * 8 * 128;
+        const v4s v8[2] = {lds_tr16(p), lds_tr16(p + 4 * 128)};
         a[i] = __builtin_bit_cast(bf16x8, v8);
       }
+    };
+    // 18 (k-step, tap) steps; the next step's halo fragment (and, two taps before the end of
+    // k-step 0, k-step 1's dY fragments) are read while this step's 4 MFMAs run
+    bf16x8 a[4], an[4];
+    read_a(0, a);
+    bf16x8 b = read_b(B, 0, 0);
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int r = t / 3, s = t % 3;
-        const int hy = py * ST + r, hx0 = q4 * ST + s, hx1 = (4 + q4) * ST + s;
-        const int y = H::ycoord(hy), x0 = H::xcoord(hx0), x1 = H::xcoord(hx1);
-        const v4s v8[2] = {lds_tr16(B + H::row(hy, hx0) * 128 + ((cw ^ swp(y, x0)) * 32) + 8 * p4),
-                           lds_tr16(B + H::row(hy, hx1) * 128 + ((cw ^ swp(y, x1)) * 32) + 8 * p4)};
-        const bf16x8 b = __builtin_bit_cast(bf16x8, v8);
+    for (int st = 0; st < 18; ++st) {
+      const int ks = st / 9, t = st % 9;
+      bf16x8 bn = b;
+      if (st < 17) bn = read_b(B, (st + 1) / 9, (st + 1) % 9);
+      if (st == 6) read_a(1, an);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][t], 0, 0, 0);
+      for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][t], 0, 0, 0);
+      b = bn;
+      if (st == 8) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = an[i];
       }
+      (void)ks;
     }
   }
   // fp32 slab ws[sidx][n][tap][c]: lane holds n = n0 + 64 nh + 16i + 4(lane >> 4) + r, c = c0 + 16 cw + (lane & 15)
@@ -267,6 +291,8 @@ at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_
   TORCH_CHECK(npatch64 > 0 && npatch64 < (int64_t(1) << 31), "conv3x3_wgrad_patch: bad patch count");
   const int npatch = (int)npatch64;
   // stride 2 with N % 128 == 0: 128-channel n tiles (8 waves sharing one staged halo)
+  // (a 128-channel tile at stride 1 measured 3-10 % slower: 96.0 / 97.5 / 93.5 / 91.7 vs
+  // 90.4 / 95.0 / 86.3 / 83.1 us on the four stage shapes, scripts/wgrad3_time.py)
   const int nb = stride == 2 && N % 128 == 0 ? 128 : 64;
   const int ntiles = (int)((N / nb) * (C / 64));
   const int per_cu = stride == 1 ? 2 : 1;  // resident blocks per CU (LDS: 72 KB | 112 / 128 KB per block)
