@@ -146,10 +146,16 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
   constexpr int CPR = BN / 8;                         // 16-B chunks per C-tile row
   static_assert(NT % CPR == 0, "readout mapping needs a fixed chunk column per thread");
   const int cc = tid % CPR;
-  float st_n = 0.f, st_s[8], st_ss[8];
-  u32x4 st_k = {0, 0, 0, 0};  // the shift, kept as the 8 packed bf16 values it came from
+  float st_s[8], st_ss[8];  // EPI: this thread's 8 channels' BN-backward sums
 #pragma unroll
   for (int e = 0; e < 8; ++e) st_s[e] = st_ss[e] = 0.f;
+  // STATS: a second pass over the stored C tile in LDS, thread = one channel pair (sp) of rows
+  // tid / SPR + SRS·i — 6 registers of state instead of 21 (the 8-channel form spilled at
+  // occupancy 4), shifted by the pair's first stored values (row 0 of the block's first tile).
+  constexpr int SPR = BN / 2, SRS = NT / SPR;
+  static_assert(SPR <= 64 && 64 % SPR == 0 && BM % SRS == 0, "stats pass mapping");
+  const int sp = tid % SPR;
+  float sn = 0.f, sk[2] = {0.f, 0.f}, ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
 
   const uint16_t* wrow[BR];
   constexpr int BCH = BN / 8;  // BT: 16-B chunks per staged k row (64 * BCH == NT * BR)
@@ -419,7 +425,26 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
         *reinterpret_cast<uint2*>(Cs + row * CST + col * 2) = pk;
       }
     lds_barrier();
-    if (STATS && mt == g) st_k = *reinterpret_cast<const u32x4*>(Cs + cc * 16);  // row 0: always valid
+    if (STATS) {
+      if (mt == g) {  // row 0: always valid
+        const uint32_t k = *reinterpret_cast<const uint32_t*>(Cs + sp * 4);
+        sk[0] = __uint_as_float(k << 16);
+        sk[1] = __uint_as_float(k & 0xffff0000u);
+      }
+#pragma unroll
+      for (int i = 0; i < BM / SRS; ++i) {
+        const int row = tid / SPR + SRS * i;
+        if (row < rows_valid) {
+          const uint32_t v = *reinterpret_cast<const uint32_t*>(Cs + row * CST + sp * 4);
+          const float d0 = __uint_as_float(v << 16) - sk[0], d1 = __uint_as_float(v & 0xffff0000u) - sk[1];
+          sn += 1.f;
+          ssum[0] += d0;
+          ssum[1] += d1;
+          ssq[0] = fmaf(d0, d0, ssq[0]);
+          ssq[1] = fmaf(d1, d1, ssq[1]);
+        }
+      }
+    }
 #pragma unroll
     for (int it = 0; it < RIT; ++it) {
       const int row = (tid + NT * it) / CPR;
@@ -454,18 +479,6 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
         }
         if (NTSTORE) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + (m0 + row) * N + n0 + cc * 8));
         else *reinterpret_cast<u32x4*>(Y + (m0 + row) * N + n0 + cc * 8) = v;
-        if (STATS) {
-          st_n += 1.f;
-#pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            const float d0 = __uint_as_float(v[h] << 16) - __uint_as_float(st_k[h] << 16);
-            const float d1 = __uint_as_float(v[h] & 0xffff0000u) - __uint_as_float(st_k[h] & 0xffff0000u);
-            st_s[2 * h] += d0;
-            st_s[2 * h + 1] += d1;
-            st_ss[2 * h] = fmaf(d0, d0, st_ss[2 * h]);
-            st_ss[2 * h + 1] = fmaf(d1, d1, st_ss[2 * h + 1]);
-          }
-        }
       }
     }
     lds_barrier();  // Cs aliases the operand buffers the next tile stores into
@@ -504,20 +517,19 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
   }
 
   if (STATS) {
-    // per thread (n, mean, M2) of its 8 channels, Chan-merged over the lanes sharing cc (xor over
-    // the lane bits above log2(CPR)), then over the waves through LDS
-    float mean[8], m2[8], n = st_n;
+    // per thread (n, mean, M2) of its channel pair, Chan-merged over the lanes sharing sp (xor over
+    // the lane bits above log2(SPR)), then over the waves through LDS
+    float mean[2], m2[2], n = sn;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float k = __uint_as_float((e & 1) ? (st_k[e >> 1] & 0xffff0000u) : (st_k[e >> 1] << 16));
-      mean[e] = n > 0.f ? k + st_s[e] / n : 0.f;
-      m2[e] = n > 0.f ? fmaxf(st_ss[e] - st_s[e] * st_s[e] / n, 0.f) : 0.f;
+    for (int e = 0; e < 2; ++e) {
+      mean[e] = n > 0.f ? sk[e] + ssum[e] / n : 0.f;
+      m2[e] = n > 0.f ? fmaxf(ssq[e] - ssum[e] * ssum[e] / n, 0.f) : 0.f;
     }
 #pragma unroll
-    for (int o = CPR; o < 64; o <<= 1) {
+    for (int o = SPR; o < 64; o <<= 1) {
       const float nb = __shfl_xor(n, o, 64), nn = n + nb;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < 2; ++e) {
         const float mb = __shfl_xor(mean[e], o, 64), m2b = __shfl_xor(m2[e], o, 64);
         if (nn > 0.f) {
           const float d = mb - mean[e];
@@ -529,12 +541,12 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
     }
     constexpr int NW = NT / 64;
     float* red = reinterpret_cast<float*>(smem);  // [NW][3][BN]
-    if (lane < CPR) {
+    if (lane < SPR) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        red[(wid * 3 + 0) * BN + cc * 8 + e] = n;
-        red[(wid * 3 + 1) * BN + cc * 8 + e] = mean[e];
-        red[(wid * 3 + 2) * BN + cc * 8 + e] = m2[e];
+      for (int e = 0; e < 2; ++e) {
+        red[(wid * 3 + 0) * BN + sp * 2 + e] = n;
+        red[(wid * 3 + 1) * BN + sp * 2 + e] = mean[e];
+        red[(wid * 3 + 2) * BN + sp * 2 + e] = m2[e];
       }
     }
     lds_barrier();

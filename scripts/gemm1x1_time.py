@@ -1,0 +1,56 @@
+#!/usr/bin/env python
+"""Register-staged 1x1 GEMM (conv1x1_gemm) per call at the ResNet-50 bs256 bottleneck conv3 shapes,
+plain / + BN statistics / + BN-apply prologue / + the prologue's side output (the pending-apply
+form the model runs), so the cost of each fused piece is visible.
+
+usage: python scripts/gemm1x1_time.py [--iters 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributeddataparallel_amd._native import load  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    C = load()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    # (K, N, H): conv3 of layer1..4 (planes -> 4 planes)
+    for K, N, H in [(64, 256, 56), (128, 512, 28), (256, 1024, 14), (512, 2048, 7)]:
+        x = torch.randn(256, K, H, H, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        w = (torch.randn(N, K, 1, 1, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+        ss = torch.cat([torch.rand(K, device="cuda", generator=g) + 0.5,
+                        torch.randn(K, device="cuda", generator=g) * 0.1]).contiguous()
+        out = torch.empty_like(x)
+        variants = {
+            "plain": lambda: C.conv1x1_gemm(x, w, 1, None, False),
+            "stats": lambda: C.conv1x1_gemm(x, w, 1, None, True),
+            "pro1+stats": lambda: C.conv1x1_gemm(x, w, 1, ss, True),
+            "pro1+stats+side": lambda: C.conv1x1_gemm(x, w, 1, ss, True, pro_out=out),
+        }
+        for name, fn in variants.items():
+            for _ in range(3):
+                fn()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            s.record()
+            for _ in range(a.iters):
+                fn()
+            e.record()
+            torch.cuda.synchronize()
+            us = s.elapsed_time(e) / a.iters * 1e3
+            M = 256 * H * H
+            print(json.dumps({"shape": f"M{M} K{K} N{N}", "variant": name, "us": round(us, 1),
+                              "tflops": round(2.0 * M * K * N / us / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
