@@ -400,13 +400,6 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
     }
 
     // ---- epilogue: round to bf16 (the stored values are what BN normalizes) ----
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = bf16_round(acc[i][j][r]);
-
     // ---- store Y through LDS: C tile [BM][BN] bf16, rows padded 16 B, then 16-B global stores ----
     // The MFMA computes the transposed tile (W rows as the first operand), so a lane's 4
     // accumulator values are 4 consecutive channels of one pixel row: one 8-B LDS store each
@@ -419,9 +412,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
       for (int j = 0; j < TN; ++j) {
         const int row = wm * WTM + i * 16 + (lane & 15);
         const int col = wn * WTN + j * 16 + (lane >> 4) * 4;
-        uint2 pk;  // exact: already bf16-rounded
-        pk.x = (__float_as_uint(acc[i][j][0]) >> 16) | (__float_as_uint(acc[i][j][1]) & 0xffff0000u);
-        pk.y = (__float_as_uint(acc[i][j][2]) >> 16) | (__float_as_uint(acc[i][j][3]) & 0xffff0000u);
+        uint2 pk;  // one v_cvt_pk_bf16_f32 (RNE) per channel pair
+        pk.x = dev::pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+        pk.y = dev::pack_bf16x2(acc[i][j][2], acc[i][j][3]);
         *reinterpret_cast<uint2*>(Cs + row * CST + col * 2) = pk;
       }
     lds_barrier();

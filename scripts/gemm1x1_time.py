@@ -19,11 +19,13 @@ from distributeddataparallel_amd._native import load  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", type=int, default=-1, help="run only this shape index")
     a = ap.parse_args()
     C = load()
     g = torch.Generator(device="cuda").manual_seed(5)
     # (K, N, H): conv3 of layer1..4 (planes -> 4 planes)
-    for K, N, H in [(64, 256, 56), (128, 512, 28), (256, 1024, 14), (512, 2048, 7)]:
+    shapes = [(64, 256, 56), (128, 512, 28), (256, 1024, 14), (512, 2048, 7)]
+    for K, N, H in (shapes if a.only < 0 else [shapes[a.only]]):
         x = torch.randn(256, K, H, H, device="cuda", generator=g).to(torch.bfloat16).contiguous(
             memory_format=torch.channels_last)
         w = (torch.randn(N, K, 1, 1, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
