@@ -54,5 +54,51 @@ def main():
                               "tflops": round(2.0 * M * K * N / us / 1e6, 1)}), flush=True)
 
 
+
+
+def epi_main():
+    """--epi: the input-gradient GEMM with the BN-reduce epilogue (EPI, form 1: + identity gradient,
+    ReLU mask bits, BN-backward partials) at the bottleneck conv1 shapes."""
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epi", action="store_true")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", type=int, default=-1)
+    a = ap.parse_args()
+    C = load()
+    g = torch.Generator(device="cuda").manual_seed(6)
+    # (planes K, in/out channels N, H)
+    shapes = [(64, 256, 56), (128, 512, 28), (256, 1024, 14), (512, 2048, 7)]
+    for K, N, H in (shapes if a.only < 0 else [shapes[a.only]]):
+        bf = dict(device="cuda", dtype=torch.bfloat16)
+        dy = torch.randn(256, K, H, H, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        w = (torch.randn(K, N, 1, 1, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+        add = torch.randn(256, N, H, H, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        y = torch.randn(256, N, H, H, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        bits = torch.randint(0, 255, (y.numel() // 8,), device="cuda", dtype=torch.uint8, generator=g)
+        mean = torch.randn(N, device="cuda", generator=g)
+        del bf
+
+        def fn():
+            return C.conv1x1_gemm(dy, w, 1, None, False, None, True, add, y, bits, mean, None, 1)
+
+        for _ in range(3):
+            fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(a.iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) / a.iters * 1e3
+        M = 256 * H * H
+        gb = (M * K + 3 * M * N) * 2 / 1e9 + M * N / 8 / 1e9
+        print(json.dumps({"shape": f"EPI M{M} K{K} N{N}", "us": round(us, 1), "TBps": round(gb / us * 1e3, 2),
+                          "tflops": round(2.0 * M * K * N / us / 1e6, 1)}), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    epi_main() if "--epi" in sys.argv else main()
