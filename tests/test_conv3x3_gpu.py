@@ -134,6 +134,8 @@ def test_conv3x3_bn_relu_forward_backward(stride):
     (1, 64, 16, 16, 128, 2),    # strided, N = 128 over a 64-channel input
     (1, 512, 7, 7, 512, 1),     # one partial patch per image, 64 tiles
     (4, 64, 56, 56, 64, 1),     # ResNet-50 layer1 shape (reduced batch): many splits
+    (2, 64, 12, 20, 64, 1),     # non-square, partial last patch column
+    (2, 128, 28, 28, 128, 1),   # layer2 shape (reduced batch)
 ])
 def test_conv3x3_wgrad_patch_matches_conv2d(b, cin, h, w, cout, s):
     """8x8-patch 3x3 weight gradient (csrc/kernels/conv3x3_wgrad.hip) vs fp32 PyTorch."""
