@@ -602,7 +602,7 @@ std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w
 // 1x1 conv (stride 1 or 2) on the 3-stage LDS-DMA pipeline: x [B, C, IH, IW] bf16 channels_last,
 // w [N, C, 1, 1] bf16; returns {y channels_last, stats partials [3, N, mtiles] group-minor}.
 // Tiles: 256x128 (8 waves, 1 block/CU) when that still gives >= 2 blocks per CU, else 128x64
-// (4 waves, 2 blocks/CU); tile (or XDDP_C1_TILE) = 0 | 4 forces one.
+// (4 waves, 2 blocks/CU); tile = 0 | 4 forces one (tests).
 std::vector<at::Tensor> conv1x1_dma_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats,
                                             int64_t tile) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&

@@ -115,7 +115,7 @@ struct RowMap {  // output pixel m -> input row (strided 1x1 conv reads every st
 // the transposing ds_read_b64_tr_b16, so no transposed weight copy is made.
 // OCC: waves per SIMD the register budget is sized for. 4 (default) = two 8-wave blocks per CU
 // within 128 VGPRs (some variants spill a few registers to scratch); 2 = one block per CU with up
-// to 256 VGPRs and no spills (XDDP_GEMM_OCC=2; the persistent grid shrinks to one block per CU).
+// to 256 VGPRs and no spills (the persistent grid shrinks to one block per CU; the host picks it).
 template <int BM, int BN, int WM, int WN, int PRO, bool STATS, bool STRIDED, bool BT = false, bool EPI = false,
           int OCC = 4>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
