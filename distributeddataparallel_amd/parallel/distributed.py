@@ -759,7 +759,8 @@ class DistributedDataParallel(nn.Module, Joinable):
             tail_chunk_bytes = int(float(os.environ.get("XDDP_TAIL_CHUNK_MB", "64")) * (1 << 20))
         side = torch.cuda.Stream(self._param_device) if self.device_type == "cuda" else None
         state = {"opt": optimizer, "side": side, "queued": False, "ddp": weakref.ref(self), "deferred": [],
-                 "schedule": schedule, "chunk_bytes": max(1 << 16, int(tail_chunk_bytes)), "last_chunks": 0}
+                 "schedule": schedule, "chunk_bytes": max(1 << 16, int(tail_chunk_bytes)), "last_chunks": 0,
+                 "pairs": []}
         self._overlap_state = state
 
         def run_side(fn):
@@ -784,6 +785,16 @@ class DistributedDataParallel(nn.Module, Joinable):
                 run_side(flush_deferred)
             if side is not None:
                 torch.cuda.current_stream(side.device).wait_stream(side)
+            # The hook hands the reducer an already-completed future (the collectives are still in
+            # flight on the comm stream), so without bucket views the reducer's own copy of the
+            # bucket into .grad may read the buffer before the all-reduce lands: copy the reduced
+            # bucket views into .grad again, ordered after the side stream (which waited for every
+            # collective).
+            pairs, state["pairs"] = state["pairs"], []
+            with torch.no_grad():
+                for p, g in pairs:
+                    if p.grad is not None and p.grad.data_ptr() != g.data_ptr():
+                        p.grad.copy_(g.view_as(p.grad) if g.shape != p.grad.shape else g)
 
         def done(buf):
             fut = torch.futures.Future()
@@ -797,6 +808,8 @@ class DistributedDataParallel(nn.Module, Joinable):
             if not st["queued"]:
                 st["queued"] = True
                 torch.autograd.Variable._execution_engine.queue_callback(join)
+            if not ddp.gradient_as_bucket_view:
+                st["pairs"].extend(zip(bucket.parameters(), bucket.gradients()))
             if st["schedule"] == "backward":
                 work = pg.allreduce(buf, xdist.ReduceOp.AVG)
                 st["deferred"].append((work, bucket.parameters(), bucket.gradients()))

@@ -436,6 +436,9 @@ def _w_overlapped_optimizer(rank, world, schedule):
         F.cross_entropy(d1(x), y).backward()  # updated inside backward
         o2.zero_grad()
         F.cross_entropy(d2(x), y).backward()
+        # .grad after the overlapped backward holds the reduced gradient, as with plain DDP
+        for p1, p2 in zip(m1.parameters(), m2.parameters()):
+            assert torch.equal(p1.grad, p2.grad)
         o2.step()
     pg.allreduce, o1.step_slices = orig_ar, orig_slices
     _assert_params_equal(m1, m2, rtol=0, atol=0)  # bitwise: same all-reduce sums, elementwise AdamW

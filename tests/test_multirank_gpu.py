@@ -127,6 +127,62 @@ print("forced-launch ok", n)
     assert r.returncode == 0 and "forced-launch ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
+@pytest.mark.parametrize("schedule,grad_as_view", [("tail", False), ("tail", True), ("backward", False)])
+def test_rccl_forced_launch_overlapped_optimizer(schedule, grad_as_view):
+    """W=1 with real RCCL kernels on the comm stream (XDDP_RCCL_FORCE_LAUNCH=1): the overlapped
+    optimizer (deferred updates under a chunked tail all-reduce, or per-bucket updates during
+    backward) trains bitwise like backward-then-step, and .grad holds the reduced gradient after
+    backward also without bucket views (the hook hands the reducer a completed future while the
+    collectives are still in flight)."""
+    import subprocess
+    import sys
+
+    code = r'''
+import os, sys, torch, torch.nn.functional as F
+import distributeddataparallel_amd as xddp
+from distributeddataparallel_amd import distributed as dist
+from distributeddataparallel_amd.models.llama import llama_tiny
+from distributeddataparallel_amd.optim import FusedAdamW
+from distributeddataparallel_amd.utils.spawn import free_port
+schedule, view = sys.argv[1], sys.argv[2] == "1"
+os.environ["MASTER_ADDR"] = "127.0.0.1"; os.environ["MASTER_PORT"] = str(free_port())
+pg = dist.init_process_group("rccl", rank=0, world_size=1, device_id=0)
+def make():  # a 2048 x 64 token embedding: the tail bucket is >= 4 chunks of 64 KB
+    torch.manual_seed(0)
+    return llama_tiny(max_seq_len=64, vocab_size=2048).cuda().to(torch.bfloat16)
+m1, m2 = make(), make()
+d1 = xddp.DDP(m1, device_ids=[0], gradient_as_bucket_view=view, bucket_cap_mb=0.25)
+d2 = xddp.DDP(m2, device_ids=[0], gradient_as_bucket_view=view, bucket_cap_mb=0.25)
+o1 = FusedAdamW(m1.parameters(), lr=1e-3, weight_decay=0.1, master_weights=True)
+o2 = FusedAdamW(m2.parameters(), lr=1e-3, weight_decay=0.1, master_weights=True)
+d1.register_overlapped_optimizer(o1, schedule=schedule, tail_chunk_bytes=1 << 16)
+vocab = m1.tok_embeddings.weight.shape[0] if hasattr(m1, "tok_embeddings") else 256
+g = torch.Generator(device="cuda").manual_seed(1)
+for it in range(3):
+    x = torch.randint(0, vocab, (2, 64), device="cuda", generator=g)
+    y = torch.randint(0, vocab, (2, 64), device="cuda", generator=g)
+    o1.zero_grad(set_to_none=False); o2.zero_grad(set_to_none=False)
+    out = d1(x); F.cross_entropy(out.float().view(-1, out.shape[-1]), y.view(-1)).backward()
+    out = d2(x); F.cross_entropy(out.float().view(-1, out.shape[-1]), y.view(-1)).backward()
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        assert torch.equal(a.grad, b.grad), it
+    o2.step()
+torch.cuda.synchronize()
+for a, b in zip(m1.parameters(), m2.parameters()):
+    assert torch.equal(a, b)
+if schedule == "tail":
+    assert d1._overlap_state["last_chunks"] >= 2, d1._overlap_state["last_chunks"]
+n = pg.comm.num_collectives()
+dist.destroy_process_group()
+print("overlap forced-launch ok", n)
+'''
+    env = dict(os.environ, XDDP_RCCL_FORCE_LAUNCH="1")
+    r = subprocess.run([sys.executable, "-c", code, schedule, "1" if grad_as_view else "0"], env=env,
+                       capture_output=True, text=True, timeout=240,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "overlap forced-launch ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
 @pytest.mark.parametrize("grad_as_view,accum", [(True, 1), (False, 2)])
 def test_two_ranks_one_gpu_ddp_parity_peer_backend(grad_as_view, accum, monkeypatch):
     """The same W=2 DDP parity on the RCCL-free peer-memory backend: bucket all-reduces, the
