@@ -139,9 +139,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
   const int lc = tid & 7, lr = tid >> 3;  // staging: 16-B chunk (8 k) and first row of this thread
   const int nk = K / kBK;
 
-  // Statistics are gathered by the C-tile readout: each thread stores a fixed 8-channel chunk
-  // column (cc) of the tiles it visits, and keeps shifted sums of those 8 channels. The shift is
-  // the block's first output row (a sample of the same channel: no cancellation when
+  // The C-tile readout: each thread stores a fixed 8-channel chunk column (cc) of the tiles it
+  // visits (EPI: and keeps that column's BN-backward sums). Statistics (STATS) are shifted sums,
+  // the shift a sample of the same channel (the block's first stored row: no cancellation when
   // |mean| >> std), so partials across tiles simply add; threads merge once, at the end.
   constexpr int CPR = BN / 8;                         // 16-B chunks per C-tile row
   static_assert(NT % CPR == 0, "readout mapping needs a fixed chunk column per thread");
