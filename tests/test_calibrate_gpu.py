@@ -90,3 +90,68 @@ def test_calibration_rccl_communicator_one_rank(corrupt):
     if corrupt:
         env["XDDP_CALIBRATE_CORRUPT_RANK"] = "0"
     run_ranks(_w_calibrate_rccl_one_rank, world=1, backend="rccl", args=(corrupt,), env=env)
+
+
+def _w_rccl_mixed_routes_ddp(rank, world):
+    """DDP buckets on a route table that mixes the peer kernels with RCCL (W = 1, forced RCCL
+    launches, the peer lanes of the calibration): small buckets take the two-shot kernel, large
+    ones the RCCL ring; gradients stay bitwise those of the plain model (AVG over one rank) for
+    several iterations. Then a coalesced burst mixing both routes (at W > 1 the bucket bursts at
+    the end of backward are one RCCL group): a peer launch inside the group closes it (the group's
+    pending RCCL kernels go out first) and reopens it at the same depth (RcclComm::launch_peer)."""
+    import torch.nn.functional as F
+
+    import distributeddataparallel_amd as xddp
+    from distributeddataparallel_amd import distributed as xdist
+    from distributeddataparallel_amd.distributed import calibrate as cal
+    from distributeddataparallel_amd.models import SimpleCNN
+    from distributeddataparallel_amd.parallel import bucket_policy as bp
+
+    pg = xdist.get_default_group()
+    try:
+        rep = cal.calibrate(pg, [64 << 10, MiB], torch.float32, iters=2)
+        assert rep["self_check"]["ok"], rep
+        pg.comm.set_route_table([3 << 19, 1 << 62], [3, 1])  # <= 1.5 MiB: two-shot, larger: RCCL
+        torch.backends.cudnn.deterministic = True
+        torch.manual_seed(0)
+        model, ref = SimpleCNN().cuda(), SimpleCNN().cuda()
+        ddp = xddp.DDP(model, device_ids=[0], bucket_cap_mb=1, first_bucket_cap_mb=0.1)
+        for it in range(4):
+            ref.load_state_dict(model.state_dict())
+            x = torch.randn(16, 3, 32, 32, device="cuda")
+            y = torch.randint(0, 10, (16,), device="cuda")
+            model.zero_grad(set_to_none=True)
+            ref.zero_grad(set_to_none=True)
+            F.cross_entropy(ddp(x), y).backward()
+            F.cross_entropy(ref(x), y).backward()
+            for p, q in zip(model.parameters(), ref.parameters()):
+                assert torch.equal(p.grad, q.grad), it
+            with torch.no_grad():
+                for p in model.parameters():
+                    p.sub_(0.01 * p.grad)
+        torch.cuda.synchronize()
+        sizes = ddp.reducer.bucket_sizes_bytes()  # (after the iteration-0 rebuild)
+        assert min(sizes) <= 3 << 19 < max(sizes), sizes  # both routes in use
+        ops = [r["op"] for r in pg.flight_records()]
+        assert "allreduce_two_shot" in ops and "allreduce" in ops, sorted(set(ops))
+        # a coalesced burst mixing both routes (what a bucket burst at the end of backward issues at
+        # W > 1): RCCL / two-shot / RCCL / two-shot inside one group, nested one level deeper too
+        xs = [torch.arange(n, device="cuda", dtype=torch.float32) for n in (700_000, 1000, 600_000, 70_000)]
+        with xdist.coalescing(pg):
+            for x in xs[:2]:
+                pg.allreduce(x, xdist.ReduceOp.SUM)
+            with xdist.coalescing(pg):
+                for x in xs[2:]:
+                    pg.allreduce(x, xdist.ReduceOp.SUM)
+        torch.cuda.synchronize()
+        for x in xs:
+            assert torch.equal(x, torch.arange(x.numel(), device="cuda", dtype=torch.float32))
+        ops = [r["op"] for r in pg.flight_records()][-4:]
+        assert ops.count("allreduce_two_shot") == 2, ops
+    finally:
+        bp.clear_calibration()
+
+
+def test_rccl_mixed_peer_and_ring_routes_in_ddp_bucket_groups():
+    env = {"XDDP_RCCL_FORCE_LAUNCH": "1", "XDDP_PEER_ALLREDUCE": "auto", "XDDP_CALIBRATE_ONE_RANK": "1"}
+    run_ranks(_w_rccl_mixed_routes_ddp, world=1, backend="rccl", env=env)
