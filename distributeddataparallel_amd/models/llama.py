@@ -18,7 +18,7 @@ import torch.nn.functional as F
 
 from ..ops.attention import flash_attention
 from ..ops.layer_norm import FusedRMSNorm
-from ..ops.linear import linear
+from ..ops.linear import linear, multi_linear
 from ..ops.transformer import rope, rope_reference, swiglu
 
 __all__ = ["LlamaConfig", "Llama", "llama3_8b", "llama_tiny"]
@@ -66,12 +66,14 @@ class Attention(nn.Module):
         rot = rope if _fused() else rope_reference
         # rotate in the projection's [B, S, H, Dh] layout, then move heads forward for attention
         if _fused():
-            # projections on the own GEMM (ops/linear.py); gfx950 flash attention in their
-            # [B, S, H, Dh] layout (GQA without materialised K/V repeats; output already in the
-            # o-projection's layout)
-            q = rot(linear(x, self.wq.weight).view(B, S, self.h, self.hd), cos, sin)
-            k = rot(linear(x, self.wk.weight).view(B, S, self.kvh, self.hd), cos, sin)
-            v = linear(x, self.wv.weight).view(B, S, self.kvh, self.hd)
+            # q / k / v from one input with their input gradient accumulated in GEMMs (ops/linear.py
+            # multi_linear); gfx950 flash attention in their [B, S, H, Dh] layout (GQA without
+            # materialised K/V repeats; output already in the o-projection's layout); the skip
+            # connection as the o-projection GEMM's beta = 1 operand
+            q, k, v = multi_linear(x, self.wq.weight, self.wk.weight, self.wv.weight)
+            q = rot(q.view(B, S, self.h, self.hd), cos, sin)
+            k = rot(k.view(B, S, self.kvh, self.hd), cos, sin)
+            v = v.view(B, S, self.kvh, self.hd)
             o = flash_attention(q, k, v, causal=True)
             return linear(o.reshape(B, S, -1), self.wo.weight, residual)
         q = rot(self.wq(x).view(B, S, self.h, self.hd), cos, sin)
@@ -96,7 +98,7 @@ class FeedForward(nn.Module):
 
     def forward(self, x, residual=None):
         if _fused():
-            return linear(swiglu(linear(x, self.w1.weight), linear(x, self.w3.weight)), self.w2.weight, residual)
+            return linear(swiglu(*multi_linear(x, self.w1.weight, self.w3.weight)), self.w2.weight, residual)
         out = self.w2(F.silu(self.w1(x)) * self.w3(x))
         return out if residual is None else residual + out
 

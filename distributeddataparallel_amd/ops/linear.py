@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from .._native import load
 
-__all__ = ["linear", "own_gemm_ok", "own_gemm_mode"]
+__all__ = ["linear", "multi_linear", "own_gemm_ok", "own_gemm_mode"]
 
 
 def own_gemm_mode() -> str:
@@ -71,10 +71,55 @@ class _Linear(torch.autograd.Function):
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``x·Wᵀ`` (+ ``residual``) — the own GEMM when the shapes allow it, else ``F.linear``."""
+    """``x·Wᵀ`` (+ ``residual``) — the own GEMM when the shapes allow it, else the library GEMM,
+    with the residual as its beta = 1 accumulate operand (``addmm``: one GEMM, one rounding, no
+    separate add pass over the residual stream)."""
     if own_gemm_ok(x, weight) and (residual is None or (residual.shape[:-1] == x.shape[:-1]
                                                         and residual.dtype == torch.bfloat16
                                                         and residual.is_contiguous())):
         return _Linear.apply(x, weight, residual)
-    y = F.linear(x, weight)
-    return y if residual is None else residual + y
+    if residual is None:
+        return F.linear(x, weight)
+    if residual.shape[:-1] != x.shape[:-1] or residual.dtype != x.dtype:
+        return residual + F.linear(x, weight)
+    shape = (*x.shape[:-1], weight.shape[0])
+    return torch.addmm(residual.reshape(-1, weight.shape[0]), x.reshape(-1, x.shape[-1]), weight.t()).view(shape)
+
+
+class _MultiLinear(torch.autograd.Function):
+    """``[x·W_iᵀ]`` for several weights over ONE input: the backward's ``dX = Σ dY_i·W_i`` is one
+    GEMM plus beta = 1 accumulating GEMMs into the same buffer (autograd would sum the per-output
+    input gradients with separate add passes: two per Llama block for q / k / v, one for w1 / w3)."""
+
+    @staticmethod
+    def forward(ctx, x, *weights):
+        x2 = x.reshape(-1, x.shape[-1])
+        ctx.save_for_backward(x2, *weights)
+        ctx.shape = x.shape
+        return tuple(torch.mm(x2, w.t()).view(*x.shape[:-1], w.shape[0]) for w in weights)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        x2, *weights = ctx.saved_tensors
+        dx = None
+        if ctx.needs_input_grad[0]:
+            for dy, w in zip(dys, weights):
+                if dy is None:
+                    continue
+                d2 = dy.reshape(-1, w.shape[0])
+                dx = torch.mm(d2, w) if dx is None else dx.addmm_(d2, w)
+            if dx is not None:
+                dx = dx.view(ctx.shape)
+        dws = [torch.mm(dy.reshape(-1, w.shape[0]).t(), x2) if dy is not None and ctx.needs_input_grad[1 + i] else None
+               for i, (dy, w) in enumerate(zip(dys, weights))]
+        return (dx, *dws)
+
+
+def multi_linear(x: torch.Tensor, *weights: torch.Tensor):
+    """``x·W_iᵀ`` for each weight (bias-free), the input gradient accumulated in GEMMs (see
+    :class:`_MultiLinear`); the own GEMM's path (``XDDP_OWN_GEMM=1``) keeps one :func:`linear` per
+    weight. ``XDDP_MULTI_LINEAR=0``: plain per-weight linears (A/B switch)."""
+    if os.environ.get("XDDP_MULTI_LINEAR", "1") == "0" or any(own_gemm_ok(x, w) for w in weights) or \
+            not all(w.dtype == x.dtype and w.dim() == 2 for w in weights):
+        return tuple(linear(x, w) for w in weights)
+    return _MultiLinear.apply(x, *weights)
