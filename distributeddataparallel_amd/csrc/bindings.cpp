@@ -346,6 +346,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("local_used_map", &Reducer::local_used_map)
       .def("bucket_indices", &Reducer::bucket_indices)
       .def("bucket_sizes_bytes", &Reducer::bucket_sizes_bytes)
+      .def("param_bucket_views", &Reducer::param_bucket_views)
       .def("grad_ready_order", &Reducer::grad_ready_order)
       .def("num_iterations", &Reducer::num_iterations)
       .def("finalized", &Reducer::finalized)

@@ -912,6 +912,17 @@ std::vector<std::vector<int64_t>> Reducer::bucket_indices() const {
   return r;
 }
 
+std::vector<at::Tensor> Reducer::param_bucket_views() const {
+  std::vector<at::Tensor> out(params_.size());
+  for (size_t v = 0; v < params_.size() && v < var_loc_.size(); ++v) {
+    const auto& loc = var_loc_[v];
+    if (loc.first < 0 || loc.first >= static_cast<int64_t>(buckets_.size())) continue;
+    const auto& bk = buckets_[loc.first];
+    if (loc.second >= 0 && loc.second < static_cast<int64_t>(bk.views.size())) out[v] = bk.views[loc.second];
+  }
+  return out;
+}
+
 std::vector<int64_t> Reducer::bucket_sizes_bytes() const {
   std::vector<int64_t> r;
   for (auto& bk : buckets_) {

@@ -112,6 +112,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   at::Tensor local_used_map() const { return local_used_.clone(); }
   std::vector<std::vector<int64_t>> bucket_indices() const;
   std::vector<int64_t> bucket_sizes_bytes() const;
+  // per parameter (constructor order): its view into its bucket's flat gradient buffer
+  std::vector<at::Tensor> param_bucket_views() const;
   std::vector<int64_t> grad_ready_order() const { return prev_ready_order_; }
   int64_t num_iterations() const { return num_iterations_; }
   bool finalized() const { return !require_finalize_; }

@@ -37,6 +37,7 @@ from torch.autograd.profiler import record_function
 
 from .. import distributed as xdist
 from .._native import load
+from ..ops import linear as _linear_ops
 from ..utils import fault as _fault
 from . import bucket_policy as _bp
 from .join import Join, Joinable, JoinHook
@@ -571,6 +572,11 @@ class DistributedDataParallel(nn.Module, Joinable):
             self.reducer.set_gradient_divide_factor(float(work._ones.item()))
         if torch.is_grad_enabled() and self.reducer.rebuild_buckets():
             logger.info("xddp: rebuilt buckets: %s", self.reducer.bucket_sizes_bytes())
+        if torch.is_grad_enabled() and self.gradient_as_bucket_view and self.device_type == "cuda" and \
+                self._comm_dtype is None and os.environ.get("XDDP_GRAD_TARGETS", "1") != "0":
+            # the library / multi-input linears write their weight gradients straight into these
+            # bucket views (ops/linear.py set_grad_targets): no per-step copy into the buckets
+            _linear_ops.set_grad_targets(self._module_parameters, self.reducer.param_bucket_views())
         if self._check_sync_bufs_pre_fwd():
             self._sync_buffers()
         if self._join_config.enable:

@@ -311,3 +311,57 @@ def test_overlapped_optimizer_matches_step_after_backward(pg):
     torch.cuda.synchronize()
     for a, b in zip(m1.parameters(), m2.parameters()):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+def test_grad_targets_write_weight_grads_into_buckets(pg):
+    """With gradient_as_bucket_view, the linears of ops/linear.py write their weight gradients
+    straight into the DDP bucket views (set_grad_targets): the gradients are bitwise those of the
+    plain model, the weights' .grad ARE their bucket views after backward (no copy into the
+    bucket), and a weight used twice in one forward still gets the sum of both uses."""
+    import copy
+
+    import torch.nn.functional as F
+
+    from distributeddataparallel_amd.models.llama import llama_tiny
+    from distributeddataparallel_amd.ops.linear import linear
+
+    class Twice(nn.Module):  # one weight, two uses: only the first may take the target
+        def __init__(self):
+            super().__init__()
+            self.lin = nn.Linear(64, 64, bias=False)
+
+        def forward(self, x):
+            return linear(linear(x, self.lin.weight), self.lin.weight, x).sum(1)
+
+    torch.manual_seed(0)
+    for make in (lambda: llama_tiny(max_seq_len=64).cuda().to(torch.bfloat16),
+                 lambda: Twice().cuda().to(torch.bfloat16)):
+        m = make()
+        ref = copy.deepcopy(m)
+        d = xddp.DDP(m, device_ids=[0], gradient_as_bucket_view=True, bucket_cap_mb=0.25)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        for it in range(3):
+            if isinstance(m, Twice):
+                x = torch.randn(4, 16, 64, device="cuda", generator=g).to(torch.bfloat16)
+                loss_of = lambda mod: mod(x).float().square().mean()  # noqa: E731
+            else:
+                x = torch.randint(0, 512, (2, 64), device="cuda", generator=g)
+                loss_of = lambda mod: F.cross_entropy(mod(x).float().view(-1, 512), x.view(-1))  # noqa: E731
+            for p in list(m.parameters()) + list(ref.parameters()):
+                p.grad = None
+            loss_of(d).backward()
+            loss_of(ref).backward()
+            for (n, a), b in zip(m.named_parameters(), ref.parameters()):
+                assert (a.grad is None) == (b.grad is None), n
+                if a.grad is not None:
+                    assert torch.equal(a.grad, b.grad), (it, n)
+            with torch.no_grad():
+                for a, b in zip(m.parameters(), ref.parameters()):
+                    if a.grad is not None:
+                        a.sub_(0.01 * a.grad)
+                        b.sub_(0.01 * b.grad)
+        views = d.reducer.param_bucket_views()
+        aliased = [n for (n, p), v in zip(m.named_parameters(), views)
+                   if p.grad is not None and v is not None and p.grad.data_ptr() == v.data_ptr()]
+        if not isinstance(m, Twice):
+            assert any("wq" in n for n in aliased) and any("w2" in n for n in aliased), aliased
