@@ -428,9 +428,16 @@ def main(argv=None):
               for _ in range(micro)]
         ys = [torch.randint(0, ncls, (B,), device=device, generator=g) for _ in range(micro)]
 
+    from distributeddataparallel_amd.ops.cross_entropy import cross_entropy as fused_xent
+
     def loss_fn(out, tgt):
         if is_lm(args):
-            return F.cross_entropy(out.float().view(-1, out.shape[-1]), tgt.view(-1))
+            # fp32 softmax cross-entropy over the bf16 logits without an fp32 copy of them
+            # (ops/cross_entropy.py; --impl torch keeps F.cross_entropy on the upcast logits)
+            flat, t = out.reshape(-1, out.shape[-1]), tgt.reshape(-1)
+            if args.impl == "xddp" and os.environ.get("XDDP_FUSED_XENT", "1") != "0":
+                return fused_xent(flat, t)
+            return F.cross_entropy(flat.float(), t)
         return F.cross_entropy(out.float(), tgt)
 
     graphed = None

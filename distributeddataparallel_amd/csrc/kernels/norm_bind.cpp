@@ -27,6 +27,10 @@ void bind_norm_kernels(py::module_& m) {
         py::arg("mean"), py::arg("invstd"), py::arg("need_dweight"), py::arg("fold_mean") = true);
   m.def("bn_backward_elem", &bn_backward_elem, py::arg("g"), py::arg("x"), py::arg("mean"), py::arg("coef"));
   m.def("bn_moments", &bn_moments, py::arg("x"));
+  m.def("cross_entropy_forward", &cross_entropy_forward, py::arg("logits"), py::arg("target"),
+        py::arg("ignore_index") = -100);
+  m.def("cross_entropy_backward", &cross_entropy_backward, py::arg("logits"), py::arg("target"), py::arg("lse"),
+        py::arg("gscale"), py::arg("ignore_index") = -100);
   m.def("bn_grad_partials", &bn_grad_partials, py::arg("dy"), py::arg("x"), py::arg("mean"));
   m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"));
   m.def("conv3x3_rot_weight", &conv3x3_rot_weight, py::arg("w"));
