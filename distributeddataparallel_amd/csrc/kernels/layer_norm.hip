@@ -106,6 +106,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
                                                      float* __restrict__ part, int64_t rows, int D,
                                                      const T* __restrict__ res) {
   constexpr int NP = RES ? 4 : 2;
+  constexpr bool DB = !RMS;  // RMSNorm has no beta: no Σdy partial (half the partial registers)
   __shared__ float red[kRowsPerBlock][64 * 8 * 2];  // one-vector-at-a-time fold buffer (two sums)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float dg[NV][8], db[NV][8], sr[RES ? NV : 1][8], so[RES ? NV : 1][8];
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
             const float xh = (a[k][j] - mean) * rstd;
             o[j] = rstd * (d[k][j] * gm[k][j] - m1 - xh * m2);
             dg[k][j] = fmaf(d[k][j], xh, dg[k][j]);
-            db[k][j] += d[k][j];
+            if (DB) db[k][j] += d[k][j];
           }
           if (RES) {
   #pragma unroll
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
             const float xh = (a[j] - mean) * rstd;
             o[j] = rstd * (d[j] * g[j] - m1 - xh * m2);
             dg[k][j] = fmaf(d[j], xh, dg[k][j]);
-            db[k][j] += d[j];
+            if (DB) db[k][j] += d[j];
           }
           if (RES) {
             float r[8];
@@ -260,7 +261,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   }
   if (!part) return;
   // fold the 4 waves' column partials, one vector slot (two sums) at a time
-  auto fold = [&](float (&pa)[NV][8], float (&pb)[NV][8], int k, int p0) {
+  auto fold = [&](float (&pa)[NV][8], float (&pb)[NV][8], int k, int p0, bool two) {
     const int c = (k * 64 + lane) * 8;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -279,15 +280,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
           b += red[q][lane * 16 + 8 + j];
         }
         pg[c + j] = a;
-        pg[D + c + j] = b;
+        if (two) pg[D + c + j] = b;
       }
     }
     __syncthreads();
   };
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    fold(dg, db, k, 0);
-    if constexpr (RES) fold(sr, so, k, 2);
+    fold(dg, db, k, 0, DB);
+    if constexpr (RES) fold(sr, so, k, 2, true);
   }
 }
 
@@ -437,7 +438,9 @@ std::vector<at::Tensor> ln_backward(const at::Tensor& dy_in, const at::Tensor& x
     (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
     return v > 0 ? v : 256;
   }();
-  const int grid_cap = nv <= 2 ? 2 * cus : 1024;
+  // (wide rows, Llama-3-8B's 4096: 512 blocks 33.5 us vs 1024 39.5 / 256 36.0 / 2048 39.2 us,
+  // scripts/ln_bwd_time.py — fewer column-partial folds and a smaller partial buffer)
+  const int grid_cap = 2 * cus;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((rows + kRowsPerBlock - 1) / kRowsPerBlock, grid_cap));
   auto part = need_part ? at::empty({grid, NP, D}, x.options().dtype(at::kFloat)) : at::Tensor();
   if (rows == 0) return {dx, dgamma, dbeta, sres, sout};
