@@ -517,6 +517,7 @@ class DistributedDataParallel(nn.Module, Joinable):
         idx, lims = C.compute_bucket_assignment_by_size(params, limits, expect_sparse)
         idx, lims = list(reversed(idx)), list(reversed(lims))
         cd = "" if self._comm_dtype is None else str(self._comm_dtype).replace("torch.", "")
+        self._grad_target_views = None  # (bucket views of the previous reducer, if any)
         self.reducer = C.Reducer(
             params, idx, lims, self.process_group.comm,
             find_unused_parameters=self.find_unused_parameters,
@@ -570,13 +571,18 @@ class DistributedDataParallel(nn.Module, Joinable):
         if work is not None and not self._divide_by_initial_world_size:
             work.wait()
             self.reducer.set_gradient_divide_factor(float(work._ones.item()))
-        if torch.is_grad_enabled() and self.reducer.rebuild_buckets():
+        rebuilt = torch.is_grad_enabled() and self.reducer.rebuild_buckets()
+        if rebuilt:
             logger.info("xddp: rebuilt buckets: %s", self.reducer.bucket_sizes_bytes())
         if torch.is_grad_enabled() and self.gradient_as_bucket_view and self.device_type == "cuda" and \
                 self._comm_dtype is None and os.environ.get("XDDP_GRAD_TARGETS", "1") != "0":
             # the library / multi-input linears write their weight gradients straight into these
-            # bucket views (ops/linear.py set_grad_targets): no per-step copy into the buckets
-            _linear_ops.set_grad_targets(self._module_parameters, self.reducer.param_bucket_views())
+            # bucket views (ops/linear.py set_grad_targets): no per-step copy into the buckets. A
+            # registration is claimed by one backward, so it is renewed every forward; the views
+            # themselves only change when the buckets are rebuilt.
+            if rebuilt or getattr(self, "_grad_target_views", None) is None:
+                self._grad_target_views = self.reducer.param_bucket_views()
+            _linear_ops.set_grad_targets(self._module_parameters, self._grad_target_views)
         if self._check_sync_bufs_pre_fwd():
             self._sync_buffers()
         if self._join_config.enable:
@@ -905,6 +911,7 @@ class DistributedDataParallel(nn.Module, Joinable):
         attrs = copy.copy(self.__dict__)
         del attrs["process_group"]
         del attrs["reducer"]
+        attrs.pop("_grad_target_views", None)  # views into this process's buckets
         attrs["_comm_hooks"] = []
         attrs["_accum_grad_hooks"] = []
         return attrs
