@@ -99,22 +99,24 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 // disappears), and two more column partials: Σ res and Σ dx — the bias gradients of the linear
 // layers whose outputs fed the residual sums after and before this norm. NP = RES ? 4 : 2.
 // With RES the narrow-row loop prefetches res with the next row's x / dy (RPF).
-template <typename T, typename W, int NV, bool RMS, bool RES, bool RPF = RES>
+// SUMS (LayerNorm's residual form): the Σ res / Σ dx column partials; RMSNorm's residual form
+// (Llama's pre-norm blocks: the skip connection's gradient) only adds res to dx.
+template <typename T, typename W, int NV, bool RMS, bool RES, bool RPF = RES, bool SUMS = RES>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const W* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, T* __restrict__ dx,
                                                      float* __restrict__ part, int64_t rows, int D,
                                                      const T* __restrict__ res) {
-  constexpr int NP = RES ? 4 : 2;
+  constexpr int NP = SUMS ? 4 : 2;
   constexpr bool DB = !RMS;  // RMSNorm has no beta: no Σdy partial (half the partial registers)
   __shared__ float red[kRowsPerBlock][64 * 8 * 2];  // one-vector-at-a-time fold buffer (two sums)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float dg[NV][8], db[NV][8], sr[RES ? NV : 1][8], so[RES ? NV : 1][8];
+  float dg[NV][8], db[NV][8], sr[SUMS ? NV : 1][8], so[SUMS ? NV : 1][8];
 #pragma unroll
   for (int k = 0; k < NV; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) dg[k][j] = db[k][j] = 0.f;
-  if (RES) {
+  if (SUMS) {
 #pragma unroll
     for (int k = 0; k < NV; ++k)
 #pragma unroll
@@ -187,8 +189,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   #pragma unroll
             for (int j = 0; j < 8; ++j) {
               o[j] += rv[RPF ? k : 0][j];
-              sr[RES ? k : 0][j] += rv[RPF ? k : 0][j];
-              so[RES ? k : 0][j] += o[j];
+              if (SUMS) {
+                sr[SUMS ? k : 0][j] += rv[RPF ? k : 0][j];
+                so[SUMS ? k : 0][j] += o[j];
+              }
             }
           }
           Vec8<T>::st(dx + row * D + c, o);
@@ -250,8 +254,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   #pragma unroll
             for (int j = 0; j < 8; ++j) {
               o[j] += r[j];
-              sr[RES ? k : 0][j] += r[j];
-              so[RES ? k : 0][j] += o[j];
+              if (SUMS) {
+                sr[SUMS ? k : 0][j] += r[j];
+                so[SUMS ? k : 0][j] += o[j];
+              }
             }
           }
           Vec8<T>::st(dx + row * D + c, o);
@@ -288,7 +294,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     fold(dg, db, k, 0, DB);
-    if constexpr (RES) fold(sr, so, k, 2, true);
+    if constexpr (SUMS) fold(sr, so, k, 2, true);
   }
 }
 
@@ -401,7 +407,8 @@ std::vector<at::Tensor> ln_forward(const at::Tensor& x_in, const c10::optional<a
   return {y, mean, rstd, xb};
 }
 
-// returns (dx, dgamma, dbeta, Σ res, Σ dx); with res: dx = LN backward + res (the last two only then)
+// returns (dx, dgamma, dbeta, Σ res, Σ dx); with res: dx = LN backward + res (the last two only then,
+// LayerNorm only)
 std::vector<at::Tensor> ln_backward(const at::Tensor& dy_in, const at::Tensor& x_in,
                                     const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& mean,
                                     const at::Tensor& rstd, bool rms, bool need_dgamma, bool need_dbeta,
@@ -413,7 +420,6 @@ std::vector<at::Tensor> ln_backward(const at::Tensor& dy_in, const at::Tensor& x
   auto dx = at::empty_like(x);
   const bool hg = gamma.has_value() && gamma->defined();
   const bool hr = res_in.has_value() && res_in->defined();
-  TORCH_CHECK(!hr || !rms, "xddp layer_norm backward: the residual form is LayerNorm-only");
   at::Tensor res;
   if (hr) {
     res = res_in->contiguous();
@@ -424,11 +430,12 @@ std::vector<at::Tensor> ln_backward(const at::Tensor& dy_in, const at::Tensor& x
   auto wopt = hg ? gamma->options() : x.options();
   at::Tensor dgamma = (hg && need_dgamma) ? at::empty({D}, wopt) : at::Tensor();
   at::Tensor dbeta = (need_dbeta && !rms) ? at::empty({D}, wopt) : at::Tensor();
-  at::Tensor sres = hr ? at::empty({D}, wopt) : at::Tensor(), sout = hr ? at::empty({D}, wopt) : at::Tensor();
+  const bool sums = hr && !rms;  // (RMSNorm's residual form: dx += res only)
+  at::Tensor sres = sums ? at::empty({D}, wopt) : at::Tensor(), sout = sums ? at::empty({D}, wopt) : at::Tensor();
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
   const int nv = (D / 8 + 63) / 64;
-  const bool need_part = dgamma.defined() || dbeta.defined() || hr;
-  const int NP = hr ? 4 : 2;
+  const bool need_part = dgamma.defined() || dbeta.defined() || sums;
+  const int NP = sums ? 4 : 2;
   // Block cap: the narrow-row (software-pipelined) loop runs at 2 waves per SIMD, so 512 blocks are
   // exactly one resident round on 256 CUs (ViT-L/16 rows: 107 -> 100 us with the residual form,
   // 96 -> 90 without, vs 1024 blocks; 2048 / 4096 were slower still: profiles/r3_ln_bwd_ab.txt).
@@ -450,7 +457,7 @@ std::vector<at::Tensor> ln_backward(const at::Tensor& dy_in, const at::Tensor& x
       using W = decltype(tw);
       nv_dispatch<1>(nv, [&](auto nvc) {
         constexpr int NV = decltype(nvc)::value;
-        auto k = rms ? ln_bwd_kernel<T, W, NV, true, false>
+        auto k = rms ? (hr ? ln_bwd_kernel<T, W, NV, true, true, true, false> : ln_bwd_kernel<T, W, NV, true, false>)
                      : (hr ? ln_bwd_kernel<T, W, NV, false, true> : ln_bwd_kernel<T, W, NV, false, false>);
         hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, stream, reinterpret_cast<const T*>(dy.data_ptr()),
                            reinterpret_cast<const T*>(x.data_ptr()),

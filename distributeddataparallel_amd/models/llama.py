@@ -112,6 +112,13 @@ class Block(nn.Module):
         self.feed_forward = FeedForward(cfg)
 
     def forward(self, x, cos, sin):
+        if _fused() and os.environ.get("XDDP_NORM_SKIP", "1") != "0":
+            # each norm's input is also the skip connection: its gradient is summed in the norm's
+            # backward kernel (ops/layer_norm.py rms_norm_with_skip), not by an add pass
+            y, skip = self.attention_norm.forward_with_skip(x)
+            x = self.attention(y, cos, sin, residual=skip)
+            y, skip = self.ffn_norm.forward_with_skip(x)
+            return self.feed_forward(y, residual=skip)
         x = self.attention(self.attention_norm(x), cos, sin, residual=x)
         return self.feed_forward(self.ffn_norm(x), residual=x)
 

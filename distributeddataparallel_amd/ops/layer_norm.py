@@ -12,7 +12,7 @@ import torch.nn.functional as F
 
 from .._native import load
 
-__all__ = ["FusedLayerNorm", "FusedRMSNorm", "layer_norm", "rms_norm"]
+__all__ = ["FusedLayerNorm", "FusedRMSNorm", "layer_norm", "rms_norm", "rms_norm_with_skip"]
 
 
 class _LN(torch.autograd.Function):
@@ -34,6 +34,43 @@ class _LN(torch.autograd.Function):
         dx, dg, db, _, _ = C.ln_backward(dy.reshape(x2.shape), x2, weight, mean, rstd, ctx.rms,
                                    ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         return dx.view(ctx.shape), dg, (db if not ctx.rms else None), None, None
+
+
+class _RMSSkip(torch.autograd.Function):
+    """RMSNorm whose input is also the block's skip connection: returns (y, skip), skip an alias of
+    x. Autograd hands this node both gradients at once, so the skip connection's gradient is added
+    inside the norm's backward kernel (``ln_backward(..., res=)``) instead of by a separate add
+    pass over the residual stream (two per Llama block)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, eps):
+        C = load()
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        y, _, rstd, _ = C.ln_forward(x2, weight, None, eps, True)
+        ctx.save_for_backward(x2, weight, rstd)
+        ctx.shape = shape
+        return y.view(shape), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dskip):
+        C = load()
+        x2, weight, rstd = ctx.saved_tensors
+        if dy is None:
+            return dskip, None, None
+        res = dskip.reshape(x2.shape) if dskip is not None else None
+        dx, dg, _, _, _ = C.ln_backward(dy.reshape(x2.shape), x2, weight, None, rstd, True,
+                                        ctx.needs_input_grad[1], False, res)
+        return dx.view(ctx.shape), dg, None
+
+
+def rms_norm_with_skip(x, normalized_shape, weight=None, eps=1e-6):
+    """``(rms_norm(x), x)`` for a pre-norm block whose skip connection is ``x``: on the fused path
+    the skip's gradient is summed inside the norm's backward (see :class:`_RMSSkip`)."""
+    d = x.shape[-1]
+    if len(normalized_shape) == 1 and _ok(x, d) and weight is not None and x.dtype == weight.dtype:
+        return _RMSSkip.apply(x, weight, float(eps))
+    return rms_norm(x, normalized_shape, weight, eps), x
 
 
 def _ok(x, d):
@@ -73,6 +110,10 @@ class FusedRMSNorm(nn.Module):
 
     def forward(self, x):
         return rms_norm(x, self.normalized_shape, self.weight, self.eps)
+
+    def forward_with_skip(self, x):
+        """``(self(x), x)`` with the skip connection's gradient added in this norm's backward."""
+        return rms_norm_with_skip(x, self.normalized_shape, self.weight, self.eps)
 
     def extra_repr(self):
         return f"{self.normalized_shape}, eps={self.eps}"

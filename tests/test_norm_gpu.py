@@ -221,3 +221,33 @@ def test_global_avg_pool_backward_kernel(dt):
     y2.backward(g)
     assert x.grad.is_contiguous(memory_format=torch.channels_last)
     torch.testing.assert_close(x.grad.float(), x2.grad.float(), rtol=1e-2 if dt == torch.bfloat16 else 1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("D", [4096, 1024, 64])
+def test_rms_norm_with_skip_matches_separate_add(D):
+    """rms_norm_with_skip: (y, skip) with the skip connection's gradient summed inside the RMSNorm
+    backward kernel (ln_backward res=) == rms_norm(x) + x composed by autograd (one add pass)."""
+    from distributeddataparallel_amd.ops.layer_norm import rms_norm, rms_norm_with_skip
+
+    torch.manual_seed(3)
+    x0 = torch.randn(4, 33, D, device="cuda").to(torch.bfloat16)
+    w0 = (torch.rand(D, device="cuda") + 0.5).to(torch.bfloat16)
+    lin = (torch.randn(D, D, device="cuda") / D ** 0.5).to(torch.bfloat16)
+    g = torch.randn(4, 33, D, device="cuda").to(torch.bfloat16)
+
+    def run(fused):
+        x = x0.clone().requires_grad_(True)
+        w = w0.clone().requires_grad_(True)
+        if fused:
+            y, skip = rms_norm_with_skip(x, (D,), w, 1e-5)
+        else:
+            y, skip = rms_norm(x, (D,), w, 1e-5), x
+        out = skip + y @ lin
+        out.backward(g)
+        return out, x.grad, w.grad
+
+    o1, dx1, dw1 = run(True)
+    o2, dx2, dw2 = run(False)
+    assert torch.equal(o1, o2)
+    torch.testing.assert_close(dx1.float(), dx2.float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(dw1.float(), dw2.float(), rtol=2e-2, atol=2e-2 * dw2.abs().max().item())
