@@ -29,7 +29,7 @@ import os
 import torch
 
 from .._native import load
-from .linear import own_gemm_mode
+from .linear import _dw, own_gemm_mode
 
 __all__ = ["encoder_block", "encoder_block_supported"]
 
@@ -82,6 +82,7 @@ class _EncoderBlockFn(torch.autograd.Function):
         ctx.save_for_backward(x2, ln1_w, mean1, rstd1, y1, w_qkv, b_qkv, qkv, o, lse, w_o, b_o, x1, ln2_w, mean2,
                               rstd2, y2, w_1, b_1, h, a, w_2, b_2)
         ctx.shape, ctx.heads, ctx.scale = (B, S, D), heads, scale
+        ctx.params = (w_qkv, w_o, w_1, w_2)  # (the parameter objects: their registered gradient targets)
         return out.view(B, S, D)
 
     @staticmethod
@@ -98,21 +99,23 @@ class _EncoderBlockFn(torch.autograd.Function):
             dhid, db_1 = C.gemm_nt(g2, w_2t, b_1, 4, h)
         else:
             db_1, dhid = C.bias_grad(torch.mm(g2, w_2), h, b_1)
-        dw_2 = torch.mm(g2.t(), a)
+        p_qkv, p_o, p_1, p_2 = ctx.params
+        # weight gradients straight into the DDP bucket views when registered (ops/linear.py _dw)
+        dw_2 = _dw(g2, a, p_2)
         dy2 = torch.mm(dhid, w_1)
-        dw_1 = torch.mm(dhid.t(), y2)
+        dw_1 = _dw(dhid, y2, p_1)
         # LN2 + residual: g1 = g2 + LN2ᵀ(dy2); Σ g2 = fc2's bias grad, Σ g1 = the out projection's
         g1, dln2_w, dln2_b, db_2, db_o = C.ln_backward(dy2, x1, ln2_w, mean2, rstd2, False, True, True, g2)
         # attention
         do = torch.mm(g1, w_o)
-        dw_o = torch.mm(g1.t(), o.view(-1, D))
+        dw_o = _dw(g1, o.view(-1, D), p_o)
         dqkv = torch.empty_like(qkv)
         d5, q5 = dqkv.view(B, S, 3, heads, dh), qkv.view(B, S, 3, heads, dh)
         C.flash_attn_backward(do.view(B, S, heads, dh), q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, lse, False,
                               ctx.scale, d5[:, :, 0], d5[:, :, 1], d5[:, :, 2])
         db_qkv, _ = C.bias_grad(dqkv, None, b_qkv)
         dy1 = torch.mm(dqkv, w_qkv)
-        dw_qkv = torch.mm(dqkv.t(), y1)
+        dw_qkv = _dw(dqkv.view(-1, 3 * D), y1, p_qkv)
         # LN1 + residual: dx = g1 + LN1ᵀ(dy1)
         dx, dln1_w, dln1_b, _, _ = C.ln_backward(dy1, x2, ln1_w, mean1, rstd1, False, True, True, g1)
         return (dx.view(B, S, D), dln1_w, dln1_b, dw_qkv, db_qkv, dw_o, db_o, dln2_w, dln2_b, dw_1, db_1, dw_2, db_2,
