@@ -271,7 +271,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("make_py_comm", &make_py_comm, py::arg("impl"), py::arg("rank"), py::arg("size"),
         py::arg("name") = "torch");
   m.def("make_debug_comm", &make_debug_comm, py::arg("inner"), py::arg("fingerprint") = true,
-        py::arg("nan_check") = false);
+        py::arg("nan_check") = false, py::arg("helper") = nullptr);
   m.def("rccl_version", &rccl_version);
   m.def("rccl_stream_handle", &rccl_stream_handle);
 

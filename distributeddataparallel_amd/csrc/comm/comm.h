@@ -207,8 +207,10 @@ std::shared_ptr<Comm> make_rccl_comm(std::shared_ptr<Store> store, int rank, int
 std::shared_ptr<Comm> make_peer_comm(std::shared_ptr<Store> store, int rank, int size, int device, int64_t capacity,
                                      int64_t two_shot_capacity, std::chrono::milliseconds timeout);
 
-// Debug wrapper: per-collective cross-rank fingerprint check and/or NaN check.
-std::shared_ptr<Comm> make_debug_comm(std::shared_ptr<Comm> inner, bool fingerprint, bool nan_check);
+// Debug wrapper: per-collective cross-rank fingerprint check and/or NaN check. `helper` (a CPU
+// communicator over the same ranks) carries the fingerprints; required for device backends.
+std::shared_ptr<Comm> make_debug_comm(std::shared_ptr<Comm> inner, bool fingerprint, bool nan_check,
+                                      std::shared_ptr<Comm> helper = nullptr);
 
 // Extra RCCL-only entry points (no-ops / errors for other backends).
 std::string rccl_version();

@@ -1,8 +1,14 @@
 // Debug communicator (TORCH_DISTRIBUTED_DEBUG=DETAIL / ProcessGroupWrapper and
 // TORCH_NCCL_NAN_CHECK analogues). Wraps any Comm:
 //  * fingerprint mode: before every collective, all-gather (seq, op, numel, dtype, arg) from all
-//    ranks through the wrapped communicator and raise a readable desync report on mismatch —
-//    turns a silent RCCL hang (ranks issuing different collectives) into an exception;
+//    ranks and raise a readable desync report on mismatch — turns a silent RCCL hang (ranks
+//    issuing different collectives) into an exception. The fingerprints travel over a separate
+//    host-side communicator (the CPU TCP ring on its own store prefix; ProcessGroupWrapper's gloo
+//    helper group in the reference stack), never through the wrapped device communicator: an RCCL
+//    collective issued inside an open ncclGroupStart (the Reducer's bucket bursts, coalescing()
+//    blocks) is only enqueued at ncclGroupEnd, so a fingerprint sent through it could not complete
+//    before the check reads it. The host exchange is synchronous and group-agnostic, so the check
+//    runs before every collective, grouped or not;
 //  * NaN check: before a reduction, scan the input with the multi-tensor non-finite kernel
 //    (GPU) or at::isfinite (CPU) and raise naming the collective.
 #include <ATen/hip/HIPContext.h>
@@ -18,8 +24,17 @@ namespace xddp {
 
 class DebugComm : public Comm {
  public:
-  DebugComm(std::shared_ptr<Comm> inner, bool fingerprint, bool nan_check)
-      : Comm(inner->rank(), inner->size()), inner_(std::move(inner)), fingerprint_(fingerprint), nan_(nan_check) {}
+  DebugComm(std::shared_ptr<Comm> inner, bool fingerprint, bool nan_check, std::shared_ptr<Comm> helper)
+      : Comm(inner->rank(), inner->size()),
+        inner_(std::move(inner)),
+        helper_(std::move(helper)),
+        fingerprint_(fingerprint),
+        nan_(nan_check) {
+    TORCH_CHECK(!fingerprint_ || helper_ || (inner_->backend() != "rccl" && inner_->backend() != "peer"),
+                "xddp debug comm: fingerprints of a device communicator need a host-side helper communicator");
+    TORCH_CHECK(!helper_ || (helper_->rank() == rank_ && helper_->size() == size_),
+                "xddp debug comm: helper communicator rank/size differ from the wrapped one");
+  }
 
   std::string backend() const override { return inner_->backend(); }
 
@@ -53,7 +68,10 @@ class DebugComm : public Comm {
   void group_start() override { inner_->group_start(); }
   void group_end() override { inner_->group_end(); }
   void abort() override { inner_->abort(); }
-  void shutdown() override { inner_->shutdown(); }
+  void shutdown() override {
+    inner_->shutdown();
+    if (helper_) helper_->shutdown();
+  }
   void set_timing(bool on) override {
     Comm::set_timing(on);
     inner_->set_timing(on);
@@ -103,14 +121,8 @@ class DebugComm : public Comm {
     const int64_t dt = t.defined() ? static_cast<int64_t>(t.scalar_type()) : -1;
     auto fp = at::tensor(std::vector<int64_t>{seq_, op_code(op), numel, dt, arg}, at::kLong);
     auto all = at::zeros({size_ * 5}, at::kLong);
-    if (inner_->backend() == "rccl") {
-      const auto dev = t.defined() && t.is_cuda() ? t.device() : at::Device(at::kCUDA, c10::hip::current_device());
-      auto fd = fp.to(dev), ad = all.to(dev);
-      inner_->allgather(ad, fd)->synchronize();
-      all = ad.cpu();
-    } else {
-      inner_->allgather(all, fp)->wait();
-    }
+    // host tensors over a host communicator: wait() returns once every rank's record is in `all`
+    (helper_ ? helper_ : inner_)->allgather(all, fp)->wait();
     const int64_t* a = all.data_ptr<int64_t>();
     bool same = true;
     for (int r = 1; r < size_; ++r)
@@ -127,12 +139,14 @@ class DebugComm : public Comm {
   }
 
   std::shared_ptr<Comm> inner_;
+  std::shared_ptr<Comm> helper_;  // host-side fingerprint exchange (device backends)
   bool fingerprint_, nan_;
   int64_t seq_ = 0;
 };
 
-std::shared_ptr<Comm> make_debug_comm(std::shared_ptr<Comm> inner, bool fingerprint, bool nan_check) {
-  return std::make_shared<DebugComm>(std::move(inner), fingerprint, nan_check);
+std::shared_ptr<Comm> make_debug_comm(std::shared_ptr<Comm> inner, bool fingerprint, bool nan_check,
+                                      std::shared_ptr<Comm> helper) {
+  return std::make_shared<DebugComm>(std::move(inner), fingerprint, nan_check, std::move(helper));
 }
 
 }  // namespace xddp

@@ -125,18 +125,21 @@ class RcclWork : public Work {
   bool is_completed() override {
     check_error();
     if (captured) return true;
+    if (!launched) return false;  // still inside an open group: nothing enqueued yet
     const bool done = hipEventQuery(ev) == hipSuccess;
     if (done) check_error();
     return done;
   }
   void wait() override {
     check_error();
+    check_launched("wait");
     auto cur = c10::hip::getCurrentHIPStream(device_);
     XDDP_HIP_CHECK(hipStreamWaitEvent(cur.stream(), ev, 0));
   }
   void synchronize() override {
     check_error();
     if (captured) return;  // host sync inside a capture is illegal; replay ordering is by stream
+    check_launched("synchronize");
     XDDP_HIP_CHECK(hipEventSynchronize(ev));
     check_error();
   }
@@ -171,8 +174,16 @@ class RcclWork : public Work {
     if (hipEventElapsedTime(&ms, iv->t0, ref.ev) != hipSuccess) return 0.0;
     return std::max(0.0, std::min<double>(ms, comm_ms()));
   }
+  // A work issued inside an open ncclGroupStart has no kernels and no recorded event until the
+  // group ends: its event (a pooled one, possibly recorded for an earlier collective) says nothing
+  // about it, so waiting on it before group_end is an error rather than a silent no-op.
+  void check_launched(const char* what) const {
+    TORCH_CHECK(launched.load(), "xddp rccl: ", what, "() on a collective issued inside an open group; ",
+                "the collective is launched at group_end() (close the coalescing block first)");
+  }
   hipEvent_t ev;
   int64_t t_start;
+  std::atomic<bool> launched{false};
   bool captured = false;
   std::shared_ptr<Interval> iv;  // timed works only
   bool owns_interval = true;     // false for the 2nd.. works of a grouped launch
@@ -614,6 +625,7 @@ class RcclComm : public Comm {
     auto w = std::make_shared<RcclWork>(pool_, device_, err_, probation_ ? nullptr : std::atomic_load(&peer_));
     w->seq = flight_.record(name, t.numel(), t.scalar_type());
     XDDP_HIP_CHECK(hipEventRecord(w->ev, c10::hip::getCurrentHIPStream(device_).stream()));
+    w->launched = true;
     flight_.finish(w->seq, "completed");
     w->outputs = {t};
     w->collective = false;  // one rank: nothing crossed a link
@@ -622,6 +634,7 @@ class RcclComm : public Comm {
 
   void finish_launch(const std::shared_ptr<RcclWork>& w) {
     XDDP_HIP_CHECK(hipEventRecord(w->ev, stream_.stream()));
+    w->launched = true;
     if (w->captured) return;  // a graph node, not a live collective
     std::lock_guard<std::mutex> g(wd_mu_);
     inflight_.push_back(w);

@@ -10,8 +10,11 @@
 //
 // One 256-thread block per row, 16-B (8 x bf16) loads; per thread an online (max, sum) pair,
 // merged across the block (shuffles, then LDS). Rows whose target is ignore_index contribute 0
-// and no gradient. Same math as torch's fp32 cross entropy on the upcast logits (the sums in a
-// different order).
+// and no gradient. A target outside [0, V) that is not ignore_index is an error, as in torch: the
+// row's loss is NaN (the step's loss shows it at once), it gets no gradient, and the kernel sets a
+// device-side flag that the Python wrapper turns into an IndexError without a per-step host sync
+// (ops/cross_entropy.py). Same math as torch's fp32 cross entropy on the upcast logits (the sums
+// in a different order).
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
@@ -36,7 +39,8 @@ __device__ __forceinline__ void merge(float& m, float& s, float m2, float s2) {
 
 __global__ __launch_bounds__(kXT) void xent_fwd_kernel(const dev::bf16_t* __restrict__ logits,
                                                        const int64_t* __restrict__ target, float* __restrict__ loss,
-                                                       float* __restrict__ lse, int64_t V, int64_t ignore_index) {
+                                                       float* __restrict__ lse, int* __restrict__ bad, int64_t V,
+                                                       int64_t ignore_index) {
   const int64_t r = blockIdx.x;
   const dev::bf16_t* row = logits + r * V;
   float m = -INFINITY, s = 0.f;
@@ -68,7 +72,9 @@ __global__ __launch_bounds__(kXT) void xent_fwd_kernel(const dev::bf16_t* __rest
     const float l = M + logf(S);
     lse[r] = l;
     const int64_t t = target[r];
-    loss[r] = (t == ignore_index || t < 0 || t >= V) ? 0.f : l - dev::bf16_to_f32(row[t].x);
+    const bool invalid = t != ignore_index && (t < 0 || t >= V);
+    if (invalid) atomicOr(bad, 1);
+    loss[r] = t == ignore_index ? 0.f : invalid ? NAN : l - dev::bf16_to_f32(row[t].x);
   }
 }
 
@@ -105,9 +111,13 @@ void check_xent(const at::Tensor& logits, const at::Tensor& target) {
 
 }  // namespace
 
-// -> (loss per row fp32 [R], lse per row fp32 [R]); rows with target == ignore_index give 0
-std::vector<at::Tensor> cross_entropy_forward(const at::Tensor& logits, const at::Tensor& target, int64_t ignore_index) {
+// -> (loss per row fp32 [R], lse per row fp32 [R]); rows with target == ignore_index give 0,
+// rows with a target outside [0, V) give NaN and set bad[0] (int32 on the device, never cleared)
+std::vector<at::Tensor> cross_entropy_forward(const at::Tensor& logits, const at::Tensor& target, int64_t ignore_index,
+                                              const at::Tensor& bad) {
   check_xent(logits, target);
+  TORCH_CHECK(bad.is_cuda() && bad.scalar_type() == at::kInt && bad.numel() >= 1 && bad.device() == logits.device(),
+              "cross_entropy: bad-target flag must be an int32 tensor on the logits' device");
   const int64_t R = logits.size(0), V = logits.size(1);
   auto loss = at::empty({R}, logits.options().dtype(at::kFloat));
   auto lse = at::empty({R}, logits.options().dtype(at::kFloat));
@@ -115,7 +125,7 @@ std::vector<at::Tensor> cross_entropy_forward(const at::Tensor& logits, const at
   auto stream = c10::hip::getCurrentHIPStream(logits.device().index()).stream();
   hipLaunchKernelGGL(xent_fwd_kernel, dim3((unsigned)R), dim3(kXT), 0, stream,
                      reinterpret_cast<const dev::bf16_t*>(logits.data_ptr()), target.data_ptr<int64_t>(),
-                     loss.data_ptr<float>(), lse.data_ptr<float>(), V, ignore_index);
+                     loss.data_ptr<float>(), lse.data_ptr<float>(), bad.data_ptr<int>(), V, ignore_index);
   XDDP_HIP_CHECK(hipGetLastError());
   return {loss, lse};
 }

@@ -127,7 +127,8 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
 void bind_norm_kernels(pybind11::module_& m);
 
 // cross_entropy.hip: softmax cross-entropy over bf16 logits [R, V] (fp32 math, no fp32 copy)
-std::vector<at::Tensor> cross_entropy_forward(const at::Tensor& logits, const at::Tensor& target, int64_t ignore_index);
+std::vector<at::Tensor> cross_entropy_forward(const at::Tensor& logits, const at::Tensor& target, int64_t ignore_index,
+                                              const at::Tensor& bad);
 at::Tensor cross_entropy_backward(const at::Tensor& logits, const at::Tensor& target, const at::Tensor& lse,
                                   const at::Tensor& gscale, int64_t ignore_index);
 

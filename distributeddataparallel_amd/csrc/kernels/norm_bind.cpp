@@ -28,7 +28,7 @@ void bind_norm_kernels(py::module_& m) {
   m.def("bn_backward_elem", &bn_backward_elem, py::arg("g"), py::arg("x"), py::arg("mean"), py::arg("coef"));
   m.def("bn_moments", &bn_moments, py::arg("x"));
   m.def("cross_entropy_forward", &cross_entropy_forward, py::arg("logits"), py::arg("target"),
-        py::arg("ignore_index") = -100);
+        py::arg("ignore_index"), py::arg("bad"));
   m.def("cross_entropy_backward", &cross_entropy_backward, py::arg("logits"), py::arg("target"), py::arg("lse"),
         py::arg("gscale"), py::arg("ignore_index") = -100);
   m.def("bn_grad_partials", &bn_grad_partials, py::arg("dy"), py::arg("x"), py::arg("mean"));

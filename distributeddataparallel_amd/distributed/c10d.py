@@ -295,9 +295,18 @@ class _World:
         self.groups: dict = {}
         self.group_count = 0
         self.store = None
+        # init generation of this process: every store key of a process group's life is scoped
+        # to it, so a second init_process_group over a persistent store (torchrun's agent store,
+        # a caller-owned store) never reads the previous generation's RCCL unique id or finds its
+        # init barrier already "done". All ranks run the same init/destroy sequence, so they agree.
+        self.init_gen = 0
 
 
 _world = _World()
+
+
+def _scoped(name: str) -> str:
+    return name if _world.init_gen <= 1 else f"gen{_world.init_gen}/{name}"
 
 
 def _excepthook_prefix(rank: int):
@@ -349,7 +358,14 @@ def _make_comm(backend: str, store, rank: int, size: int, device, timeout: timed
     detail = os.environ.get("XDDP_DEBUG", os.environ.get("TORCH_DISTRIBUTED_DEBUG", "OFF")).upper() == "DETAIL"
     nan = os.environ.get("XDDP_NAN_CHECK", "0") == "1"
     if detail or nan:
-        comm = C.make_debug_comm(comm, detail, nan)
+        helper = None
+        if detail and backend in ("rccl", "peer"):
+            # fingerprints go over a host-side ring on its own store prefix (ProcessGroupWrapper's
+            # gloo helper): grouped RCCL launches only run at group_end, so the device
+            # communicator cannot carry a check that must finish before the collective is issued
+            helper = C.make_cpu_comm(C.PrefixStore("xddp_debug", store), rank, size, timeout.total_seconds(),
+                                     advertise_host(master_addr))
+        comm = C.make_debug_comm(comm, detail, nan, helper)
     _comm_info[id(comm)] = info
     return comm
 
@@ -382,7 +398,8 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
         if rank < 0 or world_size <= 0:
             raise ValueError("rank and world_size are required when passing a store")
     device = _device_for(be, device_id)
-    pstore = C.PrefixStore("default_pg", store)
+    _world.init_gen += 1
+    pstore = C.PrefixStore(_scoped("default_pg"), store)
     comm = _make_comm(be, pstore, rank, world_size, device, timeout, master_addr)
     pg = ProcessGroup(comm, pstore, rank, world_size, be, list(range(world_size)), device,
                       group_name or "default_pg", timeout)
@@ -393,10 +410,10 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
     _excepthook_prefix(rank)
     if os.environ.get("XDDP_INIT_BARRIER", "1") == "1" and world_size > 1 and be != "fake":
         # store-based barrier: every rank's communicator is up before returning
-        n = store.add("xddp/init_barrier", 1)
+        n = store.add(_scoped("xddp/init_barrier"), 1)
         if n == world_size:
-            store.set("xddp/init_done", "1")
-        store.wait(["xddp/init_done"], timeout.total_seconds())
+            store.set(_scoped("xddp/init_done"), "1")
+        store.wait([_scoped("xddp/init_done")], timeout.total_seconds())
     return pg
 
 
@@ -480,7 +497,7 @@ def new_group(ranks: Optional[Sequence[int]] = None, timeout: Optional[timedelta
         return GroupMember.NON_GROUP_MEMBER
     timeout = timeout or world.timeout
     sub_rank = ranks.index(world.rank())
-    store = C.PrefixStore(name, _world.store)
+    store = C.PrefixStore(_scoped(name), _world.store)
     comm = _make_comm(be, store, sub_rank, len(ranks), world.device if be in ("rccl", "peer") else torch.device("cpu"),
                       timeout, os.environ.get("MASTER_ADDR", "127.0.0.1"))
     pg = ProcessGroup(comm, store, sub_rank, len(ranks), be, ranks, world.device, name, timeout)
@@ -501,9 +518,17 @@ def _group_rank(pg: ProcessGroup, global_rank: int) -> int:
 # ---------------------------------------------------------------------------------------
 # functional collectives
 # ---------------------------------------------------------------------------------------
+_coalesce_pending: List[list] = []  # per open coalescing() block: blocking collectives issued inside
+
+
 def _ret(work: Work, async_op: bool):
     if async_op:
         return work
+    if _coalesce_pending:
+        # inside coalescing() the collective is only launched when the outermost block closes
+        # (one RCCL group launch): the blocking call's wait happens there
+        _coalesce_pending[-1].append(work)
+        return None
     work.wait()
     return None
 
@@ -629,13 +654,24 @@ def monitored_barrier(group=None, timeout=None, wait_all_ranks=False):
 
 @contextlib.contextmanager
 def coalescing(group=None):
-    """Coalesce the collectives issued inside into one RCCL group launch."""
+    """Coalesce the collectives issued inside into one RCCL group launch. Blocking collectives
+    issued inside return at once and are waited for when the outermost block closes (the works of
+    ``async_op=True`` calls may only be waited on after that)."""
     pg = _resolve(group)
     pg.comm.group_start()
+    _coalesce_pending.append([])
+    ok = False
     try:
         yield
+        ok = True
     finally:
+        works = _coalesce_pending.pop()
         pg.comm.group_end()
+        if _coalesce_pending:
+            _coalesce_pending[-1].extend(works)
+        elif ok:
+            for w in works:
+                w.wait()
 
 
 def broadcast_object_list(object_list, src=0, group=None, device=None):

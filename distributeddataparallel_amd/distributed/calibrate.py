@@ -13,7 +13,10 @@ init (outside any timed region):
    every rank knows, alternating fp32 / bf16 and message sizes so both staging slots and several
    chunkings are exercised, under a short device-side timeout. Every rank's verdict is combined
    with a MAX all-reduce over the base path: ONE failing rank (wrong data, timeout, missing lane)
-   makes every rank close its lanes and keep RCCL, and the reason is reported.
+   makes every rank close its lanes and keep RCCL, and the reason is reported. On the ``peer``
+   backend the base path is the one-shot lane itself, so a failed self-check raises on every rank
+   (there is no path left to fall back to); lanes armed without probation
+   (``XDDP_PEER_ALLREDUCE=1/2``) are timed but not self-checked.
 2. **Timings.** Each route is timed at each probe size (2 warm-up + ``iters`` back-to-back calls,
    host clock around a device sync, so the launch cost is part of alpha); the timing matrix is
    MAX-reduced, so every rank holds identical numbers.
@@ -27,7 +30,8 @@ init (outside any timed region):
 All arithmetic on the measured numbers is plain Python on identical inputs: deterministic and the
 same on every rank. CPU tests drive :func:`fit_alpha_busbw` / :func:`choose_routes` on synthetic
 timings; ``tests/test_calibrate_gpu.py`` runs the whole procedure with two processes on one GPU
-over the ``peer`` backend, including a corrupted self-check that must force the fallback.
+over the ``peer`` backend, including a corrupted self-check that must raise on both ranks, and the
+RCCL communicator's probation path (fallback to the ring) with forced launches on one rank.
 """
 from __future__ import annotations
 
@@ -211,9 +215,17 @@ def calibrate(pg, sizes: Sequence[int], dtype=torch.bfloat16, iters: int = 5) ->
     sizes = sorted({int(s) for s in sizes})
     # 1. self-check of the peer lanes, agreed by all ranks
     has_peer = bool(list(comm.routes()))
-    if has_peer:
+    # Only lanes on probation can be self-checked safely: their failures are not communicator
+    # errors and closing them leaves a working base path. RCCL with XDDP_PEER_ALLREDUCE=1/2 arms the
+    # lanes at init (a self-check timeout would abort the communicator): the user chose them, they
+    # are timed but not self-checked. The peer backend has no other path: a failed self-check there
+    # is fatal (raised on every rank below).
+    on_probation = pg.backend == "peer" or comm.info().get("peer_probation", "0") == "1"
+    if has_peer and on_probation:
         comm.set_peer_timeout_ms(float(os.environ.get("XDDP_CALIBRATE_TIMEOUT_MS", "5000")))
         ok, reason = self_check(pg)
+    elif has_peer:
+        ok, reason = True, "lanes armed by XDDP_PEER_ALLREDUCE (no probation): timed, not self-checked"
     else:
         ok, reason = False, "peer lanes not created (XDDP_PEER_ALLREDUCE unset or IPC mapping failed)"
     fail = torch.tensor([0 if ok else 1], dtype=torch.int32, device=pg.device)
@@ -222,6 +234,11 @@ def calibrate(pg, sizes: Sequence[int], dtype=torch.bfloat16, iters: int = 5) ->
     all_ok = has_peer and int(fail.item()) == 0
     if has_peer and ok and not all_ok:
         reason = "another rank's self-check failed"
+    if pg.backend == "peer" and not (ok and all_ok):
+        # the verdict all-reduce itself ran on the lane under test; with no fallback path the only
+        # safe outcome is to stop every rank before a gradient is all-reduced on it
+        raise RuntimeError(f"xddp calibrate: peer backend self-check failed on rank {pg.rank()} "
+                           f"({reason}); the peer backend has no fallback path — use the rccl backend")
     if has_peer:
         if all_ok:
             timeout_ms = float(os.environ.get("XDDP_PEER_TIMEOUT_MS", pg.timeout.total_seconds() * 1000))

@@ -23,6 +23,8 @@ from .._native import load
 
 DEFAULT_MASTER_PORT = 29500
 
+_bootstrap_gen = 0  # agent-store bootstraps by this process (the address key is scoped to it)
+
 
 def _is_loopback(host: str) -> bool:
     try:
@@ -50,11 +52,14 @@ def _agent_store_bootstrap(rank: int, world_size: int, timeout: timedelta):
     """Create the xddp store when running under torchrun (agent owns MASTER_PORT)."""
     import torch.distributed as tdist
 
+    global _bootstrap_gen
     C = load()
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
     port = int(os.environ["MASTER_PORT"])
     agent = tdist.TCPStore(host, port, is_master=False, timeout=timeout, wait_for_workers=False)
-    key = f"xddp/store_addr/{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}/{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}"
+    _bootstrap_gen += 1  # a second init in the same worker must not read the first store's address
+    key = (f"xddp/store_addr/{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}/"
+           f"{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}/{_bootstrap_gen}")
     if rank == 0:
         store = C.TCPStore("0.0.0.0", 0, True, world_size, timeout.total_seconds(), False)
         agent.set(key, f"{advertise_host(host)}:{store.port}")

@@ -24,12 +24,20 @@ import torch.nn.functional as F
 
 from .._native import load
 
-__all__ = ["linear", "multi_linear", "own_gemm_ok", "own_gemm_mode", "set_grad_targets"]
+__all__ = ["linear", "multi_linear", "own_gemm_ok", "own_gemm_mode", "set_grad_targets", "clear_grad_targets"]
 
 # weight -> the tensor its gradient should be written into (DDP with gradient_as_bucket_view
 # registers each parameter's view of its bucket, ``DistributedDataParallel._pre_forward``)
-# (keyed by id: a WeakKeyDictionary would compare tensor keys with elementwise ==)
-_GRAD_TARGETS: dict = {}  # id(param) -> (weakref(param), target)
+# (keyed by id: a WeakKeyDictionary would compare tensor keys with elementwise ==). Both the
+# parameter and the target are held weakly: the DDP object owns the bucket views, so a deleted
+# DDP (or a rebuilt bucket layout) leaves only dead entries behind, never live bucket memory.
+_GRAD_TARGETS: dict = {}  # id(param) -> (weakref(param), weakref(target))
+
+
+def _autocast_on(t: torch.Tensor) -> bool:
+    """Autocast active for ``t``'s device type: the custom Functions below have no
+    custom_fwd/custom_bwd casts, so under autocast every path here defers to ``F.linear``."""
+    return torch.is_autocast_enabled(t.device.type)
 
 
 def set_grad_targets(params, targets) -> None:
@@ -40,7 +48,7 @@ def set_grad_targets(params, targets) -> None:
     read + one write of every weight gradient per step; 16 GB for Llama-3-8B)."""
     for p, t in zip(params, targets):
         if t is not None and t.shape == p.shape and t.dtype == p.dtype and t.device == p.device and t.is_contiguous():
-            _GRAD_TARGETS[id(p)] = (weakref.ref(p), t)
+            _GRAD_TARGETS[id(p)] = (weakref.ref(p), weakref.ref(t))
         else:
             _GRAD_TARGETS.pop(id(p), None)
 
@@ -49,7 +57,7 @@ def _dw(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``dW = dY2ᵀ·X2`` for weight ``w`` — into its registered target when ``w`` has no gradient
     yet (the first contribution of this backward), returned as a fresh alias of it."""
     e = _GRAD_TARGETS.pop(id(w), None)  # one claim per registration: a weight used twice in a
-    t = e[1] if e is not None and e[0]() is w else None  # forward gets one target write
+    t = e[1]() if e is not None and e[0]() is w else None  # forward gets one target write
     if t is not None and w.grad is None and not torch.is_grad_enabled():
         torch.mm(dy2.t(), x2, out=t)
         return t.view(t.shape)
@@ -62,8 +70,14 @@ def own_gemm_mode() -> str:
     return v if v in ("0", "1", "bwd") else "bwd"
 
 
+def clear_grad_targets(params) -> None:
+    """Drop the registrations of ``params`` (a DDP being torn down or rebuilt)."""
+    for p in params:
+        _GRAD_TARGETS.pop(id(p), None)
+
+
 def own_gemm_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
-    if own_gemm_mode() != "1" or torch.is_autocast_enabled():
+    if own_gemm_mode() != "1" or _autocast_on(x):
         return False
     N, K = weight.shape
     return (x.is_cuda and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and K % 64 == 0
@@ -110,7 +124,7 @@ def linear(x: torch.Tensor, weight: torch.Tensor, residual: Optional[torch.Tenso
         return _Linear.apply(x, weight, residual)
     if residual is not None and (residual.shape[:-1] != x.shape[:-1] or residual.dtype != x.dtype):
         return residual + F.linear(x, weight)
-    if weight.dim() != 2 or x.dtype != weight.dtype:
+    if weight.dim() != 2 or x.dtype != weight.dtype or _autocast_on(x):
         y = F.linear(x, weight)
         return y if residual is None else residual + y
     return _LinearBlas.apply(x, weight, residual)
@@ -176,7 +190,7 @@ def multi_linear(x: torch.Tensor, *weights: torch.Tensor):
     """``x·W_iᵀ`` for each weight (bias-free), the input gradient accumulated in GEMMs (see
     :class:`_MultiLinear`); the own GEMM's path (``XDDP_OWN_GEMM=1``) keeps one :func:`linear` per
     weight. ``XDDP_MULTI_LINEAR=0``: plain per-weight linears (A/B switch)."""
-    if os.environ.get("XDDP_MULTI_LINEAR", "1") == "0" or any(own_gemm_ok(x, w) for w in weights) or \
-            not all(w.dtype == x.dtype and w.dim() == 2 for w in weights):
+    if os.environ.get("XDDP_MULTI_LINEAR", "1") == "0" or _autocast_on(x) or any(own_gemm_ok(x, w) for w in weights) \
+            or not all(w.dtype == x.dtype and w.dim() == 2 for w in weights):
         return tuple(linear(x, w) for w in weights)
     return _MultiLinear.apply(x, *weights)

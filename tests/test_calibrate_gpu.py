@@ -1,8 +1,10 @@
 """Comm calibration on the device (distributed/calibrate.py), two processes sharing cuda:0 over
 the ``peer`` backend (RCCL refuses two ranks on one device; the peer backend runs the same peer
 kernels and the same calibration steps): the self-check passes and a route table is installed,
-and a corrupted self-check on ONE rank makes BOTH ranks drop the two-shot lane (fail-closed),
-with the reason reported. Collectives after calibration are still exact."""
+and a corrupted self-check on ONE rank makes BOTH ranks raise (fail-closed: the peer backend's
+base path is the lane under test, so there is nothing to fall back to). On the RCCL communicator
+a failed self-check closes the lanes on every rank and keeps the ring. Collectives after
+calibration are still exact."""
 import zlib
 
 import pytest
@@ -20,6 +22,11 @@ def _w_calibrate(rank, world, expect_ok):
     from distributeddataparallel_amd.parallel import bucket_policy as bp
 
     pg = xdist.get_default_group()
+    if not expect_ok:
+        with pytest.raises(RuntimeError, match="peer backend self-check failed"):
+            cal.calibrate(pg, [64 << 10, MiB, 4 * MiB], torch.bfloat16, iters=3)
+        bp.clear_calibration()
+        return
     try:
         rep = cal.calibrate(pg, [64 << 10, MiB, 4 * MiB], torch.bfloat16, iters=3)
         assert rep["self_check"]["ok"] is expect_ok, rep
@@ -53,7 +60,7 @@ def test_calibration_peer_backend_self_check_and_routes():
     run_ranks(_w_calibrate, world=2, backend="peer", args=(True,))
 
 
-def test_calibration_corrupted_self_check_falls_back_on_every_rank():
+def test_calibration_corrupted_self_check_raises_on_every_rank():
     run_ranks(_w_calibrate, world=2, backend="peer", args=(False,), env={"XDDP_CALIBRATE_CORRUPT_RANK": "1"})
 
 

@@ -37,3 +37,25 @@ def test_cross_entropy_scaled_upstream_gradient():
     b = x.clone().requires_grad_(True)
     (3.0 * F.cross_entropy(b.float(), t)).backward()
     torch.testing.assert_close(a.grad.float(), b.grad.float(), rtol=2e-2, atol=1e-2 * b.grad.abs().max().item())
+
+
+def test_cross_entropy_out_of_range_target_raises():
+    """A target outside [0, V) that is not ignore_index: NaN loss at once, IndexError at the next
+    check (torch raises too); ignore_index rows stay legal."""
+    from distributeddataparallel_amd.ops.cross_entropy import check_targets
+
+    check_targets(block=True)  # clean slate
+    x = torch.randn(8, 512, device="cuda").to(torch.bfloat16)
+    t = torch.randint(0, 512, (8,), device="cuda")
+    t[3] = 512
+    t[5] = -100
+    loss = cross_entropy(x.clone().requires_grad_(True), t)
+    assert torch.isnan(loss).item()
+    with pytest.raises(IndexError, match="out of bounds"):
+        check_targets(block=True)
+    check_targets(block=True)  # the flag was consumed
+    t[3] = -7
+    cross_entropy(x, t)
+    torch.cuda.synchronize()
+    with pytest.raises(IndexError):
+        cross_entropy(x, torch.zeros(8, dtype=torch.long, device="cuda"))  # raised lazily by the next call

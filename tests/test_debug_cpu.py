@@ -86,3 +86,74 @@ def test_flight_record_dumped_on_collective_timeout(tmp_path):
 
     spawn(_timeout_worker, args=(2, str(tmp_path / "flight_")), nprocs=2,
           env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port()), "OMP_NUM_THREADS": "1"})
+
+
+def _w_desync_in_coalescing(rank, world):
+    """Ranks agree on the first collective of a coalescing block and disagree on the second: the
+    fingerprint check (run before each collective, grouped or not) reports it on every rank."""
+    from distributeddataparallel_amd import distributed as d
+
+    a = torch.ones(8)
+    b = torch.ones(16 + 4 * rank)
+    with pytest.raises(RuntimeError, match="desync detected"):
+        with d.coalescing():
+            d.all_reduce(a)
+            d.all_reduce(b)
+    # the group is closed again and a matching collective still runs
+    c = torch.full((4,), float(rank + 1))
+    d.all_reduce(c)
+    assert torch.equal(c, torch.full((4,), 3.0))
+
+
+def test_desync_inside_coalescing_block_detected():
+    run_ranks(_w_desync_in_coalescing, world=2, env={"XDDP_DEBUG": "DETAIL"})
+
+
+def _w_helper_fingerprints(rank, world):
+    """The device backends' arrangement on CPU ranks: the fingerprints travel over a separate
+    helper communicator (own store prefix), the collectives over the wrapped one."""
+    from distributeddataparallel_amd import distributed as d
+    from distributeddataparallel_amd._native import load
+
+    C = load()
+    pg = d.get_default_group()
+    helper = C.make_cpu_comm(C.PrefixStore("fp_helper", pg.store), rank, world, 60.0, "127.0.0.1")
+    inner = C.make_cpu_comm(C.PrefixStore("fp_inner", pg.store), rank, world, 60.0, "127.0.0.1")
+    dbg = C.make_debug_comm(inner, True, False, helper)
+    t = torch.full((5,), float(rank))
+    dbg.allreduce(t, C.RedOp.SUM, 1.0).wait()
+    assert torch.equal(t, torch.full((5,), 1.0))
+    n_inner = len(inner.flight_records())
+    with pytest.raises(RuntimeError, match="desync detected"):
+        dbg.allreduce(torch.ones(3 + rank), C.RedOp.SUM, 1.0).wait()
+    assert len(inner.flight_records()) == n_inner  # the mismatched collective never reached the wrapped comm
+    dbg.shutdown()
+
+
+def test_fingerprints_over_helper_communicator():
+    run_ranks(_w_helper_fingerprints, world=2)
+
+
+def _reinit_worker(rank, world, port):
+    from distributeddataparallel_amd import distributed as xdist
+    from distributeddataparallel_amd._native import load
+
+    C = load()
+    store = C.TCPStore("127.0.0.1", port, rank == 0, world, 60.0, False)  # one store for both lives
+    for cycle in range(3):
+        xdist.init_process_group("cpu", store=store, rank=rank, world_size=world)
+        t = torch.full((6,), float(rank + cycle))
+        xdist.all_reduce(t)
+        assert torch.equal(t, torch.full((6,), float(1 + 2 * cycle))), (cycle, t)
+        xdist.barrier()
+        xdist.destroy_process_group()
+
+
+def test_reinit_over_persistent_store():
+    """init / destroy three times over ONE store: each generation's keys (communicator bootstrap,
+    init barrier) are its own, so no stale address or already-'done' barrier is read."""
+    from distributeddataparallel_amd.utils.spawn import free_port, spawn
+
+    port = free_port()
+    spawn(_reinit_worker, args=(2, port), nprocs=2,
+          env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port()), "OMP_NUM_THREADS": "1"})

@@ -127,6 +127,58 @@ print("forced-launch ok", n)
     assert r.returncode == 0 and "forced-launch ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
+def test_rccl_forced_launch_debug_detail_grouped():
+    """XDDP_DEBUG=DETAIL on the RCCL communicator with real RCCL kernels (W=1, forced launches):
+    DDP iterations whose bucket bursts are RCCL groups (iteration 0's single launch, the rebuilt
+    buckets' tail) and a nested coalescing() block run without a false desync and with exact
+    gradients — the fingerprints go over the host helper ring, not through the open group. A
+    wait() on a collective inside an open group raises instead of returning on a stale event."""
+    import subprocess
+    import sys
+
+    code = r'''
+import os, torch, pytest, torch.nn.functional as F
+import distributeddataparallel_amd as xddp
+from distributeddataparallel_amd import distributed as dist
+from distributeddataparallel_amd.models import SimpleCNN
+from distributeddataparallel_amd.utils.spawn import free_port
+os.environ["MASTER_ADDR"] = "127.0.0.1"; os.environ["MASTER_PORT"] = str(free_port())
+pg = dist.init_process_group("rccl", rank=0, world_size=1, device_id=0)
+torch.backends.cudnn.deterministic = True
+torch.manual_seed(0)
+model, ref = SimpleCNN().cuda(), SimpleCNN().cuda()
+ddp = xddp.DDP(model, device_ids=[0], bucket_cap_mb=1)
+opt = torch.optim.SGD(ddp.parameters(), lr=0.01)
+for it in range(4):
+    ref.load_state_dict(model.state_dict())
+    x = torch.randn(16, 3, 32, 32, device="cuda"); y = torch.randint(0, 10, (16,), device="cuda")
+    opt.zero_grad(); ref.zero_grad()
+    F.cross_entropy(ddp(x), y).backward(); F.cross_entropy(ref(x), y).backward()
+    for p, q in zip(model.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.grad, q.grad, rtol=0, atol=0)
+    opt.step()
+print("grouped launches", ddp._get_ddp_logging_data()["num_grouped_launches"])
+a = torch.arange(6, device="cuda", dtype=torch.float32); b = torch.ones(1000, device="cuda", dtype=torch.bfloat16)
+with dist.coalescing():
+    dist.all_reduce(a)
+    with dist.coalescing():
+        w = dist.all_reduce(b, async_op=True)
+        with pytest.raises(RuntimeError, match="inside an open group"):
+            w.wait()
+    dist.broadcast(a, 0)
+w.wait(); torch.cuda.synchronize()
+assert torch.equal(a, torch.arange(6, device="cuda", dtype=torch.float32)) and torch.equal(b, torch.ones_like(b))
+recs = [r["op"] for r in pg.flight_records()]
+assert recs.count("allreduce") >= 8, recs
+dist.destroy_process_group()
+print("detail ok")
+'''
+    env = dict(os.environ, XDDP_RCCL_FORCE_LAUNCH="1", XDDP_DEBUG="DETAIL")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "detail ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
 @pytest.mark.parametrize("schedule,grad_as_view", [("tail", False), ("tail", True), ("backward", False)])
 def test_rccl_forced_launch_overlapped_optimizer(schedule, grad_as_view):
     """W=1 with real RCCL kernels on the comm stream (XDDP_RCCL_FORCE_LAUNCH=1): the overlapped
