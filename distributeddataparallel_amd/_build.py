@@ -9,6 +9,15 @@ Usage::
 
     python -m distributeddataparallel_amd._build          # incremental
     python -m distributeddataparallel_amd._build --clean  # full rebuild
+    python -m distributeddataparallel_amd._build --sanitize address,undefined --out DIR
+
+``--sanitize`` builds the host C++ (store, communicators, Reducer, bindings)
+with the given clang sanitizers (``address,undefined`` or ``thread``) into ``build_san_<kind>/``
+and links it with the regular build's device objects (the HIP kernels are not instrumented: GPU
+sanitizers are not available on this pool) into ``DIR/distributeddataparallel_amd/_C*.so``, next
+to a copy of the Python package: a process that puts ``DIR`` first on ``sys.path`` and preloads
+the clang sanitizer runtime (:func:`sanitizer_runtime`) runs the package on the instrumented
+host code (``tests/test_sanitizers_cpu.py``).
 """
 from __future__ import annotations
 
@@ -48,7 +57,16 @@ def _ninja_escape(p: str) -> str:
     return p.replace("$", "$$").replace(" ", "$ ").replace(":", "$:")
 
 
-def write_ninja(debug: bool = False) -> Path:
+def sanitizer_runtime(kind: str) -> Path:
+    """The clang sanitizer runtime to LD_PRELOAD into an uninstrumented python for ``kind``."""
+    name = "tsan" if kind == "thread" else "asan"
+    libs = sorted((ROCM / "lib" / "llvm" / "lib" / "clang").glob(f"*/lib/linux/libclang_rt.{name}-x86_64.so"))
+    if not libs:
+        raise FileNotFoundError(f"no clang {name} runtime under {ROCM}/lib/llvm/lib/clang")
+    return libs[-1]
+
+
+def write_ninja(debug: bool = False, sanitize: str | None = None, out_so: Path | None = None) -> Path:
     tdir, incs, tlib, abi = _torch_paths()
     import pybind11
 
@@ -63,6 +81,8 @@ def write_ninja(debug: bool = False) -> Path:
         f"-D_GLIBCXX_USE_CXX11_ABI={int(abi)}"
     )
     opt = "-O0 -g" if debug else "-O3"
+    if sanitize:
+        opt = f"-O1 -g -fno-omit-frame-pointer -fsanitize={sanitize} -shared-libsan"
     common = f"-std=c++17 -fPIC {opt} -Wno-unused-result -Wno-deprecated-declarations {defs} {inc_flags}"
     hipcc = str(ROCM / "bin" / "hipcc")
     hip_flags = f"{common} -x hip --offload-arch={ARCH} -fno-gpu-rdc -munsafe-fp-atomics"
@@ -79,7 +99,8 @@ def write_ninja(debug: bool = False) -> Path:
         f"hipcc = {hipcc}",
         f"hipflags = {hip_flags}",
         f"cppflags = {cpp_flags}",
-        f"ldflags = -shared --hip-link --offload-arch={ARCH} {libs}",
+        f"ldflags = -shared --hip-link --offload-arch={ARCH} {libs}"
+        + (f" -fsanitize={sanitize} -shared-libsan" if sanitize else ""),
         "rule hip",
         "  command = $hipcc -MMD -MF $out.d $hipflags -c $in -o $out",
         "  depfile = $out.d",
@@ -94,16 +115,23 @@ def write_ninja(debug: bool = False) -> Path:
         "  command = $hipcc $in $ldflags -o $out",
         "  description = LINK $out",
     ]
+    bdir = _san_dir(sanitize) if sanitize else BUILD_DIR
+    out_so = out_so or OUT_SO
     objs = []
     for src in hip + cpp:
         rel = src.relative_to(CSRC)
-        obj = BUILD_DIR / (str(rel).replace(os.sep, "__") + ".o")
+        name = str(rel).replace(os.sep, "__") + ".o"
+        if sanitize and src.suffix == ".hip":  # the regular build's device objects, uninstrumented
+            objs.append(_ninja_escape(str(BUILD_DIR / name)))
+            continue
+        obj = bdir / name
         rule = "hip" if src.suffix == ".hip" else "cxx"
         lines.append(f"build {_ninja_escape(str(obj))}: {rule} {_ninja_escape(str(src))}")
         objs.append(_ninja_escape(str(obj)))
-    lines.append(f"build {_ninja_escape(str(OUT_SO))}: link {' '.join(objs)}")
-    lines.append(f"default {_ninja_escape(str(OUT_SO))}")
-    nf = BUILD_DIR / "build.ninja"
+    lines.append(f"build {_ninja_escape(str(out_so))}: link {' '.join(objs)}")
+    lines.append(f"default {_ninja_escape(str(out_so))}")
+    bdir.mkdir(exist_ok=True)
+    nf = bdir / "build.ninja"
     content = "\n".join(lines) + "\n"
     if not nf.exists() or nf.read_text() != content:
         nf.write_text(content)
@@ -117,6 +145,25 @@ def _ninja_bin() -> str:
     import ninja  # pip wheel ships the binary
 
     return str(Path(ninja.BIN_DIR) / "ninja")
+
+
+def _san_dir(kind: str) -> Path:
+    return PKG_DIR / ("build_san_" + kind.replace(",", "_"))
+
+
+def build_sanitized(kind: str, out_dir: Path, jobs: int | None = None) -> Path:
+    """Host code under ``kind`` sanitizers + the regular device objects -> a package copy in
+    ``out_dir`` (module docstring). Builds the regular objects first if needed."""
+    build(jobs=jobs)
+    pkg = Path(out_dir) / PKG_DIR.name
+    if pkg.exists():
+        shutil.rmtree(pkg)
+    shutil.copytree(PKG_DIR, pkg, ignore=shutil.ignore_patterns("build*", "_C*.so", "__pycache__", "csrc"))
+    so = pkg / OUT_SO.name
+    nf = write_ninja(sanitize=kind, out_so=so)
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    subprocess.run([_ninja_bin(), "-f", str(nf), "-j", str(jobs)], check=True, cwd=str(nf.parent))
+    return so
 
 
 def build(clean: bool = False, jobs: int | None = None, verbose: bool = False, debug: bool = False) -> Path:
@@ -137,8 +184,13 @@ def main(argv=None):
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--sanitize", default=None, help="address,undefined | thread (host code only)")
+    ap.add_argument("--out", default=None, help="with --sanitize: directory for the package copy")
     a = ap.parse_args(argv)
-    out = build(clean=a.clean, jobs=a.jobs, verbose=a.verbose, debug=a.debug)
+    if a.sanitize:
+        out = build_sanitized(a.sanitize, Path(a.out or f"/tmp/xddp_san_{a.sanitize.replace(',', '_')}"), a.jobs)
+    else:
+        out = build(clean=a.clean, jobs=a.jobs, verbose=a.verbose, debug=a.debug)
     print(f"built {out}")
 
 

@@ -7,8 +7,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _entry(rank, fn, world, backend, args):
-    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.environ.get("XDDP_PKG_ROOT", REPO))
     from distributeddataparallel_amd import distributed as xdist
+
+    root = os.environ.get("XDDP_PKG_ROOT")
+    if root:  # a sanitizer run: every rank must run the instrumented extension, not the repo's
+        from distributeddataparallel_amd._native import load
+
+        assert load().__file__.startswith(root), load().__file__
 
     xdist.init_process_group(backend, rank=rank, world_size=world)
     try:

@@ -6,6 +6,11 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
+# XDDP_PKG_ROOT: import the package from another root (the sanitizer builds' package copies,
+# tests/test_sanitizers_cpu.py); spawned ranks inherit this sys.path
+_root = os.environ.get("XDDP_PKG_ROOT")
+if _root:
+    sys.path.insert(0, _root)
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 # flight-record dumps from intentionally failing collectives go to a private temp dir
 import tempfile  # noqa: E402

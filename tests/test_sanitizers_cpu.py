@@ -1,8 +1,11 @@
 """Sanitizer builds of the native host code: the TCP/File stores and a
-multi-threaded stress driver compiled with AddressSanitizer+UBSan and with ThreadSanitizer."""
+multi-threaded stress driver compiled with AddressSanitizer+UBSan and with ThreadSanitizer, and the
+whole extension's host code (Reducer, communicators, bindings) under both, driving W=2 DDP
+scenarios (``_san_scenarios.py``)."""
 import os
 import shutil
 import subprocess
+import sys
 
 import pytest
 
@@ -24,3 +27,32 @@ def test_store_stress_under_sanitizer(tmp_path, san):
                TSAN_OPTIONS="halt_on_error=1")
     r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0 and "store_stress OK" in r.stdout, (r.stdout[-2000:], r.stderr[-6000:])
+
+
+_SCENARIOS = ["collectives", "parity_and_no_sync", "find_unused_and_static", "join_uneven"]
+
+
+@pytest.mark.parametrize("san", ["address,undefined", "thread"])
+def test_reducer_and_cpu_backend_under_sanitizer(tmp_path_factory, san):
+    """The Reducer (autograd hooks, bucket launches, rebuild, finalize callback, no_sync,
+    find_unused_parameters, static graph, join) and the CPU ring backend's worker thread, built
+    with ASan+UBSan / TSan (``_build.build_sanitized``: host code instrumented, device objects of
+    the regular build), W=2 ranks, halt_on_error. TSan runs with the torch-internal suppressions of
+    ``tsan_suppressions.txt`` and mutex-misuse reports off (torch's own locking is uninstrumented)."""
+    from distributeddataparallel_amd import _build
+
+    try:
+        rt = _build.sanitizer_runtime(san)
+    except FileNotFoundError as e:
+        pytest.skip(str(e))
+    out = tmp_path_factory.mktemp("san_" + san.replace(",", "_"))
+    _build.build_sanitized(san, out)
+    env = dict(os.environ, XDDP_PKG_ROOT=str(out), LD_PRELOAD=str(rt), OMP_NUM_THREADS="1",
+               ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
+               TSAN_OPTIONS="halt_on_error=1:report_signal_unsafe=0:report_mutex_bugs=0:suppressions="
+                            + os.path.join(REPO, "tests", "tsan_suppressions.txt"))
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tests", "_san_driver.py"), *_SCENARIOS],
+                       capture_output=True, text=True, env=env, timeout=900)
+    assert r.returncode == 0 and "sanitizer scenarios OK" in r.stdout, (r.stdout[-2000:], r.stderr[-8000:])
+    assert "Sanitizer" not in r.stderr, r.stderr[-8000:]
