@@ -531,6 +531,12 @@ std::vector<at::Tensor> conv3x3_halo(const at::Tensor& x, const at::Tensor& w, b
   return {y, part};
 }
 
+// the band kernel with an explicit band height (timing scripts, tests)
+std::vector<at::Tensor> conv3x3_band_forward(const at::Tensor& x, const at::Tensor& w, bool stats, int64_t rows,
+                                             int64_t cfg) {
+  return conv3x3_band(x, w, stats, rows, zero_line(x), cfg);
+}
+
 // x [B, C, IH, IW] bf16 channels_last; w [N, C, 3, 3] bf16 channels_last (OHWI memory);
 // returns {y [B, N, OH, OW] channels_last, stats partials [3, N, mtiles] (group-minor; empty if
 // !stats)}.
@@ -549,6 +555,17 @@ std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w
               "conv3x3_forward: 16-B aligned operands required");
   const int64_t OH = (IH - 1) / stride + 1, OW = (IW - 1) / stride + 1, M = B * OH * OW;
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "conv3x3_forward: bad size");
+  // stride-1 layers whose rows tile into 224 / 196-pixel bands (conv3x3_band.hip); XDDP_C3_BAND=0:
+  // the halo / dense-GEMM kernels below
+  {
+    static const bool band_on = [] {
+      const char* e = std::getenv("XDDP_C3_BAND");
+      return !e || std::atoi(e) != 0;
+    }();
+    if (band_on && stride == 1 && IW >= 14 && (N == 64 || N % 128 == 0) && conv3x3_band_rows(IW, IH, N == 64 ? 224 : 208) > 0 &&
+        x.numel() < (int64_t(1) << 31) && M * N < (int64_t(1) << 31))
+      return conv3x3_band(x, w, stats, 0, zero_line(x));
+  }
   // wide layers (N >= XDDP_C3_GEMM_MIN_N, default 256; 0 = never) on the dense GEMM's 4-phase
   // LDS-DMA pipeline with the im2col addressing (gemm.hip ConvGeo)
   {

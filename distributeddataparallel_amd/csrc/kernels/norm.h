@@ -60,6 +60,13 @@ std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w
 // 256-B zero line on the device
 std::vector<at::Tensor> conv3x3_gemm(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats,
                                      const uint16_t* zeros);
+// stride-1 3x3 conv on row bands that may span images (conv3x3_band.hip); rows = output rows per
+// band (0: the measured choice, conv3x3_band_rows; 0 returned there = shape not covered)
+std::vector<at::Tensor> conv3x3_band(const at::Tensor& x, const at::Tensor& w, bool stats, int64_t rows,
+                                     const uint16_t* zeros, int64_t cfg = -1);
+int conv3x3_band_rows(int64_t W, int64_t H, int64_t bm);
+std::vector<at::Tensor> conv3x3_band_forward(const at::Tensor& x, const at::Tensor& w, bool stats, int64_t rows,
+                                             int64_t cfg);
 at::Tensor conv3x3_rot_weight(const at::Tensor& w);
 at::Tensor conv3x3_dgrad_s2(const at::Tensor& dy, const at::Tensor& w_rot, int64_t H, int64_t W);
 at::Tensor conv3x3_dgrad_s2_gemm(const at::Tensor& dy, const at::Tensor& wr, int64_t XH, int64_t XW,

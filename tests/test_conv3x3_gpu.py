@@ -151,3 +151,38 @@ def test_conv3x3_wgrad_patch_matches_conv2d(b, cin, h, w, cout, s):
     # fp32 output: no bf16 rounding of the result, only the inputs' (exact products, fp32 sums)
     dw32 = C.conv3x3_wgrad_patch(dy, x, s, wt.float())
     torch.testing.assert_close(dw32, ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("b,cin,h,w,cout,rows,cfg,off", [
+    (2, 64, 56, 56, 64, 4, 0, 30.0),     # layer-1 band: 4 rows = 224 pixels, N = 64 tiles
+    (2, 64, 56, 56, 64, 4, 1, 0.0),      # the same, weights in registers
+    (3, 128, 28, 28, 128, 7, 2, 0.0),    # layer-2 band: 7 rows = 196 pixels, 208-row tile
+    (3, 128, 28, 28, 256, 7, 4, 0.0),    # the same, weights in registers (half-step buffers)
+    (2, 256, 7, 7, 256, 28, 4, 5.0),     # registers, bands over four images, 4 channel steps
+    (3, 256, 14, 14, 256, 14, 2, 0.0),   # layer-3: one band = one image, two N tiles
+    (5, 512, 7, 7, 512, 28, 2, 0.0),     # a band spans four images; partial last band
+    (5, 512, 7, 7, 512, 14, 3, 0.0),     # layer-4 default: two-image bands, 112-row tiles
+    (3, 128, 7, 7, 256, 29, 2, 10.0),    # bands start mid-image: first segment partial, 5 segments
+    (2, 64, 10, 12, 64, 3, 0, 0.0),      # ragged: 20 rows in bands of 3, crossing an image edge
+    (1, 128, 5, 9, 128, 23, 2, 0.0),     # more rows per band than the batch has (one partial band)
+])
+def test_conv3x3_band_matches_conv2d(b, cin, h, w, cout, rows, cfg, off):
+    """Row-band kernel (conv3x3_band.hip) with explicit band heights and configurations: bands
+    crossing image edges, partial first segments and a partial last band, output and BN statistics
+    partials."""
+    torch.manual_seed(2)
+    x = _cl(torch.randn(b, cin, h, w, device="cuda") + off)
+    wt = _cl(torch.randn(cout, cin, 3, 3, device="cuda") / (9 * cin) ** 0.5)
+    y, part = C.conv3x3_band_forward(x, wt, True, rows, cfg)
+    ref = F.conv2d(x.float(), wt.float(), padding=1)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+    assert part.shape == (3, cout, (b * h + rows - 1) // rows)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, cout)
+    rm, rv = torch.zeros(cout, device="cuda"), torch.ones(cout, device="cuda")
+    nbt = torch.zeros((), dtype=torch.long, device="cuda")
+    mean, invstd, _ = C.bn_stats_from_partials(part, yf.shape[0], None, None, rm, rv, nbt, 0.1, False, 1e-5, True)
+    torch.testing.assert_close(mean, yf.mean(0), rtol=1e-5, atol=1e-4 * yf.std(0).max().item())
+    torch.testing.assert_close(1.0 / invstd ** 2 - 1e-5, yf.var(0, unbiased=False), rtol=2e-3, atol=1e-6)
+    y2, _ = C.conv3x3_band_forward(x, wt, False, rows, cfg)  # the no-statistics instance: same output
+    assert torch.equal(y, y2)
