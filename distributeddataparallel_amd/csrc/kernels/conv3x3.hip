@@ -18,7 +18,9 @@
 // raw s_barrier (never vmcnt(0) inside the loop) retires step k's stage for every wave.
 // One block per CU (64x64 output per wave = 16 accumulators, 2 waves per SIMD), block ids
 // remapped XCD-contiguously so the N-tiles of one M-panel and neighbouring panels (which share
-// input rows through the 3x3 halo) sit in one L2.
+// input rows through the 3x3 halo) sit in one L2. Since r5 it runs the shapes the row-band kernel
+// (conv3x3_band.hip) and the dense-GEMM path do not: stride 2 at N < 256, W > 56 or odd channel
+// counts, and the stride-2 input gradient's generic (odd-size) case.
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
@@ -275,199 +277,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_fwd_kernel(
   }
 }
 
-// Halo variant for the narrow stride-1 layers (N <= 128: ResNet-50 layer1/2, W >= 14). The
-// implicit GEMM above re-stages its A tile for every one of the 9 taps: 9 x 128 B of L2->LDS
-// traffic per output pixel and 64-channel step, which at N = 64 exceeds what an XCD's L2 serves
-// per MFMA (MI355X_MICROARCH.md: ~70 GB/s per CU from L2). Here a block owns R full output rows
-// of one image (R x W <= 256 pixels) and stages the (R + 2) x (W + 2) input halo of a 64-channel
-// step ONCE; the 9 taps read shifted windows of it (row = halo pixel, 128 B, chunk XOR-swizzled
-// by (row >> 1) & 7 as the DMA source addresses pre-swizzle it). Only the weights of a tap
-// (BN x 64) stream per tap, through a 3-slot ring with counted vmcnt waits. Padding pixels of the
-// halo DMA a zero line. A lane's MFMA rows are output pixels m -> halo pixel (m / W + r) x (W + 2)
-// + m % W + s for tap (r, s); rows past R' x W (partial last band, tile padding) read a valid
-// pixel and are not stored. Epilogue as conv3x3_fwd_kernel (output rows of a band are contiguous).
-struct HaloGeo {
-  int H, W, C, R, nb;  // image size, channels, output rows per band, bands per image
-};
-
-template <int BN, int WM, int WN, bool STATS>
-__global__ __launch_bounds__(64 * WM * WN, BN == 64 ? 4 : 2) void conv3x3_halo_kernel(
-    const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y,
-    const uint16_t* __restrict__ zeros, int N, HaloGeo hg, float* __restrict__ part, int ntiles, int hrows) {
-  constexpr int BM = 256, NT = 64 * WM * WN, NW = NT / 64;
-  constexpr int BI = BN / 8 / NW;  // weight DMA wave-instructions per tap
-  static_assert(BI * NW * 8 == BN, "weight rows must split evenly over the waves");
-  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* halo = smem;                     // hrows x 128 B
-  uint8_t* ring = smem + hrows * 128;       // 3 x BN x 128 B
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
-  const int wg = dev::xcd_remap(blockIdx.x, gridDim.x);
-  const int nt = wg % ntiles, mt = wg / ntiles;  // mt = image x band
-  const int b = mt / hg.nb, band = mt - b * hg.nb;
-  const int oh0 = band * hg.R, rv = min(hg.R, hg.H - oh0), valid = rv * hg.W;
-  const int n0 = nt * BN, W2 = hg.W + 2, HP = (rv + 2) * W2;
-  const int pos = lane & 7, cbn = hg.C >> 6, K9 = 9 * hg.C;
-
-  // this lane's MFMA A rows -> halo pixel of tap (0, 0)
-  int hb[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = min(wm * WTM + i * 16 + (lane & 15), valid - 1);
-    const int rr = m / hg.W;
-    hb[i] = rr * W2 + (m - rr * hg.W);
-  }
-  int boff[BI];  // (32-bit offsets: host-checked input < 2^31 elements)
-#pragma unroll
-  for (int j = 0; j < BI; ++j) {
-    const int row = (wid * BI + j) * 8 + (lane >> 3);
-    boff[j] = (n0 + row) * K9 + 8 * (pos ^ ((row >> 1) & 7));
-  }
-  const int img = b * hg.H * hg.W;  // first pixel of this image
-  auto issue_halo = [&](int cb) {
-    for (int k = wid; k * 8 < HP; k += NW) {  // (per-wave counts differ: only vmcnt(0) / count-free waits cover it)
-      const int q = k * 8 + (lane >> 3), hr = q / W2, hc = q - hr * W2;
-      const int ih = oh0 - 1 + hr, iw = hc - 1;
-      const bool ok = q < HP && (unsigned)ih < (unsigned)hg.H && (unsigned)iw < (unsigned)hg.W;
-      const uint16_t* src = ok ? X + ((img + ih * hg.W + iw) * hg.C + cb * 64 + 8 * (pos ^ ((q >> 1) & 7))) : zeros;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(halo + k * 1024), 16, 0, 0);
-    }
-  };
-  auto issue_w = [&](int cb, int t, int slot) {
-    uint8_t* Bs = ring + slot * BN * 128;
-    const int wk = t * hg.C + cb * 64;
-#pragma unroll
-    for (int j = 0; j < BI; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(Wt + boff[j] + wk), (lds_ptr_t)(Bs + (wid * BI + j) * 1024), 16,
-                                       0, 0);
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int cb = 0; cb < cbn; ++cb) {
-    if (cb > 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // halo / ring reads done
-    issue_halo(cb);
-    issue_w(cb, 0, 0);
-    issue_w(cb, 1, 1);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      // retire tap t's weights (and, at t = 0, everything issued before them: the halo); the
-      // loads issued after them may stay in flight
-      if (t < 8) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BI) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (t + 2 < 9) issue_w(cb, t + 2, (t + 2) % 3);
-      const int r = t / 3, sx = t - 3 * r, toff = r * W2 + sx;
-      const uint8_t* Bs = ring + (t % 3) * BN * 128;
-      bf16x8 a[2][TM], bb[2][TN];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int ch = h * 4 + (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int row = hb[i] + toff;
-          a[h][i] = *reinterpret_cast<const bf16x8*>(halo + swz3(row, ch));
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bb[h][j] = *reinterpret_cast<const bf16x8*>(Bs + swz3(wn * WTN + j * 16 + (lane & 15), ch));
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[h][j], a[h][i], acc[i][j], 0, 0, 0);
-    }
-  }
-
-  // ---- epilogue: bf16 C tile through LDS, 16-B row stores of the valid rows (+ statistics) ----
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  constexpr int CST = BN * 2 + 16;
-  uint8_t* Cs = smem;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int row = wm * WTM + i * 16 + (lane & 15);
-      const int col = wn * WTN + j * 16 + (lane >> 4) * 4;
-      uint2 pk;
-      pk.x = dev::pack_bf16x2(acc[i][j][0], acc[i][j][1]);
-      pk.y = dev::pack_bf16x2(acc[i][j][2], acc[i][j][3]);
-      *reinterpret_cast<uint2*>(Cs + row * CST + col * 2) = pk;
-    }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  constexpr int CPR = BN / 8;
-  const int cc = tid % CPR;
-  float st_n = 0.f, st_s[8], st_ss[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) st_s[e] = st_ss[e] = 0.f;
-  const u32x4 st_k = *reinterpret_cast<const u32x4*>(Cs + cc * 16);
-  const int64_t y0 = img + (int64_t)oh0 * hg.W;  // the band's first output pixel
-#pragma unroll 4
-  for (int q = tid; q < BM * CPR; q += NT) {
-    const int row = q / CPR;
-    if (row < valid) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + (y0 + row) * N + n0 + cc * 8));
-      if (STATS) {
-        st_n += 1.f;
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const float d0 = __uint_as_float(v[h] << 16) - __uint_as_float(st_k[h] << 16);
-          const float d1 = __uint_as_float(v[h] & 0xffff0000u) - __uint_as_float(st_k[h] & 0xffff0000u);
-          st_s[2 * h] += d0;
-          st_s[2 * h + 1] += d1;
-          st_ss[2 * h] = fmaf(d0, d0, st_ss[2 * h]);
-          st_ss[2 * h + 1] = fmaf(d1, d1, st_ss[2 * h + 1]);
-        }
-      }
-    }
-  }
-  if (!STATS) return;
-#pragma unroll
-  for (int o = CPR; o < 64; o <<= 1) {
-    st_n += __shfl_xor(st_n, o, 64);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      st_s[e] += __shfl_xor(st_s[e], o, 64);
-      st_ss[e] += __shfl_xor(st_ss[e], o, 64);
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  float* red = reinterpret_cast<float*>(smem);
-  float* redn = red + NW * 2 * BN;
-  float* redk = redn + NW * CPR;
-  if (lane < CPR) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[(wid * 2 + 0) * BN + cc * 8 + e] = st_s[e];
-      red[(wid * 2 + 1) * BN + cc * 8 + e] = st_ss[e];
-      if (wid == 0) redk[cc * 8 + e] = __uint_as_float((e & 1) ? (st_k[e >> 1] & 0xffff0000u) : (st_k[e >> 1] << 16));
-    }
-    redn[wid * CPR + cc] = st_n;
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  const int G = gridDim.x / ntiles;
-  for (int c = tid; c < BN; c += NT) {
-    float tn = 0.f, ts = 0.f, tss = 0.f;
-    for (int w = 0; w < NW; ++w) {
-      tn += redn[w * CPR + c / 8];
-      ts += red[(w * 2 + 0) * BN + c];
-      tss += red[(w * 2 + 1) * BN + c];
-    }
-    const float mean_s = ts / tn;
-    part[((int64_t)0 * N + n0 + c) * G + mt] = tn;
-    part[((int64_t)1 * N + n0 + c) * G + mt] = redk[c] + mean_s;
-    part[((int64_t)2 * N + n0 + c) * G + mt] = fmaxf(tss - ts * mean_s, 0.f);
-  }
-}
-
 // W'[c][t][n] = W[n][8 - t][c] (OHWI in, OHWI out): the stride-1 input-gradient weights. One
 // 64x64 (n, c) tile of one tap per block, transposed through LDS.
 __global__ __launch_bounds__(256) void rot_weight_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ out,
@@ -501,36 +310,6 @@ int tile_choice(int N) { return N % 128 == 0 ? 0 : 4; }
 
 }  // namespace
 
-// stride-1 3x3 conv on the halo kernel (N = 64 or 128, 14 <= W <= 128)
-std::vector<at::Tensor> conv3x3_halo(const at::Tensor& x, const at::Tensor& w, bool stats, const uint16_t* zeros) {
-  const int64_t B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), N = w.size(0);
-  TORCH_CHECK((N == 64 || N == 128) && W >= 14 && W <= 128 && C % 64 == 0 && x.numel() < (int64_t(1) << 31),
-              "conv3x3_halo: unsupported shape");
-  // rows per band: as many as fit 256 pixels, spread evenly over the bands of an image
-  const int rmax = (int)std::min<int64_t>(H, 256 / W), nb = (int)((H + rmax - 1) / rmax);
-  const int R = (int)((H + nb - 1) / nb);
-  const int hrows = ((R + 2) * ((int)W + 2) + 7) / 8 * 8;
-  auto y = at::empty({B, N, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int64_t mtiles = B * nb;
-  TORCH_CHECK(mtiles < (int64_t(1) << 31) / (N / 64), "conv3x3_halo: too many tiles");
-  auto part = stats ? at::empty({3, N, mtiles}, x.options().dtype(at::kFloat)) : at::empty({0}, x.options().dtype(at::kFloat));
-  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
-  const HaloGeo hg{(int)H, (int)W, (int)C, R, nb};
-  const int BN = (int)N;
-  const size_t lds = std::max<size_t>((size_t)hrows * 128 + 3 * (size_t)BN * 128, (size_t)256 * (BN * 2 + 16));
-  auto go = [&](auto kern, int nt) {
-    ensure_dyn_lds((const void*)kern, lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)mtiles), dim3(nt), lds, stream,
-                       reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
-                       reinterpret_cast<uint16_t*>(y.data_ptr()), zeros, (int)N, hg,
-                       stats ? part.data_ptr<float>() : nullptr, 1, hrows);
-    XDDP_HIP_CHECK(hipGetLastError());
-  };
-  if (N == 64) { if (stats) go(conv3x3_halo_kernel<64, 4, 2, true>, 512); else go(conv3x3_halo_kernel<64, 4, 2, false>, 512); }
-  else { if (stats) go(conv3x3_halo_kernel<128, 4, 2, true>, 512); else go(conv3x3_halo_kernel<128, 4, 2, false>, 512); }
-  return {y, part};
-}
-
 // the band kernel with an explicit band height (timing scripts, tests)
 std::vector<at::Tensor> conv3x3_band_forward(const at::Tensor& x, const at::Tensor& w, bool stats, int64_t rows,
                                              int64_t cfg) {
@@ -555,36 +334,16 @@ std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w
               "conv3x3_forward: 16-B aligned operands required");
   const int64_t OH = (IH - 1) / stride + 1, OW = (IW - 1) / stride + 1, M = B * OH * OW;
   TORCH_CHECK(M > 0 && M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "conv3x3_forward: bad size");
-  // stride-1 layers whose rows tile into 224 / 196-pixel bands (conv3x3_band.hip); XDDP_C3_BAND=0:
-  // the halo / dense-GEMM kernels below
-  {
-    static const bool band_on = [] {
-      const char* e = std::getenv("XDDP_C3_BAND");
-      return !e || std::atoi(e) != 0;
-    }();
-    if (band_on && stride == 1 && IW >= 14 && (N == 64 || N % 128 == 0) && conv3x3_band_rows(IW, IH, N == 64 ? 224 : 208) > 0 &&
-        x.numel() < (int64_t(1) << 31) && M * N < (int64_t(1) << 31))
-      return conv3x3_band(x, w, stats, 0, zero_line(x));
-  }
-  // wide layers (N >= XDDP_C3_GEMM_MIN_N, default 256; 0 = never) on the dense GEMM's 4-phase
-  // LDS-DMA pipeline with the im2col addressing (gemm.hip ConvGeo)
-  {
-    static const int min_n = [] {
-      const char* e = std::getenv("XDDP_C3_GEMM_MIN_N");
-      return e ? std::atoi(e) : 256;
-    }();
-    if (min_n > 0 && N >= min_n && N % 128 == 0 && x.numel() < (int64_t(1) << 31) && ((C / 64) & (C / 64 - 1)) == 0)
-      return conv3x3_gemm(x, w, stride, stats, zero_line(x));
-  }
-  // narrow stride-1 layers with W >= 14 on the halo kernel (XDDP_C3_HALO=0: never)
-  {
-    static const bool halo_on = [] {
-      const char* e = std::getenv("XDDP_C3_HALO");
-      return !e || std::atoi(e) != 0;
-    }();
-    if (halo_on && stride == 1 && (N == 64 || N == 128) && IW >= 14 && IW <= 128 && x.numel() < (int64_t(1) << 31))
-      return conv3x3_halo(x, w, stats, zero_line(x));
-  }
+  // stride-1 layers whose rows tile into 224 / 196-pixel bands (W = 56 / 28 / 14): the row-band
+  // kernel (conv3x3_band.hip; it replaced r3's whole-row halo kernel: 101 / 62 / 58 vs 108 / 91 /
+  // 70 us forward at the ResNet-50 bs256 shapes)
+  if (stride == 1 && IW >= 14 && (N == 64 || N % 128 == 0) && conv3x3_band_rows(IW, IH, N == 64 ? 224 : 208) > 0 &&
+      x.numel() < (int64_t(1) << 31) && M * N < (int64_t(1) << 31))
+    return conv3x3_band(x, w, stats, 0, zero_line(x));
+  // N >= 256 (the W = 7 stride-1 layer, the stride-2 layers) on the dense GEMM's 4-phase LDS-DMA
+  // pipeline with im2col addressing (gemm.hip ConvGeo)
+  if (N >= 256 && N % 128 == 0 && x.numel() < (int64_t(1) << 31) && ((C / 64) & (C / 64 - 1)) == 0)
+    return conv3x3_gemm(x, w, stride, stats, zero_line(x));
   auto y = at::empty({B, N, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int cfg = tile_choice((int)N);
   const int BM = cfg == 1 || cfg == 3 || cfg == 4 ? 128 : 256, BN = cfg <= 1 ? 128 : 64;

@@ -10,7 +10,8 @@
 // tiles for 256 CUs (77 % of the last round busy). A band of R rows with R·W = 224 (W = 56: R = 4)
 // or 196 (W = 28 / 14 / 7: R = 7 / 14 / 28; one tile = one image at W = 14, four at W = 7) packs
 // the band's pixels contiguously into the tile rows: 0 % / 6 % padding rows, and 3584 / 1024 / 512
-// / 256 x (N / BN) tiles — whole rounds of 2 blocks per CU.
+// / 256 x (N / BN) tiles — whole rounds of 2 blocks per CU. (W = 7 runs the dense-GEMM path of
+// conv3x3.hip: 256 tiles of 4-image bands leave one 4-wave block per CU, 73 vs 63 us.)
 //
 // The input halo of a band is staged ONCE per 64-channel K step and read by all 9 taps (shifted
 // windows): a band that spans images is a list of segments, each staged as its rows plus one row
@@ -21,8 +22,11 @@
 // image boundary. Operands go global -> LDS with global_load_lds_dwordx4 (LDS-DMA, rows of 128 B =
 // 64 channels, chunk XOR-swizzled by (row >> 1) & 7 through pre-swizzled source addresses); the
 // tap's weights (BN x 64) stream through a RING-slot ring with counted `s_waitcnt vmcnt` + raw
-// s_barrier. Four waves (WM x WN) of TM x TN 16x16x32 MFMA tiles; two blocks per CU (LDS <= 80 KB
-// a block), so one block's halo wait and epilogue run under the other's MFMAs.
+// s_barrier (N = 64), or — N % 128 == 0 — go straight from global memory (L2-resident) into each
+// wave's registers per 32-deep half step, three half steps ahead, so the 9 taps of a 64-channel
+// step need no barrier at all (only the halo reload between channel steps does). Four waves
+// (WM x WN) of TM x TN 16x16x32 MFMA tiles; two blocks per CU, so one block's halo wait and
+// epilogue run under the other's MFMAs.
 //
 // Epilogue as conv3x3.hip: the bf16 C tile through LDS, 16-B row stores of the valid pixels (the
 // band's output pixels are contiguous in NHWC memory), BatchNorm (count, mean, M2) partials per
@@ -319,12 +323,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv3x3_band_kernel(
 }  // namespace
 
 // Band geometry for a stride-1 3x3 conv: rows per band for a tile of bm pixels (0: not covered).
-// R·W = 224 (W = 56) or 196 (W = 28 / 14) output pixels, two images at W = 7 (module comment).
+// R·W = 224 (W = 56) or 196 (W = 28 / 14 / 7) output pixels (module comment).
 int conv3x3_band_rows(int64_t W, int64_t H, int64_t bm) {
   int r = 0;
-  if (W == 56) r = 4;
-  else if (W == 7) r = 2 * (int)H;
+  if (W == 56) r = (int)(bm / 56);
   else if (W <= 28 && 196 % W == 0) r = (int)(196 / W);
+  (void)H;
   return r > 0 && r * W <= bm ? r : 0;
 }
 
@@ -347,15 +351,18 @@ std::vector<at::Tensor> conv3x3_band(const at::Tensor& x, const at::Tensor& w, b
               "conv3x3_band: 16-B aligned operands required");
   // configurations {TM, WM, TN, WN, RING}: tile BM = 16·TM·WM pixels x BN = 16·TN·WN channels
   struct Cfg { int tm, wm, tn, wn, ring; };
+  // (r5 A/Bs at the ResNet-50 bs256 shapes, scripts/c3_time.py, profiles/r5_conv3x3_band.txt: for N = 64
+  // weights in registers (100.7 / 87.2 us) or 448-row tiles (95.9 / 87.1) gained nothing over the
+  // ring; for N % 128 == 0 the registers beat the two-slot ring (62.0 / 59.1 vs 67.6 / 63.0 us at
+  // C128, 57.7 / 55.4 vs 62.8 / 59.9 at C256: no barrier per tap); 112-row two-image bands at
+  // W = 7 lost to the dense-GEMM path, 72.9 vs 63.0 us)
   static constexpr Cfg kCfgs[] = {
       {7, 2, 2, 2, 3},   // 0: N = 64, 224 x 64 tiles, waves 2 x 2 of 112 x 32, three-slot weight ring
-      {7, 2, 2, 2, 0},   // 1: the same, weights in registers
-      {13, 1, 2, 4, 2},  // 2: N % 128 == 0, 208 x 128 tiles (196-pixel bands), waves 1 x 4 of 208 x 32
-      {7, 1, 2, 4, 2},   // 3: N % 128 == 0, 112 x 128 tiles (W = 7: two-image bands), waves 1 x 4
-      {13, 1, 2, 4, 0},  // 4: as 2, weights in registers
+      {13, 1, 2, 4, 0},  // 1: N % 128 == 0, 208 x 128 tiles (196-pixel bands), waves 1 x 4 of
+                         //    208 x 32, weights in registers (per 32-deep half step, 3 deep)
   };
-  if (cfg < 0) cfg = N == 64 ? 0 : (W <= 7 ? 3 : 2);
-  TORCH_CHECK(cfg < 5, "conv3x3_band: unknown configuration ", cfg);
+  if (cfg < 0) cfg = N == 64 ? 0 : 1;
+  TORCH_CHECK(cfg < 2, "conv3x3_band: unknown configuration ", cfg);
   const Cfg cf = kCfgs[cfg];
   const int BM = 16 * cf.tm * cf.wm, BN = 16 * cf.tn * cf.wn, ntiles = (int)(N / BN);
   TORCH_CHECK(N % BN == 0, "conv3x3_band: N must be a multiple of the configuration's ", BN, " channels");
@@ -393,13 +400,8 @@ std::vector<at::Tensor> conv3x3_band(const at::Tensor& x, const at::Tensor& w, b
     if (stats) go(conv3x3_band_kernel<TM_, WM_, TN_, WN_, true, RING_>, RING_);    \
     else go(conv3x3_band_kernel<TM_, WM_, TN_, WN_, false, RING_>, RING_);         \
   } while (0)
-  switch (cfg) {
-    case 0: XDDP_BAND(7, 2, 2, 2, 3); break;
-    case 1: XDDP_BAND(7, 2, 2, 2, 0); break;
-    case 2: XDDP_BAND(13, 1, 2, 4, 2); break;
-    case 3: XDDP_BAND(7, 1, 2, 4, 2); break;
-    default: XDDP_BAND(13, 1, 2, 4, 0); break;
-  }
+  if (cfg == 0) XDDP_BAND(7, 2, 2, 2, 3);
+  else XDDP_BAND(13, 1, 2, 4, 0);
 #undef XDDP_BAND
   return {y, part};
 }

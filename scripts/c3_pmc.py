@@ -20,8 +20,7 @@ for c, hw in ((64, 56), (128, 28), (256, 14), (512, 7)):
         memory_format=torch.channels_last)
     rot = C.conv3x3_rot_weight(w)
     for fn in (lambda: C.conv3x3_forward(x, w, 1, True), lambda: C.conv3x3_forward(x, rot, 1, False),
-               lambda: C.conv3x3_band_forward(x, w, True, 0, 0), lambda: C.conv3x3_band_forward(x, rot, False, 0, 0),
-               lambda: C.conv3x3_band_forward(x, w, True, 0, 1), lambda: C.conv3x3_band_forward(x, rot, False, 0, 1),
+               lambda: C.conv3x3_band_forward(x, w, True, 0, -1), lambda: C.conv3x3_band_forward(x, rot, False, 0, -1),
                lambda: C.conv3x3_wgrad_patch(x, x, 1, w)):
         for _ in range(3):
             fn()

@@ -1,8 +1,8 @@
 #!/usr/bin/env python
 """Per-call time of the stride-1 3x3 conv kernels at the ResNet-50 bs256 shapes: the dispatcher's
-path (conv3x3_forward: band / halo / dense-GEMM by XDDP_C3_BAND, XDDP_C3_HALO...) and the row-band
-kernel called directly (conv3x3_band_forward, optional band heights), forward with BN statistics
-and the input gradient (no statistics), plus the weight gradient; us per call and TF/s.
+path (conv3x3_forward: row-band kernel or dense-GEMM path) and the row-band kernel called directly
+(conv3x3_band_forward, optional band heights and configurations), forward with BN statistics and
+the input gradient (no statistics), plus the weight gradient; us per call and TF/s.
 
 usage: python scripts/c3_time.py [--iters 20] [--rows 56:4,28:7,...] [--batch 256]"""
 import argparse

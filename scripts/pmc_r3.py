@@ -58,7 +58,7 @@ for cin, hw in ((64, 56), (128, 28), (256, 14), (512, 7)):
     x, w = bf(B, cin, hw, hw), bf(cin, cin, 3, 3, scale=(9 * cin) ** -0.5)
     m = B * hw * hw
     fl, by = 2.0 * m * cin * 9 * cin, 2.0 * (2 * x.numel() + w.numel())
-    pat = "conv3x3_halo_kernel" if cin <= 128 else "gemm_nt_kernel"
+    pat = "conv3x3_band_kernel" if cin <= 256 else "gemm_nt_kernel"
     run(f"conv3x3 fwd C{cin} {hw}x{hw}", pat, fl, by, lambda: C.conv3x3_forward(x, w, 1, True))
     wr = C.conv3x3_rot_weight(w)
     run(f"conv3x3 dgrad C{cin} {hw}x{hw}", pat, fl, by, lambda: C.conv3x3_forward(x, wr, 1, False))

@@ -27,10 +27,10 @@ def _cl(t):
     (2, 128, 9, 11, 384, 1, 0.0),    # three 128-wide N tiles, odd spatial size
     (2, 256, 15, 13, 256, 2, 0.0),   # strided, odd input size
     (2, 192, 8, 8, 256, 1, 0.0),     # C / 64 = 3 (not a power of two): the conv3x3.hip kernel
-    # N <= 128, stride 1, W >= 14: the halo kernel (R output rows per block, one staged halo)
+    # stride 1, W = 56 / 28 / 14: the row-band kernel (conv3x3_band.hip)
     (2, 64, 56, 56, 64, 1, 30.0),    # layer-1 shape: 4-row bands
     (2, 128, 28, 28, 128, 1, 0.0),   # layer-2 shape: two 64-channel steps, 7-row bands
-    (3, 128, 17, 23, 64, 1, 0.0),    # ragged: last band shorter, odd width
+    (3, 128, 17, 23, 64, 1, 0.0),    # odd width: the conv3x3.hip kernel
     (1, 64, 15, 130, 64, 1, 0.0),    # W > 128: the conv3x3.hip kernel
 ])
 def test_conv3x3_forward_matches_conv2d(b, cin, h, w, cout, s, off):
@@ -154,17 +154,15 @@ def test_conv3x3_wgrad_patch_matches_conv2d(b, cin, h, w, cout, s):
 
 
 @pytest.mark.parametrize("b,cin,h,w,cout,rows,cfg,off", [
-    (2, 64, 56, 56, 64, 4, 0, 30.0),     # layer-1 band: 4 rows = 224 pixels, N = 64 tiles
-    (2, 64, 56, 56, 64, 4, 1, 0.0),      # the same, weights in registers
-    (3, 128, 28, 28, 128, 7, 2, 0.0),    # layer-2 band: 7 rows = 196 pixels, 208-row tile
-    (3, 128, 28, 28, 256, 7, 4, 0.0),    # the same, weights in registers (half-step buffers)
-    (2, 256, 7, 7, 256, 28, 4, 5.0),     # registers, bands over four images, 4 channel steps
-    (3, 256, 14, 14, 256, 14, 2, 0.0),   # layer-3: one band = one image, two N tiles
-    (5, 512, 7, 7, 512, 28, 2, 0.0),     # a band spans four images; partial last band
-    (5, 512, 7, 7, 512, 14, 3, 0.0),     # layer-4 default: two-image bands, 112-row tiles
-    (3, 128, 7, 7, 256, 29, 2, 10.0),    # bands start mid-image: first segment partial, 5 segments
+    (2, 64, 56, 56, 64, 4, 0, 30.0),     # layer-1 band: 4 rows = 224 pixels, N = 64 tiles, weight ring
+    (3, 128, 28, 28, 128, 7, 1, 0.0),    # layer-2 band: 7 rows = 196 pixels, 208-row tile, B in registers
+    (3, 128, 28, 28, 256, 7, 1, 0.0),    # two N tiles
+    (2, 256, 7, 7, 256, 28, 1, 5.0),     # bands over four images, 4 channel steps
+    (3, 256, 14, 14, 256, 14, 1, 0.0),   # layer-3: one band = one image, two N tiles
+    (5, 512, 7, 7, 512, 28, 1, 0.0),     # a band spans four images; partial last band
+    (3, 128, 7, 7, 256, 29, 1, 10.0),    # bands start mid-image: first segment partial, 5 segments
     (2, 64, 10, 12, 64, 3, 0, 0.0),      # ragged: 20 rows in bands of 3, crossing an image edge
-    (1, 128, 5, 9, 128, 23, 2, 0.0),     # more rows per band than the batch has (one partial band)
+    (1, 128, 5, 9, 128, 23, 1, 0.0),     # more rows per band than the batch has (one partial band)
 ])
 def test_conv3x3_band_matches_conv2d(b, cin, h, w, cout, rows, cfg, off):
     """Row-band kernel (conv3x3_band.hip) with explicit band heights and configurations: bands
