@@ -59,8 +59,9 @@ struct Dg2Geo {
   int start[4];      // first block tile of each phase
 };
 
-// TAPS = 9: the 3x3 conv (pad 1). TAPS = 1: a 1x1 conv (pad 0, stride 1 or 2) through the same
-// 3-stage LDS-DMA pipeline — the K loop of the register-staged 1x1 GEMM (conv_gemm.hip) waits a
+// TAPS = 9: the 3x3 conv (pad 1). (TAPS = 1, a 1x1 conv on this pipeline, lost its r2 A/B to the
+// register-staged 1x1 GEMM and the deep-K LDS-DMA GEMM; its entry point was removed in r5.) Earlier
+// rationale: the K loop of the register-staged 1x1 GEMM (conv_gemm.hip) waits a
 // full memory latency per 64-deep step, which dominates the deep-K / few-tile layers (ResNet-50
 // layer3/4: K = 1024..2048 with 400-800 output tiles).
 template <int BM, int BN, int WM, int WN, bool STATS, int TAPS = 9, bool DG2 = false>
@@ -372,56 +373,6 @@ std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w
     default: TORCH_CHECK(false, "conv3x3_forward: bad tile config");
   }
 #undef XDDP_C3
-  return {y, part};
-}
-
-// 1x1 conv (stride 1 or 2) on the 3-stage LDS-DMA pipeline: x [B, C, IH, IW] bf16 channels_last,
-// w [N, C, 1, 1] bf16; returns {y channels_last, stats partials [3, N, mtiles] group-minor}.
-// Tiles: 256x128 (8 waves, 1 block/CU) when that still gives >= 2 blocks per CU, else 128x64
-// (4 waves, 2 blocks/CU); tile = 0 | 4 forces one (tests).
-std::vector<at::Tensor> conv1x1_dma_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats,
-                                            int64_t tile) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
-                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "conv1x1_dma_forward: x must be a bf16 channels_last CUDA tensor");
-  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 1 && w.size(3) == 1 &&
-                  w.size(1) == x.size(1),
-              "conv1x1_dma_forward: w must be bf16 [N, C, 1, 1]");
-  TORCH_CHECK(stride == 1 || stride == 2, "conv1x1_dma_forward: stride 1 or 2");
-  auto wc = w.contiguous();  // [N][C] either memory format (1x1: same bytes)
-  const int64_t B = x.size(0), C = x.size(1), IH = x.size(2), IW = x.size(3), N = w.size(0);
-  TORCH_CHECK(C % 64 == 0 && N % 64 == 0, "conv1x1_dma_forward: channel counts must be multiples of 64");
-  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) % 16) == 0 && (reinterpret_cast<uintptr_t>(wc.data_ptr()) % 16) == 0,
-              "conv1x1_dma_forward: 16-B aligned operands required");
-  const int64_t OH = (IH - 1) / stride + 1, OW = (IW - 1) / stride + 1, M = B * OH * OW;
-  TORCH_CHECK(M > 0 && M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "conv1x1_dma_forward: bad size");
-  auto y = at::empty({B, N, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  int cfg = tile == 0 || tile == 4 ? (int)tile : -1;
-  if (N % 128 != 0) cfg = 4;
-  if (cfg < 0) cfg = ((M + 255) / 256) * (N / 128) >= 512 ? 0 : 4;
-  const int BM = cfg == 0 ? 256 : 128, BN = cfg == 0 ? 128 : 64;
-  const int mtiles = (int)((M + BM - 1) / BM), ntiles = (int)(N / BN);
-  auto part = stats ? at::empty({3, N, mtiles}, x.options().dtype(at::kFloat)) : at::empty({0}, x.options().dtype(at::kFloat));
-  auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
-  Geo3 geo{(int)IH, (int)IW, (int)OH, (int)OW, (int)stride};
-  const uint16_t* zeros = zero_line(x);
-  auto go = [&](auto kern, int nt, size_t lds) {
-    ensure_dyn_lds((const void*)kern, lds);
-    hipLaunchKernelGGL(kern, dim3(mtiles * ntiles), dim3(nt), lds, stream,
-                       reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(wc.data_ptr()),
-                       reinterpret_cast<uint16_t*>(y.data_ptr()), zeros, (int)M, (int)N, (int)C, geo,
-                       stats ? part.data_ptr<float>() : nullptr, ntiles, Dg2Geo{});
-    XDDP_HIP_CHECK(hipGetLastError());
-  };
-#define XDDP_C1(BM_, BN_, WM_, WN_)                                                                             \
-  do {                                                                                                           \
-    const size_t lds = (size_t)kStages * (BM_ + BN_) * 128;                                                      \
-    if (stats) go(conv3x3_fwd_kernel<BM_, BN_, WM_, WN_, true, 1>, 64 * WM_ * WN_, lds);                        \
-    else go(conv3x3_fwd_kernel<BM_, BN_, WM_, WN_, false, 1>, 64 * WM_ * WN_, lds);                             \
-  } while (0)
-  if (cfg == 0) XDDP_C1(256, 128, 4, 2);
-  else XDDP_C1(128, 64, 2, 2);
-#undef XDDP_C1
   return {y, part};
 }
 

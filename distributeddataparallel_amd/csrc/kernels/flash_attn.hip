@@ -759,12 +759,9 @@ std::vector<at::Tensor> flash_attn_forward(const at::Tensor& q, const at::Tensor
   };
 #define XDDP_FA(D_, C_) \
   if (nw == 8) go(fa_fwd_kernel<D_, C_, 8>); else go(fa_fwd_kernel<D_, C_, 4>)
-  // XDDP_FA_WHOLE=0: the double-buffered tile loop for the short non-causal heads too (A/Bs)
-  static const bool whole_ok = [] {
-    const char* e = std::getenv("XDDP_FA_WHOLE");
-    return !(e && e[0] == '0');
-  }();
-  const bool whole = whole_ok && D == 64 && !causal && Sk <= 4 * kBK;
+  // short non-causal D = 64 heads (ViT: 197 keys) stage all of K / V at once (r3 A/B vs the
+  // double-buffered tile loop: profiles/r3_flash_whole_kv_ab.txt)
+  const bool whole = D == 64 && !causal && Sk <= 4 * kBK;
   if (D == 128) { if (causal) { XDDP_FA(128, true); } else { XDDP_FA(128, false); } }
   else if (whole) { if (nw == 8) go(fa_fwd_kernel<64, false, 8, true>); else go(fa_fwd_kernel<64, false, 4, true>); }
   else { if (causal) { XDDP_FA(64, true); } else { XDDP_FA(64, false); } }

@@ -493,7 +493,6 @@ void launch_gemm(const at::Tensor& a, const at::Tensor& b, uint16_t* y, uint16_t
 // Tile width: 256 x 256 unless the 256 x 128 grid fills the CUs' last round better (one block
 // per CU: a 256 x 256 grid of 800 tiles on 256 CUs runs 4 rounds, the last 1/8 full).
 int pick_bn(int64_t M, int64_t N, int cus) {
-  if (const char* e = std::getenv("XDDP_GEMM_BN")) return std::atoi(e) == 128 || N % 256 ? 128 : 256;
   if (N % 256) return 128;
   const int64_t mt = (M + kBM - 1) / kBM;
   const int64_t r256 = (mt * (N / 256) + cus - 1) / cus, r128 = (mt * (N / 128) + cus - 1) / cus;

@@ -53,8 +53,6 @@ at::Tensor bn_backward_elem(const at::Tensor& g, const at::Tensor& x, const at::
 std::vector<at::Tensor> gemm_nt(const at::Tensor& a, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                                 int64_t epi, const c10::optional<at::Tensor>& residual,
                                 const c10::optional<at::Tensor>& out);
-std::vector<at::Tensor> conv1x1_dma_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats,
-                                            int64_t tile);
 std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride, bool stats);
 // the same on the dense GEMM pipeline (gemm.hip; N % 128 == 0, input < 2^31 elements); zeros: a
 // 256-B zero line on the device
@@ -102,9 +100,6 @@ at::Tensor global_avg_pool_backward(const at::Tensor& g, const at::Tensor& x_lik
 // (csrc/kernels/stem_conv.hip)
 std::vector<at::Tensor> stem_conv_forward(const at::Tensor& x, const at::Tensor& w);
 at::Tensor stem_conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w_like);
-at::Tensor stem_conv_wgrad_fused(const at::Tensor& dyp, const c10::optional<at::Tensor>& dyp2, const at::Tensor& idx,
-                                 const at::Tensor& y, const at::Tensor& x, const at::Tensor& w_like,
-                                 const at::Tensor& ss, const at::Tensor& mean, const at::Tensor& coef);
 // ResNet stem bn1 -> ReLU -> maxpool(3, 2, 1) without the normalized activation (csrc/kernels/pool.hip)
 std::vector<at::Tensor> stem_pool_forward(const at::Tensor& x, const at::Tensor& ss);
 at::Tensor stem_pool_bn_backward(const at::Tensor& dy, const c10::optional<at::Tensor>& dy2, const at::Tensor& idx,

@@ -48,8 +48,6 @@ void bind_norm_kernels(py::module_& m) {
   m.def("bn_stats_from_partials", &bn_stats_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"),
         py::arg("momentum"), py::arg("cumulative"), py::arg("eps"), py::arg("group_minor") = false);
-  m.def("conv1x1_dma_forward", &conv1x1_dma_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"),
-        py::arg("tile") = -1);
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("w"), py::arg("bias") = py::none(), py::arg("epi") = 0,
         py::arg("residual") = py::none(), py::arg("out") = py::none(),
         "y = a @ w.T (bf16, MFMA LDS-DMA GEMM) with epilogue 0 none | 1 +bias | 2 +bias->GELU | 3 +residual | "
@@ -65,8 +63,6 @@ void bind_norm_kernels(py::module_& m) {
   m.def("swiglu_backward", &swiglu_backward, py::arg("grad"), py::arg("a"), py::arg("b"));
   m.def("stem_conv_forward", &stem_conv_forward, py::arg("x"), py::arg("w"));
   m.def("stem_conv_wgrad", &stem_conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("w_like"));
-  m.def("stem_conv_wgrad_fused", &stem_conv_wgrad_fused, py::arg("dyp"), py::arg("dyp2"), py::arg("idx"), py::arg("y"),
-        py::arg("x"), py::arg("w_like"), py::arg("scale_shift"), py::arg("mean"), py::arg("coef"));
   m.def("stem_pool_forward", &stem_pool_forward, py::arg("x"), py::arg("scale_shift"));
   m.def("stem_pool_bn_backward", &stem_pool_bn_backward, py::arg("dy"), py::arg("dy2"), py::arg("idx"), py::arg("x"),
         py::arg("scale_shift"), py::arg("mean"), py::arg("coef") = py::none());

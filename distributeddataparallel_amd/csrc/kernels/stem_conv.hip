@@ -264,36 +264,18 @@ __device__ __forceinline__ v4s lds_tr16(const uint8_t* p) {
 // one half-wave transposed read) land in distinct blocks
 __device__ __forceinline__ int dswz(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 1); }
 
-// FUSED: dY is not read from memory but built per tile from the stem's pooled gradient — the
-// backward of bn1 -> ReLU -> maxpool(3, 2, 1) (pool.hip stem_pool_bn_bwd ELEM pass) fused into
-// this kernel's operand staging, so the conv-output gradient (411 MB at bs256) is never written.
-struct PoolBwd {
-  const uint16_t* dyp;   // pooled-output gradient [N, OHp, OWp, 64]
-  const uint16_t* dyp2;  // second consumer's gradient (or null)
-  const uint8_t* idx;    // byte argmax [N, OHp, OWp, 64]
-  const uint16_t* y;     // conv output (BN input) [N, OH, OW, 64]
-  const float* coef6;    // [6][64]: scale, shift, mean, k1, k2, k3 - k2·mean (dY = k1·g + k2·y + k3')
-  int OHp, OWp;
-};
-
 __device__ __forceinline__ float bfx(uint32_t w, int hi) { return __uint_as_float(hi ? (w & 0xffff0000u) : (w << 16)); }
 
-template <bool FUSED>
-__global__ __launch_bounds__(256, FUSED ? 1 : 2) void stem_conv_wgrad_kernel(const uint16_t* __restrict__ dy,
+__global__ __launch_bounds__(256, 2) void stem_conv_wgrad_kernel(const uint16_t* __restrict__ dy,
                                                                  const uint16_t* __restrict__ x,
                                                                  const uint16_t* __restrict__ zeros,
                                                                  float* __restrict__ ws, int N, int H, int W, int OH,
-                                                                 int OW, int tiles_h, int tiles_w, PoolBwd pb) {
+                                                                 int OW, int tiles_h, int tiles_w) {
   __shared__ __attribute__((aligned(16))) uint8_t Dl[2][kDBytes];
   __shared__ __attribute__((aligned(16))) uint8_t Hl[2][kWHalo];
-  __shared__ __attribute__((aligned(16))) float Cf[FUSED ? 6 * 64 : 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l15 = lane & 15, l4 = lane >> 4;
   const int cp = wv & 1, nh = wv >> 1;
   const int ntiles = N * tiles_h * tiles_w;
-  if (FUSED) {
-    for (int i = tid; i < 6 * 64; i += 256)  // k3' = k3 - k2·mean, the fma stem_pool_bn_backward uses
-      Cf[i] = i < 320 ? pb.coef6[i] : fmaf(-pb.coef6[i - 64], pb.coef6[i - 192], pb.coef6[i]);
-  }
 
   auto tile_pos = [&](int tile, int& n, int& oh0, int& ow0) {
     const int tw = tile % tiles_w, th = (tile / tiles_w) % tiles_h;
@@ -314,88 +296,6 @@ __global__ __launch_bounds__(256, FUSED ? 1 : 2) void stem_conv_wgrad_kernel(con
       const uint16_t* src = (oh < OH && ow < OW) ? dy + (((int64_t)n * OH + oh) * OW + ow) * 64 + co : zeros;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(Dl[buf] + q * 1024), 16, 0, 0);
     }
-  };
-  // FUSED staging: thread = one 2x2 quad of conv-output pixels x 8 channels (32 quads x 8 chunks
-  // per 8 x 16 tile); the quad is covered by pooling windows (t|t+1, u|u+1)
-  const int qr = (tid >> 3) >> 3, qc = (tid >> 3) & 7, c8 = tid & 7;
-  uint32_t pk_idx[4][2];
-  dev::u32x4 pk_g[4], pk_g2[4];
-  auto load_pool = [&](int tile) {
-    int n, oh0, ow0;
-    tile_pos(tile, n, oh0, ow0);
-    const int t = (oh0 >> 1) + qr, u = (ow0 >> 1) + qc;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const int ohp = min(t + (d >> 1), pb.OHp - 1), owp = min(u + (d & 1), pb.OWp - 1);
-      const int64_t o = (((int64_t)n * pb.OHp + ohp) * pb.OWp + owp) * 64 + c8 * 8;
-      const uint2 ix = *reinterpret_cast<const uint2*>(pb.idx + o);
-      pk_idx[d][0] = ix.x;
-      pk_idx[d][1] = ix.y;
-      pk_g[d] = *reinterpret_cast<const dev::u32x4*>(pb.dyp + o);
-      pk_g2[d] = pb.dyp2 ? *reinterpret_cast<const dev::u32x4*>(pb.dyp2 + o) : dev::u32x4{0, 0, 0, 0};
-    }
-  };
-  auto produce = [&](int tile, int buf) {
-    dev::u32x4 pk_y[4];
-    int n, oh0, ow0;
-    tile_pos(tile, n, oh0, ow0);
-    const int t = (oh0 >> 1) + qr, u = (ow0 >> 1) + qc;
-    // the BN input of the quad, loaded here rather than prefetched (keeps the prefetch to the
-    // pooled gradient: the register budget of the MFMA loop)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const int h = min(2 * t + (d >> 1), OH - 1), w = min(2 * u + (d & 1), OW - 1);
-      pk_y[d] = *reinterpret_cast<const dev::u32x4*>(pb.y + (((int64_t)n * OH + h) * OW + w) * 64 + c8 * 8);
-    }
-    // dy + dy2 at storage precision, as autograd sums the pool output's two uses in the unfused
-    // stack (and as the materializing stem_pool_bn_backward does)
-    if (pb.dyp2) {
-#pragma unroll
-      for (int d = 0; d < 4; ++d)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          pk_g[d][e] = dev::pack_bf16x2(bfx(pk_g[d][e], 0) + bfx(pk_g2[d][e], 0), bfx(pk_g[d][e], 1) + bfx(pk_g2[d][e], 1));
-    }
-    // one pixel of the quad at a time (8 live sums): pixel (2t + a, 2u + b) sits at offset
-    // (1 + a - 2dh, 1 + b - 2dw) of window (t + dh, u + dw)
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        float acc[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const int dh = d >> 1, dw = d & 1, kh = 1 + a - 2 * dh, kw = 1 + b - 2 * dw;
-          if (kh < 0 || kw < 0) continue;  // compile-time after unrolling
-          const bool win = t + dh < pb.OHp && u + dw < pb.OWp;
-          const uint32_t pos = (uint32_t)(kh * 3 + kw);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const uint32_t am = (pk_idx[d][j >> 2] >> (8 * (j & 3))) & 0xffu;
-            if (win && am == pos) acc[j] += bfx(pk_g[d][j >> 1], j & 1);
-          }
-        }
-        const int row = (2 * qr + a) * 16 + 2 * qc + b;  // pixel index inside the 8 x 16 tile
-        const bool valid = oh0 + 2 * qr + a < OH && ow0 + 2 * qc + b < OW;
-        uint32_t o4[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float r2[2];
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            const int j = 2 * e + hh, c = c8 * 8 + j;
-            const float yv = bfx(pk_y[a * 2 + b][e], hh);
-            // g at the precision the unfused maxpool backward stores it, masked by the ReLU
-            const float g = fmaf(yv, Cf[c], Cf[64 + c]) > 0.f ? bf16r(acc[j]) : 0.f;
-            r2[hh] = valid ? fmaf(Cf[192 + c], g, fmaf(Cf[256 + c], yv, Cf[320 + c])) : 0.f;
-          }
-          o4[e] = dev::pack_bf16x2(r2[0], r2[1]);
-        }
-        const int unit = (((c8 >> 1) ^ dswz(row)) * 2) + (c8 & 1);
-        *reinterpret_cast<uint4*>(Dl[buf] + row * 128 + unit * 16) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
-      }
   };
   uint2 stage[kWSlots];
   auto load_halo = [&](int tile) {
@@ -426,13 +326,7 @@ __global__ __launch_bounds__(256, FUSED ? 1 : 2) void stem_conv_wgrad_kernel(con
 
   int k = 0;
   if ((int)blockIdx.x < ntiles) {
-    if (FUSED) {
-      __syncthreads();  // the coefficient table
-      load_pool(blockIdx.x);
-      produce(blockIdx.x, 0);
-    } else {
-      issue_dy(blockIdx.x, 0);
-    }
+    issue_dy(blockIdx.x, 0);
     load_halo(blockIdx.x);
   }
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++k) {
@@ -447,8 +341,7 @@ __global__ __launch_bounds__(256, FUSED ? 1 : 2) void stem_conv_wgrad_kernel(con
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     const int next = tile + gridDim.x;
     if (next < ntiles) {
-      if (FUSED) load_pool(next);  // in flight during this tile's MFMAs, turned into dY after them
-      else issue_dy(next, buf ^ 1);
+      issue_dy(next, buf ^ 1);
       load_halo(next);
     }
     const uint8_t* D = Dl[buf];
@@ -478,9 +371,6 @@ __global__ __launch_bounds__(256, FUSED ? 1 : 2) void stem_conv_wgrad_kernel(con
         for (int c = 0; c < 2; ++c) acc[c][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b, acc[c][jj], 0, 0, 0);
       }
     }
-    // (FUSED) the next tile's dY into the other buffer: every wave finished reading it at the
-    // barrier above, and the next barrier publishes it
-    if (FUSED && next < ntiles) produce(next, buf ^ 1);
   }
   // partial dW of this workgroup: lane holds co = cf*16 + 4*l4 + i, k = j*16 + l15
   float* out = ws + (int64_t)blockIdx.x * 64 * 224;
@@ -568,56 +458,6 @@ namespace {
 at::Tensor stem_wgrad_reduce(const at::Tensor& ws, int grid, const at::Tensor& w_like, hipStream_t stream);
 }
 
-// The stem weight gradient straight from the pooled-output gradient: dY = the backward of
-// bn1 -> ReLU -> maxpool(3, 2, 1) is formed per tile in the kernel (stem_conv_wgrad_kernel<true>).
-// dyp / dyp2 [N, 64, OHp, OWp] bf16 (dyp2 optional), idx the byte argmax, y the conv output
-// [N, 64, OH, OW], ss [2, 64] BN scale/shift, mean [64], coef [3, 64] unfolded BN-backward coefficients.
-at::Tensor stem_conv_wgrad_fused(const at::Tensor& dyp_in, const c10::optional<at::Tensor>& dyp2_in,
-                                 const at::Tensor& idx, const at::Tensor& y, const at::Tensor& x,
-                                 const at::Tensor& w_like, const at::Tensor& ss, const at::Tensor& mean,
-                                 const at::Tensor& coef) {
-  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.size(1) == 3 && x.scalar_type() == at::kBFloat16 &&
-                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "stem_conv_wgrad_fused: x must be a channels_last bf16 [N, 3, H, W] GPU tensor");
-  const int N = (int)x.size(0), H = (int)x.size(2), W = (int)x.size(3);
-  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1, OHp = (OH - 1) / 2 + 1, OWp = (OW - 1) / 2 + 1;
-  TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.size(0) == N && y.size(1) == 64 && y.size(2) == OH &&
-                  y.size(3) == OW && y.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "stem_conv_wgrad_fused: y must be the channels_last bf16 conv output");
-  auto dyp = dyp_in.contiguous(at::MemoryFormat::ChannelsLast);
-  at::Tensor dyp2 = (dyp2_in.has_value() && dyp2_in->defined()) ? dyp2_in->contiguous(at::MemoryFormat::ChannelsLast)
-                                                                  : at::Tensor();
-  TORCH_CHECK(dyp.scalar_type() == at::kBFloat16 && dyp.size(0) == N && dyp.size(1) == 64 && dyp.size(2) == OHp &&
-                  dyp.size(3) == OWp && idx.numel() == dyp.numel() && idx.scalar_type() == at::kByte,
-              "stem_conv_wgrad_fused: pooled gradient / argmax shapes");
-  if (dyp2.defined()) TORCH_CHECK(dyp2.sizes() == dyp.sizes() && dyp2.scalar_type() == dyp.scalar_type(), "dyp2");
-  TORCH_CHECK(ss.numel() == 128 && mean.numel() == 64 && coef.numel() == 192 && ss.scalar_type() == at::kFloat &&
-                  mean.scalar_type() == at::kFloat && coef.scalar_type() == at::kFloat,
-              "stem_conv_wgrad_fused: ss [2, 64], mean [64], coef [3, 64] float");
-  TORCH_CHECK(w_like.dim() == 4 && w_like.size(0) == 64 && w_like.size(1) == 3 && w_like.size(2) == 7 &&
-                  w_like.size(3) == 7,
-              "stem_conv_wgrad_fused: w must be [64, 3, 7, 7]");
-  auto coef6 = at::cat({ss.reshape({2, 64}), mean.reshape({1, 64}), coef.reshape({3, 64})}, 0).contiguous();
-  const int tiles_h = (OH + kWT - 1) / kWT, tiles_w = (OW + 15) / 16;
-  const int64_t ntiles = (int64_t)N * tiles_h * tiles_w;
-  TORCH_CHECK(ntiles > 0 && ntiles < (1 << 30), "stem_conv_wgrad_fused: bad size");
-  int dev_id = x.device().index(), cus = 0;
-  XDDP_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_id));
-  // one 4-wave workgroup per CU: the prefetched pooled gradient needs more than the 256 VGPRs of
-  // two waves per SIMD
-  const int grid = (int)std::min<int64_t>(ntiles, (int64_t)cus);
-  auto ws = at::empty({grid, 64, 224}, x.options().dtype(at::kFloat));
-  auto stream = c10::hip::getCurrentHIPStream(dev_id).stream();
-  PoolBwd pb{reinterpret_cast<const uint16_t*>(dyp.data_ptr()),
-             dyp2.defined() ? reinterpret_cast<const uint16_t*>(dyp2.data_ptr()) : nullptr, idx.data_ptr<uint8_t>(),
-             reinterpret_cast<const uint16_t*>(y.data_ptr()), coef6.data_ptr<float>(), OHp, OWp};
-  hipLaunchKernelGGL(stem_conv_wgrad_kernel<true>, dim3(grid), dim3(256), 0, stream, nullptr,
-                     reinterpret_cast<const uint16_t*>(x.data_ptr()), nullptr, ws.data_ptr<float>(), N, H, W, OH, OW,
-                     tiles_h, tiles_w, pb);
-  XDDP_HIP_CHECK(hipGetLastError());
-  return stem_wgrad_reduce(ws, grid, w_like, stream);
-}
-
 // dY [N, 64, OH, OW] channels_last bf16, x [N, 3, H, W] channels_last bf16 -> dW like w_like
 at::Tensor stem_conv_wgrad(const at::Tensor& dy_in, const at::Tensor& x, const at::Tensor& w_like) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.size(1) == 3 && x.scalar_type() == at::kBFloat16 &&
@@ -641,10 +481,10 @@ at::Tensor stem_conv_wgrad(const at::Tensor& dy_in, const at::Tensor& x, const a
   auto ws = at::empty({grid, 64, 224}, x.options().dtype(at::kFloat));
   auto zeros = at::zeros({64}, x.options());
   auto stream = c10::hip::getCurrentHIPStream(dev_id).stream();
-  hipLaunchKernelGGL(stem_conv_wgrad_kernel<false>, dim3(grid), dim3(256), 0, stream,
+  hipLaunchKernelGGL(stem_conv_wgrad_kernel, dim3(grid), dim3(256), 0, stream,
                      reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
                      reinterpret_cast<const uint16_t*>(zeros.data_ptr()), ws.data_ptr<float>(), N, H, W, OH, OW,
-                     tiles_h, tiles_w, PoolBwd{});
+                     tiles_h, tiles_w);
   XDDP_HIP_CHECK(hipGetLastError());
   return stem_wgrad_reduce(ws, grid, w_like, stream);
 }

@@ -149,47 +149,12 @@ def _expand_s2(add, like):
     return full
 
 
-class BNReLULink:
-    """Backward hand-off from a bottleneck's conv3 to the conv2 (3x3) + BN2 + ReLU that produced
-    its input (a single consumer). conv3's input-gradient GEMM masks its output by BN2's ReLU
-    (recomputed from y2 and BN2's scale/shift) and reduces BN2's backward partials in its epilogue
-    (``conv1x1_gemm(..., epi_ss=...)``, csrc/kernels/conv_gemm.hip EpiBN second form); BN2's
-    backward then skips its reduce pass over (dout, y2). ``g`` is the exact tensor handed to
-    autograd: if the gradient that reaches BN2 is any other tensor (another consumer's gradient
-    was summed in), the partials do not describe it and BN2 falls back to its own reduce."""
-
-    __slots__ = ("y", "mean", "ss", "part", "g")
-
-    def __init__(self, y, mean, ss):
-        self.y, self.mean, self.ss = y, mean, ss
-        self.part = self.g = None
-
-
-def _c1_dma(x, w) -> bool:
-    """1x1 forward on the LDS-DMA pipeline? XDDP_C1_DMA = 0 (never, default) | 1 (always) | min Cin.
-
-    Measured on ResNet-50 bs256 (profiles/r2_c1dma_ab.txt): no threshold beats the register-staged
-    GEMM (11,662 img/s off, 11,625 at Cin >= 1024, 11,508 for every 1x1), so it stays opt-in."""
-    v = os.environ.get("XDDP_C1_DMA", "0")
-    if v == "0":
-        return False
-    return x.size(1) >= (1 if v == "1" else int(v))
-
-
-def _c1_blas_min_k() -> int:
-    """Stride-1 1x1 forwards with Cin >= XDDP_C1_BLAS_MIN_K (default 1024; 0 = never) run the GEMM
-    on hipBLASLt + a statistics pass instead of the fused-statistics GEMM."""
-    v = int(os.environ.get("XDDP_C1_BLAS_MIN_K", "1024"))
-    return v if v > 0 else 1 << 30
-
-
-def _deep_k_own() -> bool:
-    """The deep-K 1x1 forwards run the own LDS-DMA GEMM with the BN-statistics epilogue (gemm.hip
-    kEpiStats) instead of hipBLASLt + a bn_moments pass: ResNet-50 bs256 12,896-12,917 vs
-    12,695-12,775 img/s interleaved (profiles/README.md r3). XDDP_DEEP_K_OWN=0: hipBLASLt (A/B
-    switch; a block output pending on such a conv is resolved by its own apply pass either way —
-    absorbing it on the register-staged GEMM measured no gain)."""
-    return os.environ.get("XDDP_DEEP_K_OWN", "1") != "0"
+# Stride-1 1x1 forwards with Cin >= this run the GEMM on the LDS-DMA kernel with the statistics
+# epilogue (gemm.hip kEpiStats): the register-staged GEMM waits a memory latency per 64-deep K step,
+# which dominates the deep-K, few-tile layers (ResNet-50 layer3/4 conv1: K = 1024 / 2048).
+# (Measured and removed in r5's switch cleanup: hipBLASLt + a statistics pass there, 12,695-12,775 vs
+# 12,896-12,917 img/s; the 3-stage LDS-DMA kernel for every 1x1 forward, 11,508-11,625 vs 11,662.)
+_DEEP_K = 1024
 
 
 def _same_tensor(a, b) -> bool:
@@ -200,10 +165,10 @@ def _same_tensor(a, b) -> bool:
 class _Conv1x1BN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, residual, relu, dual,
-                stride, link_out, link_x, link_res, link_in, link_ds, defer, res_defer, pend_in, pend_out):
+                stride, link_out, link_x, link_res, link_ds, defer, res_defer, pend_in, pend_out):
         C = load()
         ctx.set_materialize_grads(False)
-        dma = _c1_dma(x, w)
+        dma = False
         if pend_in is not None:
             # x is a pending BN apply (PendingApply): computed in this GEMM's prologue and stored
             # into x's storage by the N-tile-0 blocks (the caller checked _absorbs)
@@ -212,22 +177,12 @@ class _Conv1x1BN(torch.autograd.Function):
                                      pro_res_ss=p.rss, pro_nbt=p.nbt, pro_res_nbt=p.rnbt)
             p.done = True
             p.y = p.res = p.ss = p.rss = None
-        elif dma:  # deep-K / few-tile shapes: the 3-stage LDS-DMA pipeline (csrc/kernels/conv3x3.hip TAPS=1)
-            y, part = C.conv1x1_dma_forward(x, w, stride, True)
-        elif stride == 1 and x.size(1) >= _c1_blas_min_k() and (w.size(0) % 128 == 0 or not _deep_k_own()):
-            # deep-K, few-tile layers (ResNet-50 layer3/4 conv1: K = 1024 / 2048, 400-800 output
-            # tiles): the register-staged GEMM waits a memory latency per 64-deep K step there;
-            # the LDS-DMA GEMM (gemm.hip) runs them with the statistics in its epilogue (or
-            # hipBLASLt + a statistics pass, XDDP_DEEP_K_OWN=0)
+        elif stride == 1 and x.size(1) >= _DEEP_K and w.size(0) % 128 == 0:
+            # deep-K, few-tile layers: the LDS-DMA GEMM with the statistics epilogue (_DEEP_K)
             B, K, H, W = x.shape
-            if _deep_k_own():  # the own LDS-DMA GEMM with the statistics epilogue (gemm.hip kEpiStats)
-                y, part = C.gemm_nt(x.permute(0, 2, 3, 1).reshape(-1, K), w.view(w.size(0), K), None, 5)
-                y = y.view(B, H, W, -1).permute(0, 3, 1, 2)
-                dma = True  # (group-minor partials, as the LDS-DMA kernels leave them)
-            else:
-                y = torch.mm(x.permute(0, 2, 3, 1).reshape(-1, K), w.view(w.size(0), K).t())
-                y = y.view(B, H, W, -1).permute(0, 3, 1, 2)
-                part = C.bn_moments(y).view(1, 3, -1)
+            y, part = C.gemm_nt(x.permute(0, 2, 3, 1).reshape(-1, K), w.view(w.size(0), K), None, 5)
+            y = y.view(B, H, W, -1).permute(0, 3, 1, 2)
+            dma = True  # (group-minor partials, as the LDS-DMA kernels leave them)
         else:
             y, part = C.conv1x1_gemm(x, w, stride, None, True)
         M = y.numel() // y.size(1)
@@ -248,7 +203,7 @@ class _Conv1x1BN(torch.autograd.Function):
             out, bits = C.bn_apply(y, ss, residual, relu, keep_mask, nbt)
         ctx.relu, ctx.has_res, ctx.stride = relu, residual is not None, stride
         ctx.save_for_backward(x, w, y, bits if keep_mask else None, weight, mean, invstd, ss)
-        ctx.link_out, ctx.link_x, ctx.link_res, ctx.link_in = link_out, link_x, link_res, link_in
+        ctx.link_out, ctx.link_x, ctx.link_res = link_out, link_x, link_res
         ctx.link_ds = link_ds
         if link_out is not None:
             if keep_mask and dual:
@@ -288,7 +243,7 @@ class _Conv1x1BN(torch.autograd.Function):
         if dout is None:
             dout, dout2 = dout2, None
         if dout is None:
-            return (None,) * 23
+            return (None,) * 22
         need_bn_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         s = ctx.stride
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
@@ -303,9 +258,9 @@ class _Conv1x1BN(torch.autograd.Function):
             dx = dw = None
             if s == 1 and need_x and need_w and _bwd_fused_ok(ctx, C, w):
                 dx, dw = C.conv1x1_bwd_fused(g, y, coef, x, w)
-            if s == 1 and need_x and dx is None and _dgrad_gemm():
-                dx = _dgrad_in(ctx, C, g, w, coef, y)
-            if need_w and dw is None and s == 1 and _wgrad_gemm():
+            if s == 1 and need_x and dx is None:
+                dx = _dgrad(C, g, w, coef, y)
+            if need_w and dw is None and s == 1:
                 dw = C.conv1x1_wgrad(g, x, 1, w, y, coef)
             if (need_x and dx is None) or (need_w and dw is None):
                 v = lambda i: coef[i].view(1, -1, 1, 1)  # noqa: E731
@@ -317,8 +272,7 @@ class _Conv1x1BN(torch.autograd.Function):
                 dx = gx if dx is None else dx
                 dw = gw if dw is None else dw
             return _grads(ctx, dx, dw, dw_bn, db_bn, dres)
-        if (s == 1 and need_x and need_w and _bwd_prologue() and _dgrad_gemm() and _wgrad_gemm()
-                and (need_dres or (dout2 is None and bits is None and (not ctx.relu or _bwd_prologue_masked())))):
+        if s == 1 and need_x and need_w and (need_dres or (dout2 is None and bits is None and not ctx.relu)):
             # BN-backward elementwise pass folded into both GEMMs: dY = k1·g + k2·y + k3' is formed
             # while staging (g = the masked gradient the reduce pass writes as d(residual), or the
             # incoming gradient itself, masked in the prologue by relu(y·scale + shift) > 0 when
@@ -329,13 +283,13 @@ class _Conv1x1BN(torch.autograd.Function):
             if _bwd_fused_ok(ctx, C, w):
                 dx, dw = C.conv1x1_bwd_fused(g, y, coef, x, w)
             else:
-                dx = _dgrad_in(ctx, C, g, w, coef, y)
+                dx = _dgrad(C, g, w, coef, y)
                 dw = C.conv1x1_wgrad(g, x, 1, w, y, coef)
             return _grads(ctx, dx, dw, dw_bn, db_bn, dres)
         dy, dw_bn, db_bn, dres = C.bn_backward(dout, y, None, weight, mean, invstd, ss, ctx.relu, need_dres,
                                                need_bn_w, dout2, bits)
         dx = dw = None
-        if need_x and s == 1 and _dgrad_gemm():
+        if need_x and s == 1:
             # dX[M, K] = dY[M, N] · W[N, K] is the same NT GEMM on (dY, Wᵀ): 35 % less time than
             # MIOpen's 1x1 dgrad over the ResNet-50 shapes (scripts/dgrad_bench.py)
             lx = ctx.link_x
@@ -347,9 +301,9 @@ class _Conv1x1BN(torch.autograd.Function):
                                              2 if lx.add_s2 else 1)
                 lx.add, lx.g, lx.add_s2 = None, dx, False
             else:
-                dx = _dgrad_in(ctx, C, dy, w, None, None)
+                dx = _dgrad(C, dy, w, None, None)
             need_x = False
-        elif need_x and s == 2 and _dgrad_gemm():
+        elif need_x and s == 2:
             # strided 1x1 input gradient: only the stride-2 pixels receive dY·W. The compact product
             # is one stride-1 GEMM; linked (downsample of a bottleneck whose input is the previous
             # block's output) it goes to conv1's epilogue, else it is scattered into zeros
@@ -360,7 +314,7 @@ class _Conv1x1BN(torch.autograd.Function):
             else:
                 dx = _expand_s2(dxe, x)
             need_x = False
-        if need_w and _wgrad_gemm():
+        if need_w:
             # dW[N, K] = dYᵀ[N, M] · X[M, K] (strided pixel rows for the downsample): 14 % less
             # time than MIOpen's 1x1 wgrad over the ResNet-50 shapes (scripts/dgrad_bench.py)
             dw = C.conv1x1_wgrad(dy, x, s, w)
@@ -374,45 +328,25 @@ class _Conv1x1BN(torch.autograd.Function):
 
 
 def _grads(ctx, dx, dw, dw_bn, db_bn, dres):
-    """The 23 input gradients of _Conv1x1BN; a linked residual gradient goes to the consumer link."""
+    """The 22 input gradients of _Conv1x1BN; a linked residual gradient goes to the consumer link."""
     if dres is not None and ctx.link_res is not None:
         ctx.link_res.add, dres = dres, None
     return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
             None, None, None, None, None, None, dres if ctx.has_res else None, None, None, None, None, None, None,
-            None, None, None, None, None, None)
+            None, None, None, None, None)
 
 
 def _bwd_fused_ok(ctx, C, w) -> bool:
     """Input and weight gradient of a stride-1 1x1 conv from one staging of its BN-backward dY
     (``conv1x1_bwd_fused``): the ResNet-50 layer-1 shapes (N, K) = (256, 64), (64, 256), where
-    both gradient kernels sit at the HBM roofline reading the same two tensors.
-    XDDP_CONV_BWD_FUSED=0 keeps the two separate kernels (A/B switch)."""
-    if os.environ.get("XDDP_CONV_BWD_FUSED", "1") == "0":
-        return False
-    if ctx.link_in is not None and _epi() and os.environ.get("XDDP_CONV_EPI2", "0") == "1":
-        return False  # the dgrad epilogue has extra work to do there
+    both gradient kernels sit at the HBM roofline reading the same two tensors."""
     return (w.dtype == torch.bfloat16 and w.is_contiguous() and w.shape[2] == 1 and w.shape[3] == 1
             and C.conv1x1_bwd_fused_supported(w.shape[0], w.shape[1]))
 
 
-def _dgrad_in(ctx, C, g, w, coef, y):
-    """Stride-1 input gradient; with a BNReLULink on the input, also the producer's masked BN-backward
-    partials (epilogue second form)."""
-    li = ctx.link_in
-    # XDDP_CONV_EPI2=1 opts in. Off by default: measured 10,534 vs 10,808 img/s (ResNet-50 bs256,
-    # MI355X) with 45 spilled registers at 2 blocks/CU, and still 11,746 vs 12,092-12,170 at one
-    # block/CU without spills (the EPI default since): the conv3 input-gradient GEMM re-reads y2
-    # per output tile, costing more than BN2's separate reduce pass.
-    if li is None or not _epi() or os.environ.get("XDDP_CONV_EPI2", "0") != "1":
-        return _dgrad(C, g, w, coef, y)
-    dx, li.part = C.conv1x1_gemm(g, w, 1, coef, False, y, True, None, li.y, None, li.mean, li.ss)
-    li.g = dx
-    return dx
-
-
 class _Conv3x3BNReLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, stride, link, pend_out):
+    def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, stride, pend_out):
         C = load()
         ctx.set_materialize_grads(False)
         y, part = C.conv3x3_forward(x, w, stride, True)
@@ -427,67 +361,43 @@ class _Conv3x3BNReLU(torch.autograd.Function):
             out, _ = C.bn_apply(y, ss, None, True, False, nbt)
         ctx.stride = stride
         ctx.save_for_backward(x, w, y, weight, mean, invstd, ss)
-        ctx.link = link
-        if link is not None:
-            link.y, link.mean, link.ss = y, mean, ss
         return out
 
     @staticmethod
     def backward(ctx, dout):
         if dout is None:
-            return (None,) * 13
+            return (None,) * 12
         C = load()
         x, w, y, weight, mean, invstd, ss = ctx.saved_tensors
         need_bn_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
-        lk = ctx.link
-        part = lk.part if (lk is not None and _same_tensor(dout, lk.g)) else None
-        if lk is not None:
-            lk.y = lk.mean = lk.ss = lk.part = lk.g = None
-        if part is not None:
-            # dout is already masked by this BN's ReLU and its backward partials were reduced by
-            # conv3's input-gradient epilogue: only the finalize + the elementwise pass remain
-            M = y.numel() // y.size(1)
-            coef, dw_bn, db_bn = C.bn_backward_from_partials(part, M, weight, mean, invstd, need_bn_w, False)
-            dy = C.bn_backward_elem(dout, y, mean, coef)
-        else:
-            # ReLU mask recomputed from y·scale + shift inside the BN backward (no mask tensor kept)
-            dy, dw_bn, db_bn, _ = C.bn_backward(dout.contiguous(memory_format=torch.channels_last), y, None, weight,
-                                                mean, invstd, ss, True, False, need_bn_w, None, None)
+        # ReLU mask recomputed from y·scale + shift inside the BN backward (no mask tensor kept).
+        # (r5: conv3's input-gradient epilogue reducing this BN's backward partials instead, the
+        # kernel's EPI mask-recompute form, still lost: 12,940 vs 13,399 img/s interleaved.)
+        dy, dw_bn, db_bn, _ = C.bn_backward(dout.contiguous(memory_format=torch.channels_last), y, None, weight,
+                                            mean, invstd, ss, True, False, need_bn_w, None, None)
         s = ctx.stride
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dx = dw = None
         if need_x and s == 1:
             dx = C.conv3x3_forward(dy, C.conv3x3_rot_weight(w), 1, False)[0]
-            need_x = False
-        elif need_x and s == 2 and _dgrad3_s2():
-            # four phase grids of the strided dX, 1/2/2/4 taps each, one launch (conv3x3.hip DG2)
+        elif need_x:
+            # four phase grids of the strided dX, 1/2/2/4 taps each, one launch (conv3x3.hip DG2):
+            # 142 / 97 / 86 vs MIOpen's 170 / 141 / 136 us (profiles/r4_s2_bwd_vs_miopen.txt)
             dx = C.conv3x3_dgrad_s2(dy, C.conv3x3_rot_weight(w), x.size(2), x.size(3))
-            need_x = False
-        if need_w and _wgrad3() and (s == 1 or os.environ.get("XDDP_CONV3X3_WGRAD_S2", "1") != "0"):
+        if need_w:
             # 8x8 output patches sharing one staged X halo across the 9 taps (conv3x3_wgrad.hip):
             # 96-98 us vs MIOpen's 120-182 us per stride-1 ResNet-50 shape (bs256); at stride 2 the
             # phase-split halo is shared by 128 output channels (8 waves): 127 / 118 / 108 vs
-            # MIOpen's 150 / 139 / 145 us (profiles/r4_s2_bwd_vs_miopen.txt; XDDP_CONV3X3_WGRAD_S2=0
-            # hands it back to MIOpen)
+            # MIOpen's 150 / 139 / 145 us (profiles/r4_s2_bwd_vs_miopen.txt)
             dw = C.conv3x3_wgrad_patch(dy, x, s, w)
-            need_w = False
-        if need_x or need_w:
-            gx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
-                                                            [need_x, need_w, False])
-            dx = gx if need_x else dx
-            dw = gw if need_w else dw
         return (dx, dw, dw_bn if ctx.needs_input_grad[2] else None, db_bn if ctx.needs_input_grad[3] else None,
-                None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
 def _dgrad(C, g, w, coef, y):
     """dX = dY · W on the MFMA GEMM, W read K-major through transposed LDS reads (no transposed
-    weight copy; XDDP_GEMM_WT=0 makes the copy instead, A/B switch)."""
-    if os.environ.get("XDDP_GEMM_WT", "1") != "0":
-        return C.conv1x1_gemm(g, w, 1, coef, False, y, True)[0]
-    n_out, k_in = w.shape[0], w.shape[1]
-    wt = w.reshape(n_out, k_in).t().contiguous().view(k_in, n_out, 1, 1)
-    return C.conv1x1_gemm(g, wt, 1, coef, False, y)[0]
+    weight copy)."""
+    return C.conv1x1_gemm(g, w, 1, coef, False, y, True)[0]
 
 
 def _conv3x3() -> bool:
@@ -495,47 +405,10 @@ def _conv3x3() -> bool:
     return os.environ.get("XDDP_CONV3X3", "1") != "0"
 
 
-def _dgrad3_s2() -> bool:
-    """The stride-2 3x3 input gradient as four phase GEMMs on the 4-phase LDS-DMA GEMM pipeline
-    (gemm.hip DGS2: 1/2/2/4 taps per phase, written straight to the strided pixels, no zero-fill):
-    142 / 97 / 86 us vs MIOpen's 170 / 141 / 136 us on the three ResNet-50 bs256 shapes
-    (profiles/r4_s2_bwd_vs_miopen.txt). XDDP_CONV3X3_DGRAD_S2=0 hands it back to MIOpen."""
-    return os.environ.get("XDDP_CONV3X3_DGRAD_S2", "1") != "0"
-
-
 def _epi() -> bool:
     """XDDP_CONV_EPI=0 keeps the previous block's BN-backward reduce pass separate instead of
     folding it into the next block's conv1 input-gradient GEMM epilogue (A/B switch)."""
     return os.environ.get("XDDP_CONV_EPI", "1") != "0"
-
-
-def _wgrad3() -> bool:
-    """XDDP_CONV3X3_WGRAD=0 sends the bottleneck 3x3 weight gradient back to MIOpen (A/B switch)."""
-    return os.environ.get("XDDP_CONV3X3_WGRAD", "1") != "0"
-
-
-def _dgrad_gemm() -> bool:
-    """XDDP_CONV_DGRAD_GEMM=0 sends the stride-1 input gradient back to MIOpen (A/B switch)."""
-    return os.environ.get("XDDP_CONV_DGRAD_GEMM", "1") != "0"
-
-
-def _bwd_prologue() -> bool:
-    """XDDP_CONV_BWD_PROLOGUE=0 materializes the BN-backward gradient instead of folding it into
-    the stride-1 input/weight-gradient GEMMs (A/B switch)."""
-    return os.environ.get("XDDP_CONV_BWD_PROLOGUE", "1") != "0"
-
-
-def _bwd_prologue_masked() -> bool:
-    """XDDP_CONV_BWD_PROLOGUE_MASK=1 also folds the BN+ReLU (recomputed-mask) backward of the
-    bottleneck's conv1 into its gradient GEMMs. Off by default: that input-gradient GEMM re-reads
-    its A operand once per output-channel tile (C_in / 128 of them), so reading two sources there
-    costs more than the skipped pass saves (10,378 vs 10,436 img/s, ResNet-50 bs256)."""
-    return os.environ.get("XDDP_CONV_BWD_PROLOGUE_MASK", "0") == "1"
-
-
-def _wgrad_gemm() -> bool:
-    """XDDP_CONV_WGRAD_GEMM=0 sends the weight gradient back to MIOpen (A/B switch)."""
-    return os.environ.get("XDDP_CONV_WGRAD_GEMM", "1") != "0"
 
 
 def conv_bn_supported(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module) -> bool:
@@ -561,13 +434,10 @@ def conv3x3_bn_relu(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, pending: bo
     resolve(x)
     if not (_conv3x3() and conv.kernel_size == (3, 3) and conv_bn_supported(x, conv, bn)):
         return bn(conv(x), relu=True)
-    link = BNReLULink(None, None, None) if _epi() else None
     pend = [] if (pending and _pending_apply()) else None
     out = _Conv3x3BNReLU.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), int(conv.stride[0]),
-                               link, pend)
-    if link is not None:
-        out._xddp_bnr = link
+                               pend)
     if pend:
         out._xddp_pend = pend[0]
     return out
@@ -604,11 +474,10 @@ def conv1x1_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, residual: Op
         return bn(conv(x), residual=residual, relu=relu, dual_output=dual_output)
     dfr = DeferredBN() if (defer and residual is None and not relu and not dual_output) else None
     link_out = EpiLink() if (dual_output and residual is not None and relu and _epi()) else None
-    link_in = getattr(x, "_xddp_bnr", None) if conv.stride[0] == 1 else None
     pend_out = [] if (pending and dual_output and residual is not None and relu and _pending_apply()) else None
     out = _Conv1x1BN.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                            bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), residual, relu,
-                           dual_output, int(conv.stride[0]), link_out, link_x, link_res, link_in,
+                           dual_output, int(conv.stride[0]), link_out, link_x, link_res,
                            link_ds if conv.stride[0] == 2 else None, dfr, res_defer, pend_in, pend_out)
     if dfr is not None:
         out._xddp_bnss = dfr
@@ -624,5 +493,5 @@ def _absorbs(x, conv, bn, p) -> bool:
     GEMM path only (stride 1; not the LDS-DMA or hipBLASLt deep-K forwards), and the pending form
     must match the tensor (C, 8-channel chunks)."""
     return (conv.kernel_size == (1, 1) and conv.stride[0] == 1 and conv_bn_supported(x, conv, bn)
-            and not _c1_dma(x, conv.weight) and x.size(1) < _c1_blas_min_k()
+            and x.size(1) < _DEEP_K
             and p.out.data_ptr() == x.data_ptr() and p.out.shape == x.shape)

@@ -4,9 +4,10 @@ Forward: ``stem_conv_forward`` (implicit GEMM from an LDS halo, BN statistics re
 epilogue) -> ``bn_stats_from_partials`` -> ``stem_pool_forward`` (normalize + ReLU + pool in one
 pass). Neither a separate statistics pass over the conv output nor the normalized activation
 exists. Backward: ``stem_pool_bn_backward`` twice (BN partial sums, then dX, the pooled gradient
-and the ReLU mask rebuilt on the fly) -> ``stem_conv_wgrad`` (``stem_conv_wgrad_fused``, which
-forms dX tile by tile inside the weight-gradient kernel, is the opt-in alternative). The image needs no
-gradient, so there is no input-gradient pass (if it does, torch's convolution backward adds it).
+and the ReLU mask rebuilt on the fly) -> ``stem_conv_wgrad``. (r4/r5: forming the conv-output
+gradient tile by tile inside the weight-gradient kernel instead needed more than 256 VGPRs and ran
+one wave per SIMD, 555 us vs 176 + 130 us; removed.) The image needs no gradient, so there is no
+input-gradient pass (if it does, torch's convolution backward adds it).
 Kernels: csrc/kernels/stem_conv.hip, csrc/kernels/pool.hip.
 """
 from __future__ import annotations
@@ -51,11 +52,7 @@ class _Stem(torch.autograd.Function):
         part = C.stem_pool_bn_backward(dy, dy2, idx, y, ss, mean)
         coef, dgamma, dbeta = C.bn_backward_from_partials(part, M, weight, mean, invstd, need_bn, False)
         dx = dw = None
-        if ctx.needs_input_grad[1] and not ctx.needs_input_grad[0] and _wgrad_fused():
-            # the conv-output gradient is formed tile by tile inside the weight-gradient kernel
-            # (never written to HBM)
-            dw = C.stem_conv_wgrad_fused(dy, dy2, idx, y, x, w, ss, mean, coef)
-        elif ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             dconv = C.stem_pool_bn_backward(dy, dy2, idx, y, ss, mean, coef)
             if ctx.needs_input_grad[1]:
                 dw = C.stem_conv_wgrad(dconv, x, w)
@@ -64,14 +61,6 @@ class _Stem(torch.autograd.Function):
                                                          [True, False, False])[0]
         return (dx, dw, dgamma if ctx.needs_input_grad[2] else None, dbeta if ctx.needs_input_grad[3] else None,
                 None, None, None, None, None, None, None)
-
-
-def _wgrad_fused() -> bool:
-    """XDDP_STEM_WGRAD_FUSED=1 forms the conv-output gradient inside the weight-gradient kernel.
-    Off by default: the fused kernel needs more than 256 VGPRs per wave (the prefetched pooled
-    gradient on top of the MFMA loop) and so runs one wave per SIMD — 555 us vs 176 + 130 us for
-    the ELEM pass + the two-waves-per-SIMD weight gradient (ResNet-50 bs256, MI355X)."""
-    return os.environ.get("XDDP_STEM_WGRAD_FUSED", "0") == "1"
 
 
 def _single(v):

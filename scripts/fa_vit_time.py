@@ -1,6 +1,6 @@
 """Time the flash attention forward at the ViT-L/16 bs256 head shape (B256, S197, H16, D64).
 
-usage: python scripts/fa_vit_time.py   (XDDP_FA_WHOLE=0 selects the double-buffered tile loop)
+usage: python scripts/fa_vit_time.py
 Prints one JSON line: us per forward call and per forward + backward.
 """
 import json
@@ -47,5 +47,5 @@ for _ in range(iters):
 e1.record()
 torch.cuda.synchronize()
 fb = e0.elapsed_time(e1) * 1e3 / iters
-print(json.dumps({"shape": [B, S, H, D], "whole": os.environ.get("XDDP_FA_WHOLE", "1"), "fwd_us": round(us, 1),
+print(json.dumps({"shape": [B, S, H, D], "fwd_us": round(us, 1),
                   "tflops": round(tf, 1), "fwd_bwd_us": round(fb, 1)}))

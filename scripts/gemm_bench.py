@@ -47,12 +47,6 @@ for name, M, K, N in shapes:
         own = f"own {t_own:.3f} ms ({fl / t_own / 1e9:.0f} TF/s, maxerr {err:.3f})"
     except Exception as e:  # noqa: BLE001
         own = f"own: {str(e)[:80]}"
-    for tile in (0, 4):  # the 3-stage LDS-DMA pipeline (conv3x3.hip TAPS=1): 256x128 / 128x64 tiles
-        try:
-            t_d = timeit(lambda: C.conv1x1_dma_forward(x4, w4, 1, False, tile))
-            own += f" | dma{tile} {t_d:.3f} ms ({fl / t_d / 1e9:.0f} TF/s)"
-        except Exception as e:  # noqa: BLE001
-            own += f" | dma{tile}: {str(e)[:60]}"
     gb = 2.0 * (M * K + N * K + M * N) / 1e9
     print(f"{name:14s} M{M} K{K} N{N}: hipBLASLt {t_mm:.3f} ms ({fl / t_mm / 1e9:.0f} TF/s, {gb / t_mm:.1f} TB/s) | "
           f"{own} [{gb / t_own if 'own ' in own else 0:.1f} TB/s]", flush=True)

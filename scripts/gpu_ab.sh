@@ -1,7 +1,7 @@
 #!/bin/bash
 # Generic A/B of the headline bench (or any bench.py arguments) under environment variants, on one
 # box, e.g.:
-#   gpurun -- 'bash scripts/gpu_ab.sh "" "XDDP_DS_DEFER=0" "XDDP_CONV_EPI2=1"'
+#   gpurun -- 'bash scripts/gpu_ab.sh "" "XDDP_DS_DEFER=0" "XDDP_PENDING_APPLY=0"'
 #   BENCH_ARGS="--model vit_l_16 --steps 10 --warmup 4" gpurun -- 'bash scripts/gpu_ab.sh "" "XDDP_OWN_GEMM=0"'
 # Each variant runs under its own time limit; the first failure stops the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

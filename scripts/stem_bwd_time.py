@@ -1,6 +1,6 @@
 """Time the stem's fused maxpool + ReLU + BN backward passes at ResNet-50 bs256 shapes.
 
-usage: python scripts/stem_bwd_time.py [batch]   (XDDP_STEM_PF=0 selects the unpipelined walk)
+usage: python scripts/stem_bwd_time.py [batch]
 Prints one JSON line: us per call of the partial-sums pass and of the dX pass.
 """
 import json
@@ -41,5 +41,5 @@ def timeit(fn, iters=20):
 
 red = timeit(lambda: C.stem_pool_bn_backward(d1, d2, idx, y, ss, mean))
 elem = timeit(lambda: C.stem_pool_bn_backward(d1, d2, idx, y, ss, mean, coef))
-print(json.dumps({"batch": B, "pf": os.environ.get("XDDP_STEM_PF", "1"), "reduce_us": round(red, 1),
+print(json.dumps({"batch": B, "reduce_us": round(red, 1),
                   "elem_us": round(elem, 1)}))

@@ -59,32 +59,6 @@ def test_conv1x1_wgrad_matches_fp32(b, cin, h, w, cout, s, wdt):
     torch.testing.assert_close(dw.float(), ref, rtol=tol, atol=tol * ref.abs().max().item())
 
 
-@pytest.mark.parametrize("b,cin,h,w,cout,s,tile", [
-    (1, 1024, 14, 14, 256, 1, 4),   # layer3 conv1 shape class, 128x64 tiles, partial last M-tile
-    (2, 2048, 7, 7, 512, 1, 0),     # layer4 conv1 class (32 K-steps), 256x128 tiles
-    (2, 512, 15, 15, 1024, 2, 4),   # strided (downsample) rows, odd input size
-    (1, 64, 9, 7, 128, 1, 0),       # a single K-step
-])
-def test_conv1x1_dma_forward_matches_fp32(b, cin, h, w, cout, s, tile):
-    """The 1x1 conv on the 3-stage LDS-DMA pipeline (conv3x3.hip TAPS=1): output vs fp32 torch,
-    statistics partials (group-minor) vs torch's mean/var of the stored bf16 output."""
-    torch.manual_seed(5)
-    x = _x(b, cin, h, w, offset=3.0)
-    wt = (torch.randn(cout, cin, 1, 1, device="cuda") / cin ** 0.5).to(torch.bfloat16)
-    y, part = C.conv1x1_dma_forward(x, wt, s, True, int(tile))
-    ref = F.conv2d(x.float(), wt.float(), stride=s)
-    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
-    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
-    y2, _ = C.conv1x1_gemm(x, wt, s, None, True)
-    assert (y.float() - y2.float()).abs().max().item() <= 1e-2 * ref.abs().max().item()
-    yf = y.float().permute(0, 2, 3, 1).reshape(-1, cout)
-    rm, rv = torch.zeros(cout, device="cuda"), torch.ones(cout, device="cuda")
-    nbt = torch.zeros((), dtype=torch.long, device="cuda")
-    mean, invstd, _ = C.bn_stats_from_partials(part, yf.shape[0], None, None, rm, rv, nbt, 0.1, False, 1e-5, True)
-    torch.testing.assert_close(mean, yf.mean(0), rtol=1e-5, atol=1e-4 * yf.std(0).max().item())
-    torch.testing.assert_close(1.0 / invstd ** 2 - 1e-5, yf.var(0, unbiased=False), rtol=2e-3, atol=1e-6)
-
-
 @pytest.mark.parametrize("offset", [0.0, 300.0])
 def test_epilogue_stats_match_torch(offset):
     """Epilogue partials -> mean/var equal torch's over the stored bf16 output, also when
@@ -132,21 +106,22 @@ def test_bn_backward_prologue_in_gemms(b, cin, h, w, cout, masked):
     torch.testing.assert_close(dw, refw, rtol=2e-2, atol=2e-2 * refw.abs().max().item())
 
 
-@pytest.mark.parametrize("residual,relu,stride,dma", [(False, True, 1, "0"), (True, True, 1, "0"),
-                                                      (False, False, 2, "0"), (False, False, 1, "0"),
-                                                      (True, True, 1, "1"), (False, False, 2, "1")])
-def test_conv1x1_bn_act_forward_backward(residual, relu, stride, dma, monkeypatch):
+@pytest.mark.parametrize("residual,relu,stride,cin", [(False, True, 1, 128), (True, True, 1, 128),
+                                                      (False, False, 2, 128), (False, False, 1, 128),
+                                                      (True, True, 1, 1024), (False, False, 1, 1024)])
+def test_conv1x1_bn_act_forward_backward(residual, relu, stride, cin):
+    """cin = 1024: the deep-K forward on the LDS-DMA GEMM with the statistics epilogue (group-minor
+    partials, ops/conv_bn.py _DEEP_K)."""
     from distributeddataparallel_amd.ops import FusedBatchNorm2d, conv1x1_bn_act
 
-    monkeypatch.setenv("XDDP_C1_DMA", dma)  # "1": forward on the LDS-DMA kernel (group-minor partials)
     torch.manual_seed(2)
-    conv = torch.nn.Conv2d(128, 256, 1, stride=stride, bias=False).cuda().to(torch.bfloat16)
+    conv = torch.nn.Conv2d(cin, 256, 1, stride=stride, bias=False).cuda().to(torch.bfloat16)
     bn = FusedBatchNorm2d(256).cuda().to(torch.bfloat16)
     with torch.no_grad():
         bn.weight.uniform_(0.5, 1.5)
         bn.bias.uniform_(-0.5, 0.5)
     conv = conv.to(memory_format=torch.channels_last)
-    x = _x(4, 128, 12, 12).requires_grad_()
+    x = _x(4, cin, 12, 12).requires_grad_()
     oh = (12 - 1) // stride + 1
     res = _x(4, 256, oh, oh).requires_grad_() if residual else None
     out = conv1x1_bn_act(x, conv, bn, residual=res, relu=relu)
@@ -419,34 +394,6 @@ def test_dgrad_bn_mask_recompute_epilogue(pro, b, cin, h, w, cout):
     want = weight.view(1, -1, 1, 1) * invstd.view(1, -1, 1, 1) * (
         gq - (sd / M).view(1, -1, 1, 1) - xh * (sdx * invstd / M).view(1, -1, 1, 1))
     torch.testing.assert_close(dx.float(), want, rtol=2e-2, atol=2e-2 * want.abs().max().item())
-
-
-def test_bottleneck_bn2_fold_matches_separate_pass(monkeypatch):
-    """conv3's input-gradient epilogue folding BN2's backward reduce (XDDP_CONV_EPI2=1) gives the
-    same gradients as BN2's own reduce pass (=0)."""
-    from distributeddataparallel_amd.models.resnet import Bottleneck, ResNet
-    from distributeddataparallel_amd.ops import FusedBatchNorm2d
-
-    torch.manual_seed(8)
-    m = ResNet(Bottleneck, [2, 2, 1, 1], norm_layer=FusedBatchNorm2d).cuda().to(torch.bfloat16)
-    m = m.to(memory_format=torch.channels_last)
-    x = torch.randn(4, 3, 64, 64, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (4,), device="cuda")
-    sd = {k: v.clone() for k, v in m.state_dict().items()}
-
-    def run(flag):
-        monkeypatch.setenv("XDDP_CONV_EPI2", flag)
-        m.load_state_dict(sd)
-        m.zero_grad()
-        loss = F.cross_entropy(m(x).float(), y)
-        loss.backward()
-        return loss.item(), torch.cat([p.grad.float().flatten() for p in m.parameters()])
-
-    l1, g1 = run("1")
-    l0, g0 = run("0")
-    assert abs(l1 - l0) < 1e-6 * max(1.0, abs(l0))
-    assert ((g1 - g0).norm() / g0.norm()).item() < 2e-2
-    assert F.cosine_similarity(g1, g0, dim=0).item() > 0.999
 
 
 @pytest.mark.parametrize("N,K,pro", [(256, 64, 2), (256, 64, 3), (64, 256, 2), (64, 256, 3)])

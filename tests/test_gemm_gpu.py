@@ -36,12 +36,12 @@ def test_gemm_nt_plain_and_bias(M, K, N):
     assert _rel(yb, ref + b.float()) < 5e-3
 
 
-@pytest.mark.parametrize("bn,K", [("128", 512), ("256", 512), ("256", 576)])
-def test_gemm_nt_gelu_and_residual(bn, K, monkeypatch):
-    monkeypatch.setenv("XDDP_GEMM_BN", bn)  # read per call: both tile widths on one shape
+@pytest.mark.parametrize("M,N,K", [(777, 1152, 512),    # N % 256 != 0: 256 x 128 tiles
+                                   (777, 1024, 576),    # few tiles: 256 x 128 fills the CUs better
+                                   (16384, 1024, 512)])  # 256 x 256 tiles (gemm.hip pick_bn)
+def test_gemm_nt_gelu_and_residual(M, N, K):
     C = _C()
     g = torch.Generator(device="cuda").manual_seed(7)
-    M, N = 777, 1024
     a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
     w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
     b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)

@@ -74,7 +74,7 @@ def _run_three(batch, size, branch_gamma=None):
     C = load()
     fused, ref32, ref16, x16, y = _models(batch, size, branch_gamma=branch_gamma)
     counts, orig = _counting(C, ["conv1x1_gemm", "conv3x3_forward", "conv1x1_wgrad", "bn_backward_from_partials",
-                                 "conv1x1_bwd_fused", "conv1x1_dma_forward", "bn_moments", "gemm_nt"])
+                                 "conv1x1_bwd_fused", "bn_moments", "gemm_nt"])
     try:
         lf = F.cross_entropy(fused(x16).float(), y)
         lf.backward()
@@ -86,12 +86,12 @@ def _run_three(batch, size, branch_gamma=None):
     l16 = F.cross_entropy(ref16(x16).float(), y)
     l16.backward()
     _run_three.ref16 = ref16
-    # every fused path ran: 1x1 GEMM fwd (36 convs; XDDP_C1_DMA puts some on the LDS-DMA kernel, the
-    # deep-K ones (Cin >= 1024) run the LDS-DMA gemm_nt with its statistics epilogue) +
+    # every fused path ran: 1x1 GEMM fwd (36 convs; the deep-K ones (Cin >= 1024) run the LDS-DMA
+    # gemm_nt with its statistics epilogue) +
     # stride-1 dgrad (layer-1 conv3 x 3 and the downsample as the fused dgrad+wgrad kernel), 3x3
     # implicit GEMM (16 forward + 12 stride-1 dgrad), MFMA wgrad, EpiLink epilogue + its BN finalize
     assert counts["conv1x1_bwd_fused"] >= 4, counts
-    assert (counts["conv1x1_gemm"] + counts["conv1x1_dma_forward"] + counts["conv1x1_bwd_fused"]
+    assert (counts["conv1x1_gemm"] + counts["conv1x1_bwd_fused"]
             + counts["bn_moments"] + counts["gemm_nt"] >= 36 + 30), counts
     assert counts["conv3x3_forward"] >= 16 + 12, counts
     assert counts["conv1x1_wgrad"] + counts["conv1x1_bwd_fused"] >= 32, counts

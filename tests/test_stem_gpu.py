@@ -174,34 +174,3 @@ def test_resnet_stem_matches_unfused_stack():
     assert rel(own[0], ref[0]) < 2e-2
     for a, b in zip(own[1:4], ref[1:4]):
         assert rel(a, b) < 5e-2, rel(a, b)
-
-
-def test_stem_wgrad_fused_matches_materialized():
-    """stem_conv_wgrad_fused (dY built in-kernel from the pooled gradient) == stem_conv_wgrad of the
-    materialized dY (stem_pool_bn_backward ELEM pass): the same math and roundings."""
-    from distributeddataparallel_amd._native import load
-
-    C = load()
-    g = torch.Generator(device="cuda").manual_seed(21)
-    N, H, W = 4, 224, 224
-    x = torch.randn(N, 3, H, W, device="cuda", generator=g).to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    w = (torch.randn(64, 3, 7, 7, device="cuda", generator=g) * 0.1).to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    y, part = C.stem_conv_forward(x, w)
-    M = y.numel() // 64
-    gamma = torch.rand(64, device="cuda", generator=g) + 0.5
-    beta = torch.randn(64, device="cuda", generator=g) * 0.1
-    mean, invstd, ss = C.bn_stats_from_partials(part, M, gamma, beta, None, None, None, 0.0, False, 1e-5)
-    pooled, idx = C.stem_pool_forward(y, ss)
-    d1 = torch.randn(pooled.shape, device="cuda", generator=g).to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    d2 = torch.randn(pooled.shape, device="cuda", generator=g).to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    bp = C.stem_pool_bn_backward(d1, d2, idx, y, ss, mean)
-    coef, _, _ = C.bn_backward_from_partials(bp, M, gamma, mean, invstd, False, False)
-    dconv = C.stem_pool_bn_backward(d1, d2, idx, y, ss, mean, coef)
-    ref = C.stem_conv_wgrad(dconv, x, w).float()
-    fused = C.stem_conv_wgrad_fused(d1, d2, idx, y, x, w, ss, mean, coef).float()
-    rel = ((fused - ref).norm() / ref.norm()).item()
-    assert rel < 2e-3, rel
