@@ -194,6 +194,8 @@ def tail_report(sizes: List[int], plan: BucketPlan, world_size: int, overlapped_
     if overlapped_optimizer is True:
         overlapped_optimizer = "backward"
     exposed = exposed_tail_us(sizes, world_size) if world_size > 1 else 0.0
+    # the tail bucket exceeds its cap (buckets close at the first tensor that reaches the cap, so
+    # this means the tail's last tensor alone — or with the tensors before it — overshoots)
     over_cap = plan.tail_bytes > 0 and sizes[-1] > plan.tail_bytes
     if world_size <= 1:
         mitigation = "none needed (one rank: nothing is communicated)"
@@ -209,7 +211,7 @@ def tail_report(sizes: List[int], plan: BucketPlan, world_size: int, overlapped_
     else:
         mitigation = "none"
     return {"tail_bytes": int(sizes[-1]), "tail_cap_bytes": int(plan.tail_bytes),
-            "tail_is_one_tensor_over_cap": bool(over_cap), "exposed_tail_us_model": round(exposed, 1),
+            "tail_over_cap": bool(over_cap), "exposed_tail_us_model": round(exposed, 1),
             "optimizer_schedule": overlapped_optimizer or "after backward", "tail_chunks": int(tail_chunks),
             "mitigation": mitigation}
 

@@ -71,7 +71,7 @@ def test_llama3_8b_layout_pinned():
     by = bp.bucket_bytes(sizes, lay)
     assert by[-1] == sizes[-1] > plan.tail_bytes
     rep = bp.tail_report(by, plan, 8, overlapped_optimizer=False)
-    assert rep["tail_is_one_tensor_over_cap"] and rep["mitigation"] == "none"
+    assert rep["tail_over_cap"] and rep["mitigation"] == "none"
     assert rep["exposed_tail_us_model"] > 4000
     rep = bp.tail_report(by, plan, 8, overlapped_optimizer="tail", tail_chunks=16)
     assert rep["mitigation"].startswith("deferred optimizer") and "16 chunk" in rep["mitigation"]
@@ -84,7 +84,7 @@ def test_llama3_8b_layout_pinned():
 def test_tail_report_small_tail_uses_cap():
     plan = bp.xgmi_plan(100 * MiB, 8, alpha_us=30, busbw_gbps=350)
     rep = bp.tail_report([40 * MiB, 50 * MiB, plan.tail_bytes // 2], plan, 8, overlapped_optimizer=False)
-    assert not rep["tail_is_one_tensor_over_cap"] and rep["mitigation"].startswith("tail cap")
+    assert not rep["tail_over_cap"] and rep["mitigation"].startswith("tail cap")
     assert rep["exposed_tail_us_model"] < 60
     assert bp.tail_report([1, 2], plan, 1, False)["exposed_tail_us_model"] == 0.0
 
