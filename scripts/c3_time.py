@@ -37,10 +37,23 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--rows", default="", help="W:R,... band heights for the direct band calls")
     ap.add_argument("--cfgs", default="-1", help="comma list of band kernel configurations to time")
+    ap.add_argument("--wgrad-only", action="store_true", help="time the weight gradient only (stride 1 and 2)")
     a = ap.parse_args()
     C = load()
     rows = {int(k): int(v) for k, v in (p.split(":") for p in a.rows.split(",") if p)}
     g = torch.Generator(device="cuda").manual_seed(0)
+    if a.wgrad_only:
+        for c, hw, st in ((64, 56, 1), (128, 28, 1), (256, 14, 1), (512, 7, 1), (128, 56, 2), (256, 28, 2), (512, 14, 2)):
+            x = torch.randn(a.batch, c, hw, hw, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+                memory_format=torch.channels_last)
+            oh = (hw - 1) // st + 1
+            dy = torch.randn(a.batch, c, oh, oh, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+                memory_format=torch.channels_last)
+            w = torch.empty(c, c, 3, 3, device="cuda", dtype=torch.bfloat16)
+            t = timed(lambda: C.conv3x3_wgrad_patch(dy, x, st, w), a.iters)
+            fl = 2.0 * a.batch * oh * oh * c * 9 * c
+            print(f"wgrad C{c} {hw}x{hw} s{st}: {t:7.1f} us {fl / t / 1e6:6.0f} TF/s", flush=True)
+        return
     cfgs = [int(c) for c in a.cfgs.split(",")]
     print(f"{'shape':18s} {'path fwd':>14s} {'path dgrad':>14s} {'wgrad':>14s} " +
           " ".join(f"{'band%d fwd' % c:>14s} {'band%d dgrad' % c:>14s}" for c in cfgs))
