@@ -1,7 +1,8 @@
 """Time the flash attention forward at the ViT-L/16 bs256 head shape (B256, S197, H16, D64).
 
 usage: python scripts/fa_vit_time.py
-Prints one JSON line: us per forward call and per forward + backward.
+Prints one JSON line: us per forward call, per forward + backward through autograd (q / k / v
+views of one qkv tensor), and per call of the backward kernels alone.
 """
 import json
 import os
@@ -47,5 +48,20 @@ for _ in range(iters):
 e1.record()
 torch.cuda.synchronize()
 fb = e0.elapsed_time(e1) * 1e3 / iters
+# the backward kernels alone (delta pre-pass + dK/dV/dQ), as the encoder block calls them
+from distributeddataparallel_amd._native import load  # noqa: E402
+
+C = load()
+qd, kd, vd = (t.detach() for t in (q, k, v))
+o, lse = C.flash_attn_forward(qd, kd, vd, False, D ** -0.5)[:2]
+for _ in range(3):
+    C.flash_attn_backward(g, qd, kd, vd, o, lse, False, D ** -0.5, None, None, None)
+torch.cuda.synchronize()
+e0.record()
+for _ in range(iters):
+    C.flash_attn_backward(g, qd, kd, vd, o, lse, False, D ** -0.5, None, None, None)
+e1.record()
+torch.cuda.synchronize()
+bw = e0.elapsed_time(e1) * 1e3 / iters
 print(json.dumps({"shape": [B, S, H, D], "fwd_us": round(us, 1),
-                  "tflops": round(tf, 1), "fwd_bwd_us": round(fb, 1)}))
+                  "tflops": round(tf, 1), "fwd_bwd_us": round(fb, 1), "bwd_kernels_us": round(bw, 1)}))
