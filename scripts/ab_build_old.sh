@@ -17,7 +17,7 @@ restore() { for f in "$@"; do cp "$keep/$f" "$f"; done; }
 trap 'restore "$@"' EXIT
 timeout 1800 python -c "import __graft_entry__ as g; g.build()" > /tmp/ab_build_old.log 2>&1
 mkdir -p ab_old/distributeddataparallel_amd
-(cd distributeddataparallel_amd && tar cf - --exclude=build --exclude=__pycache__ --exclude=csrc .) | (cd ab_old/distributeddataparallel_amd && tar xf -)
+(cd distributeddataparallel_amd && tar cf - --exclude=build --exclude="build_san_*" --exclude=__pycache__ --exclude=csrc .) | (cd ab_old/distributeddataparallel_amd && tar xf -)
 cp bench.py ab_old/
 ln -s ../tuning ab_old/tuning
 restore "$@"
