@@ -663,7 +663,11 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
   const int tap = KS == 3 ? k0 / Cin : 0, tap_c0 = KS == 3 ? k0 - tap * Cin : 0;
   const int tap_r = tap / 3, tap_s = tap - 3 * (tap / 3);
 
-  u32x4 sa[LA], sb[LB], sa2[PRO ? LA : 1];
+  // Two register slots: the loads of step m + 2·BM go out while step m computes, so each load has
+  // two steps of MFMAs (not one) to land. Loads are unconditional (rows clamped to M - 1, always
+  // valid memory) and the rows past the range are zeroed when a slot is stored: a conditional
+  // load or a select right after it would make the compiler wait for every load in flight.
+  u32x4 sa[2][LA], sb[2][LB], sa2[2][PRO ? LA : 1];
   float pa[8], pb[8], pc[8], pms[8], pmt[8];  // this thread's 8 dY channels (fixed: 256 % CA == 0)
   if (PRO) {
     const int c = tid % CA;
@@ -675,50 +679,41 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
       dev::Vec8<float>::ld(coef + 4 * N + n0 + c * 8, pmt);
     }
   }
-  auto load = [&](int m) {
+  auto load = [&](int slot, int m) {
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int q = tid + 256 * i, row = q / CA, c = q - (q / CA) * CA;
-      const int mm = m + row;
-      const int64_t off = (int64_t)min(mm, M - 1) * N + n0 + c * 8;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(dY + off);
-      if (PRO) {
-        sa[i] = v;  // the row-range select happens after the transform (store)
-        sa2[i] = *reinterpret_cast<const u32x4*>(Y2 + off);
-      } else {
-        sa[i] = mm < m_end ? v : u32x4{0, 0, 0, 0};  // rows past the range contribute zero
-      }
+      const int64_t off = (int64_t)min(m + row, M - 1) * N + n0 + c * 8;
+      sa[slot][i] = *reinterpret_cast<const u32x4*>(dY + off);
+      if (PRO) sa2[slot][i] = *reinterpret_cast<const u32x4*>(Y2 + off);
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int q = tid + 256 * i, row = q / CB, c = q - (q / CB) * CB;
-      const int mm = m + row;
+      const int mm = min(m + row, M - 1);
       if (KS == 3) {
-        const int mc = min(mm, M - 1), hw = rm.OH * rm.OW;
-        const int b = mc / hw, rem = mc - b * hw, oh = rem / rm.OW, ow = rem - oh * rm.OW;
-        const int ih = oh * rm.stride - 1 + tap_r, iw = ow * rm.stride - 1 + tap_s;
-        const bool ok = mm < m_end && (unsigned)ih < (unsigned)rm.IH && (unsigned)iw < (unsigned)rm.IW;
-        const u32x4 v = *reinterpret_cast<const u32x4*>(
-            X + (((int64_t)b * rm.IH + (ok ? ih : 0)) * rm.IW + (ok ? iw : 0)) * Cin + tap_c0 + c * 8);
-        sb[i] = ok ? v : u32x4{0, 0, 0, 0};
+        const int hw = rm.OH * rm.OW;
+        const int b = mm / hw, rem = mm - b * hw, oh = rem / rm.OW, ow = rem - oh * rm.OW;
+        const int ih = min(max(oh * rm.stride - 1 + tap_r, 0), rm.IH - 1);
+        const int iw = min(max(ow * rm.stride - 1 + tap_s, 0), rm.IW - 1);  // (padding taps zeroed at store)
+        sb[slot][i] = *reinterpret_cast<const u32x4*>(X + (((int64_t)b * rm.IH + ih) * rm.IW + iw) * Cin + tap_c0 + c * 8);
       } else {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(X + rm.in_row<STRIDED>(min(mm, M - 1)) * K + k0 + c * 8);
-        sb[i] = mm < m_end ? v : u32x4{0, 0, 0, 0};
+        sb[slot][i] = *reinterpret_cast<const u32x4*>(X + rm.in_row<STRIDED>(mm) * K + k0 + c * 8);
       }
     }
   };
-  auto store = [&](int buf, int m) {
+  auto store = [&](int buf, int slot, int m) {
     uint8_t* A = smem + buf * BUF;
     uint8_t* B = A + ABYTES;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int q = tid + 256 * i, row = q / CA, c = q - (q / CA) * CA;
+      u32x4 t = sa[slot][i];
       if (PRO) {
-        u32x4 t;
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
-          float g0 = __uint_as_float(sa[i][h] << 16), g1 = __uint_as_float(sa[i][h] & 0xffff0000u);
-          const float x0 = __uint_as_float(sa2[i][h] << 16), x1 = __uint_as_float(sa2[i][h] & 0xffff0000u);
+          float g0 = __uint_as_float(sa[slot][i][h] << 16), g1 = __uint_as_float(sa[slot][i][h] & 0xffff0000u);
+          const float x0 = __uint_as_float(sa2[slot][i][h] << 16), x1 = __uint_as_float(sa2[slot][i][h] & 0xffff0000u);
           if (PRO == 3) {
             g0 = fmaf(x0, pms[2 * h], pmt[2 * h]) > 0.f ? g0 : 0.f;
             g1 = fmaf(x1, pms[2 * h + 1], pmt[2 * h + 1]) > 0.f ? g1 : 0.f;
@@ -726,14 +721,20 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
           t[h] = dev::pack_bf16x2(fmaf(pa[2 * h], g0, fmaf(pb[2 * h], x0, pc[2 * h])),
                                   fmaf(pa[2 * h + 1], g1, fmaf(pb[2 * h + 1], x1, pc[2 * h + 1])));
         }
-        sa[i] = m + row < m_end ? t : u32x4{0, 0, 0, 0};
       }
-      *reinterpret_cast<u32x4*>(A + row * SA + c * 16) = sa[i];
+      *reinterpret_cast<u32x4*>(A + row * SA + c * 16) = m + row < m_end ? t : u32x4{0, 0, 0, 0};
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int q = tid + 256 * i, row = q / CB, c = q - (q / CB) * CB;
-      *reinterpret_cast<u32x4*>(B + row * SB + c * 16) = sb[i];
+      bool ok = m + row < m_end;
+      if (KS == 3) {
+        const int mm = min(m + row, M - 1), hw = rm.OH * rm.OW;
+        const int b = mm / hw, rem = mm - b * hw, oh = rem / rm.OW, ow = rem - oh * rm.OW;
+        const int ih = oh * rm.stride - 1 + tap_r, iw = ow * rm.stride - 1 + tap_s;
+        ok = ok && (unsigned)ih < (unsigned)rm.IH && (unsigned)iw < (unsigned)rm.IW;
+      }
+      *reinterpret_cast<u32x4*>(B + row * SB + c * 16) = ok ? sb[slot][i] : u32x4{0, 0, 0, 0};
     }
   };
 
@@ -745,43 +746,52 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
 
   // transposed-read addressing: lane (4q + p) of its 16-lane group addresses row q, columns 4p..4p+3
   const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-  if (m_begin < m_end) {
-    load(m_begin);
-    store(0, m_begin);
-    lds_barrier();
-    int cur = 0;
-    for (int m = m_begin; m < m_end; m += BM) {
-      const bool more = m + BM < m_end;
-      if (more) load(m + BM);  // in flight during the MFMAs below
-      const uint8_t* A = smem + cur * BUF;
-      const uint8_t* B = A + ABYTES;
+  auto compute = [&](int cur) {
+    const uint8_t* A = smem + cur * BUF;
+    const uint8_t* B = A + ABYTES;
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int r0 = s2 * 32 + 8 * g + q4;
-        bf16x8 a[FN], b[FK];
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r0 = s2 * 32 + 8 * g + q4;
+      bf16x8 a[FN], b[FK];
 #pragma unroll
-        for (int i = 0; i < FN; ++i) {
-          const int col = wn * WTN + i * 16 + 4 * p4;
-          const v4s lo = lds_tr16(A + r0 * SA + col * 2), hi = lds_tr16(A + (r0 + 4) * SA + col * 2);
-          const v4s v8[2] = {lo, hi};
-          a[i] = __builtin_bit_cast(bf16x8, v8);
-        }
-#pragma unroll
-        for (int j = 0; j < FK; ++j) {
-          const int col = wk * WTK + j * 16 + 4 * p4;
-          const v4s lo = lds_tr16(B + r0 * SB + col * 2), hi = lds_tr16(B + (r0 + 4) * SB + col * 2);
-          const v4s v8[2] = {lo, hi};
-          b[j] = __builtin_bit_cast(bf16x8, v8);
-        }
-#pragma unroll
-        for (int i = 0; i < FN; ++i)
-#pragma unroll
-          for (int j = 0; j < FK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < FN; ++i) {
+        const int col = wn * WTN + i * 16 + 4 * p4;
+        const v4s lo = lds_tr16(A + r0 * SA + col * 2), hi = lds_tr16(A + (r0 + 4) * SA + col * 2);
+        const v4s v8[2] = {lo, hi};
+        a[i] = __builtin_bit_cast(bf16x8, v8);
       }
-      if (more) store(cur ^ 1, m + BM);
-      lds_barrier();
-      cur ^= 1;
+#pragma unroll
+      for (int j = 0; j < FK; ++j) {
+        const int col = wk * WTK + j * 16 + 4 * p4;
+        const v4s lo = lds_tr16(B + r0 * SB + col * 2), hi = lds_tr16(B + (r0 + 4) * SB + col * 2);
+        const v4s v8[2] = {lo, hi};
+        b[j] = __builtin_bit_cast(bf16x8, v8);
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+  };
+  if (m_begin < m_end) {
+    // step pairs (slot 0 = even steps, LDS buffer 0; slot 1 = odd steps, buffer 1), branch-free
+    // loads; the steps past m_end of the last pair compute on zero rows (stored zeroed)
+    load(0, m_begin);
+    load(1, m_begin + BM);
+    store(0, 0, m_begin);
+    lds_barrier();
+    for (int m = m_begin; m < m_end; m += 2 * BM) {
+      load(0, m + 2 * BM);  // (clamped rows: always valid memory)
+      compute(0);
+      store(1, 1, m + BM);
+      lds_barrier();
+      if (m + BM >= m_end) break;  // (uniform) an odd step count: the last odd step is empty
+      load(1, m + 3 * BM);
+      compute(1);
+      store(0, 0, m + 2 * BM);
+      lds_barrier();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing prefetch loads retire here
   }
   // fp32 slab of this pixel range: ws[sidx][n][k]; lane holds rows n = (lane>>4)*4 + r, col k = lane&15
   float* out = ws + (int64_t)sidx * N * K;
