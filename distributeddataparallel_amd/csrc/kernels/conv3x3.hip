@@ -295,6 +295,36 @@ __global__ __launch_bounds__(256) void rot_weight_kernel(const uint16_t* __restr
   }
 }
 
+// Several weights in one launch (the model's 3x3 weights once per step, ops/conv_bn.py): block b
+// belongs to the tensor whose first block is the largest start <= b, then runs as above.
+constexpr int kRotMax = 32;
+struct RotBatch {
+  const uint16_t* w[kRotMax];
+  uint16_t* out[kRotMax];
+  int N[kRotMax], C[kRotMax], start[kRotMax + 1];
+  int count;
+};
+
+__global__ __launch_bounds__(256) void rot_weights_kernel(RotBatch rb) {
+  __shared__ uint16_t tile[64][66];
+  int e = 0;
+  while (e + 1 < rb.count && (int)blockIdx.x >= rb.start[e + 1]) ++e;
+  const int N = rb.N[e], C = rb.C[e], local = (int)blockIdx.x - rb.start[e];
+  const int nb = N / 64, cb = C / 64;
+  const int t = local / (nb * cb), rem = local - t * nb * cb, c0 = (rem / nb) * 64, n0 = (rem % nb) * 64;
+  const uint16_t* w = rb.w[e];
+  uint16_t* out = rb.out[e];
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int r = i >> 6, c = i & 63;
+    tile[r][c] = w[((int64_t)(n0 + r) * 9 + (8 - t)) * C + c0 + c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int r = i >> 6, n = i & 63;
+    out[((int64_t)(c0 + r) * 9 + t) * N + n0 + n] = tile[n][r];
+  }
+}
+
 const uint16_t* zero_line(const at::Tensor& like) {
   // 256 zero bytes per device that padding lanes read instead of branching; never freed (a
   // static tensor would be destroyed after the HIP runtime at exit)
@@ -446,6 +476,40 @@ at::Tensor conv3x3_rot_weight(const at::Tensor& w) {
                      (int)N, (int)C);
   XDDP_HIP_CHECK(hipGetLastError());
   return out;
+}
+
+// conv3x3_rot_weight of every tensor in ws (same device) in one launch per 32 tensors
+std::vector<at::Tensor> conv3x3_rot_weights(const std::vector<at::Tensor>& ws) {
+  std::vector<at::Tensor> outs;
+  outs.reserve(ws.size());
+  for (size_t i0 = 0; i0 < ws.size(); i0 += kRotMax) {
+    RotBatch rb{};
+    int total = 0;
+    const size_t i1 = std::min(ws.size(), i0 + kRotMax);
+    for (size_t i = i0; i < i1; ++i) {
+      const at::Tensor& w = ws[i];
+      TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 3 &&
+                      w.size(3) == 3 && w.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                      w.device() == ws[i0].device(),
+                  "conv3x3_rot_weights: bf16 [N, C, 3, 3] channels_last weights on one device expected");
+      const int64_t N = w.size(0), C = w.size(1);
+      TORCH_CHECK(N % 64 == 0 && C % 64 == 0, "conv3x3_rot_weights: channel counts must be multiples of 64");
+      outs.push_back(at::empty({C, N, 3, 3}, w.options().memory_format(at::MemoryFormat::ChannelsLast)));
+      const int e = (int)(i - i0);
+      rb.w[e] = reinterpret_cast<const uint16_t*>(w.data_ptr());
+      rb.out[e] = reinterpret_cast<uint16_t*>(outs.back().data_ptr());
+      rb.N[e] = (int)N;
+      rb.C[e] = (int)C;
+      rb.start[e] = total;
+      total += (int)((N / 64) * (C / 64) * 9);
+    }
+    rb.count = (int)(i1 - i0);
+    rb.start[rb.count] = total;
+    auto stream = c10::hip::getCurrentHIPStream(ws[i0].device().index()).stream();
+    hipLaunchKernelGGL(rot_weights_kernel, dim3(total), dim3(256), 0, stream, rb);
+    XDDP_HIP_CHECK(hipGetLastError());
+  }
+  return outs;
 }
 
 }  // namespace kernels

@@ -66,6 +66,7 @@ int conv3x3_band_rows(int64_t W, int64_t H, int64_t bm);
 std::vector<at::Tensor> conv3x3_band_forward(const at::Tensor& x, const at::Tensor& w, bool stats, int64_t rows,
                                              int64_t cfg);
 at::Tensor conv3x3_rot_weight(const at::Tensor& w);
+std::vector<at::Tensor> conv3x3_rot_weights(const std::vector<at::Tensor>& ws);
 at::Tensor conv3x3_dgrad_s2(const at::Tensor& dy, const at::Tensor& w_rot, int64_t H, int64_t W);
 at::Tensor conv3x3_dgrad_s2_gemm(const at::Tensor& dy, const at::Tensor& wr, int64_t XH, int64_t XW,
                                  const uint16_t* zeros);

@@ -34,6 +34,7 @@ void bind_norm_kernels(py::module_& m) {
   m.def("bn_grad_partials", &bn_grad_partials, py::arg("dy"), py::arg("x"), py::arg("mean"));
   m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("stats"));
   m.def("conv3x3_rot_weight", &conv3x3_rot_weight, py::arg("w"));
+  m.def("conv3x3_rot_weights", &conv3x3_rot_weights, py::arg("ws"));
   m.def("conv3x3_band_forward", &conv3x3_band_forward, py::arg("x"), py::arg("w"), py::arg("stats"),
         py::arg("rows") = 0, py::arg("cfg") = -1);
   m.def("conv3x3_dgrad_s2", &conv3x3_dgrad_s2, py::arg("dy"), py::arg("w_rot"), py::arg("H"), py::arg("W"));

@@ -21,6 +21,7 @@ state_dict layout and DDP bucketing are unchanged.
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Optional
 
 import torch
@@ -344,11 +345,41 @@ def _bwd_fused_ok(ctx, C, w) -> bool:
             and C.conv1x1_bwd_fused_supported(w.shape[0], w.shape[1]))
 
 
+# The input gradients read the 180-degree-rotated, channel-swapped 3x3 weights. Each forward marks
+# its weight stale; the first 3x3 backward of the step rotates every stale weight in ONE launch
+# (conv3x3_rot_weights) instead of one small kernel per layer (16 per ResNet-50 step, ~5 us each).
+# Staleness comes from the forward, not from the tensor version: fused optimizers write parameter
+# memory without bumping it.
+_ROT_PENDING: dict = {}  # id(w) -> weakref(w), marked by a forward, rotated by the next backward
+_ROT_CACHE: dict = {}    # id(w) -> (weakref(w), data_ptr, rotated weight)
+
+
+def _rot_mark(w):
+    _ROT_PENDING[id(w)] = weakref.ref(w)
+    _ROT_CACHE.pop(id(w), None)
+
+
+def _rot_weight(C, w):
+    hit = _ROT_CACHE.get(id(w))
+    if hit is not None and hit[0]() is w and hit[1] == w.data_ptr():
+        return hit[2]
+    batch = [t for t in (r() for r in _ROT_PENDING.values()) if t is not None and t.device == w.device]
+    if not any(t is w for t in batch):
+        batch.append(w)
+    for k in [k for k, e in _ROT_CACHE.items() if e[0]() is None]:  # weights that are gone
+        del _ROT_CACHE[k]
+    for t, r in zip(batch, C.conv3x3_rot_weights(batch)):
+        _ROT_CACHE[id(t)] = (weakref.ref(t), t.data_ptr(), r)
+        _ROT_PENDING.pop(id(t), None)
+    return _ROT_CACHE[id(w)][2]
+
+
 class _Conv3x3BNReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, stride, pend_out):
         C = load()
         ctx.set_materialize_grads(False)
+        _rot_mark(w)
         y, part = C.conv3x3_forward(x, w, stride, True)
         M = y.numel() // y.size(1)
         mean, invstd, ss = C.bn_stats_from_partials(part, M, weight, bias, running_mean, running_var, nbt, momentum,
@@ -379,11 +410,11 @@ class _Conv3x3BNReLU(torch.autograd.Function):
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dx = dw = None
         if need_x and s == 1:
-            dx = C.conv3x3_forward(dy, C.conv3x3_rot_weight(w), 1, False)[0]
+            dx = C.conv3x3_forward(dy, _rot_weight(C, w), 1, False)[0]
         elif need_x:
             # four phase grids of the strided dX, 1/2/2/4 taps each, one launch (conv3x3.hip DG2):
             # 142 / 97 / 86 vs MIOpen's 170 / 141 / 136 us (profiles/r4_s2_bwd_vs_miopen.txt)
-            dx = C.conv3x3_dgrad_s2(dy, C.conv3x3_rot_weight(w), x.size(2), x.size(3))
+            dx = C.conv3x3_dgrad_s2(dy, _rot_weight(C, w), x.size(2), x.size(3))
         if need_w:
             # 8x8 output patches sharing one staged X halo across the 9 taps (conv3x3_wgrad.hip):
             # 96-98 us vs MIOpen's 120-182 us per stride-1 ResNet-50 shape (bs256); at stride 2 the

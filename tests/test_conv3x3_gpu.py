@@ -64,6 +64,48 @@ def test_conv3x3_rotated_weight_gives_input_gradient(cin, cout, h, w):
     torch.testing.assert_close(dx.float(), xr.grad, rtol=1e-2, atol=1e-2 * xr.grad.abs().max().item())
 
 
+def test_conv3x3_rot_weights_batched_matches_single():
+    """One launch over several weights (40 > one 32-tensor batch) equals the per-tensor rotation."""
+    torch.manual_seed(4)
+    ws = [_cl(torch.randn(64 * (1 + i % 4), 64 * (1 + (i // 4) % 3), 3, 3, device="cuda")) for i in range(40)]
+    outs = C.conv3x3_rot_weights(ws)
+    for w, o in zip(ws, outs):
+        assert torch.equal(o, C.conv3x3_rot_weight(w))
+
+
+def test_conv3x3_rotated_weights_follow_in_place_updates():
+    """The backward's rotated weights are recomputed after every forward (the fused optimizers
+    write parameter memory in place without bumping the tensor version): two steps with an
+    in-place weight change in between give the same input gradients as fresh modules."""
+    from distributeddataparallel_amd.ops import FusedBatchNorm2d, conv3x3_bn_relu
+
+    torch.manual_seed(5)
+    conv = torch.nn.Conv2d(64, 64, 3, padding=1, bias=False).cuda().to(torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    bn = FusedBatchNorm2d(64).cuda().to(torch.bfloat16)
+    bn.relu = True
+    x = _cl(torch.randn(2, 64, 12, 12, device="cuda")).requires_grad_()
+    g = torch.randn(2, 64, 12, 12, device="cuda", dtype=torch.bfloat16)
+    for step in range(2):
+        x.grad = None
+        conv3x3_bn_relu(x, conv, bn).backward(g)
+        got = x.grad.clone()
+        ref_conv = torch.nn.Conv2d(64, 64, 3, padding=1, bias=False).cuda().to(torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        ref_bn = FusedBatchNorm2d(64).cuda().to(torch.bfloat16)
+        ref_bn.relu = True
+        ref_conv.load_state_dict(conv.state_dict())
+        ref_bn.load_state_dict(bn.state_dict())
+        xr = x.detach().clone().requires_grad_()
+        ref_bn.train()
+        with torch.no_grad():  # the same batch statistics: start from bn's pre-step running stats
+            ref_bn.running_mean.copy_(bn.running_mean)
+        conv3x3_bn_relu(xr, ref_conv, ref_bn).backward(g)
+        assert torch.equal(got, xr.grad), step
+        with torch.no_grad():
+            conv.weight.data.mul_(-0.5).add_(0.01)  # an in-place update the next step must see
+
+
 @pytest.mark.parametrize("b,cin,h,w,cout", [
     (2, 128, 10, 11, 64),    # odd width: phase grids of unequal size
     (3, 64, 15, 15, 128),    # odd input: the last dY row/column feeds the even phase only
