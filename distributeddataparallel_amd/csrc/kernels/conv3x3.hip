@@ -371,9 +371,10 @@ std::vector<at::Tensor> conv3x3_forward(const at::Tensor& x, const at::Tensor& w
   if (stride == 1 && IW >= 14 && (N == 64 || N % 128 == 0) && conv3x3_band_rows(IW, IH, N == 64 ? 224 : 208) > 0 &&
       x.numel() < (int64_t(1) << 31) && M * N < (int64_t(1) << 31))
     return conv3x3_band(x, w, stats, 0, zero_line(x));
-  // N >= 256 (the W = 7 stride-1 layer, the stride-2 layers) on the dense GEMM's 4-phase LDS-DMA
+  // N % 128 == 0 (the W = 7 stride-1 layer, the stride-2 layers) on the dense GEMM's 4-phase LDS-DMA
   // pipeline with im2col addressing (gemm.hip ConvGeo)
-  if (N >= 256 && N % 128 == 0 && x.numel() < (int64_t(1) << 31) && ((C / 64) & (C / 64 - 1)) == 0)
+  // (r5: N = 128 too — the stride-2 layer2.0 conv2, 98.5 vs 105.9 us on conv3x3_fwd_kernel)
+  if (N >= 128 && N % 128 == 0 && x.numel() < (int64_t(1) << 31) && ((C / 64) & (C / 64 - 1)) == 0)
     return conv3x3_gemm(x, w, stride, stats, zero_line(x));
   auto y = at::empty({B, N, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int cfg = tile_choice((int)N);
