@@ -635,16 +635,13 @@ __global__ __launch_bounds__(256) void bn_partial_finalize_kernel(
 // PRO (2, 3): dY = a_n·G + b_n·Y2 + c_n is formed while staging (the BatchNorm-backward
 // elementwise pass folded in; G is the masked upstream gradient, Y2 the BN input; with 3 the ReLU
 // mask (Y2·s_n + t_n > 0) is applied to G here).
-// KS = 3: the 3x3 (pad 1) weight gradient dW[n][tap][c]: the K columns are 9 taps x Cin
-// channels, a column tile lies in one tap, and its X rows are the tap-shifted input pixels (zero
-// outside the image) — an implicit im2col of the B operand, never materialized.
-template <int TN, int TK, bool STRIDED, int PRO, int KS = 1>
+template <int TN, int TK, bool STRIDED, int PRO>
 __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* __restrict__ dY,
                                                                 const uint16_t* __restrict__ X,
                                                                 float* __restrict__ ws, int M, int N, int K,
                                                                 RowMap rm, int ntiles, int ktiles, int mchunk,
                                                                 const uint16_t* __restrict__ Y2,
-                                                                const float* __restrict__ coef, int Cin) {
+                                                                const float* __restrict__ coef) {
   constexpr int BM = 64;                       // pixel rows per step (two 32-deep MFMA k-steps)
   constexpr int SA = TN * 2 + 32, SB = TK * 2 + 32;
   constexpr int ABYTES = BM * SA, BUF = ABYTES + BM * SB;
@@ -659,9 +656,6 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
   const int sidx = bid / tiles, tile = bid % tiles;  // neighbours share the pixel range (L2 reuse)
   const int n0 = (tile % ntiles) * TN, k0 = (tile / ntiles) * TK;
   const int m_begin = sidx * mchunk, m_end = min(M, m_begin + mchunk);
-  // KS = 3: this column tile's tap (r, s) and first channel
-  const int tap = KS == 3 ? k0 / Cin : 0, tap_c0 = KS == 3 ? k0 - tap * Cin : 0;
-  const int tap_r = tap / 3, tap_s = tap - 3 * (tap / 3);
 
   // Two register slots: the loads of step m + 2·BM go out while step m computes, so each load has
   // two steps of MFMAs (not one) to land. Loads are unconditional (rows clamped to M - 1, always
@@ -690,16 +684,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int q = tid + 256 * i, row = q / CB, c = q - (q / CB) * CB;
-      const int mm = min(m + row, M - 1);
-      if (KS == 3) {
-        const int hw = rm.OH * rm.OW;
-        const int b = mm / hw, rem = mm - b * hw, oh = rem / rm.OW, ow = rem - oh * rm.OW;
-        const int ih = min(max(oh * rm.stride - 1 + tap_r, 0), rm.IH - 1);
-        const int iw = min(max(ow * rm.stride - 1 + tap_s, 0), rm.IW - 1);  // (padding taps zeroed at store)
-        sb[slot][i] = *reinterpret_cast<const u32x4*>(X + (((int64_t)b * rm.IH + ih) * rm.IW + iw) * Cin + tap_c0 + c * 8);
-      } else {
-        sb[slot][i] = *reinterpret_cast<const u32x4*>(X + rm.in_row<STRIDED>(mm) * K + k0 + c * 8);
-      }
+      sb[slot][i] = *reinterpret_cast<const u32x4*>(X + rm.in_row<STRIDED>(min(m + row, M - 1)) * K + k0 + c * 8);
     }
   };
   auto store = [&](int buf, int slot, int m) {
@@ -727,14 +712,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_wgrad_kernel(const uint16_t* _
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const int q = tid + 256 * i, row = q / CB, c = q - (q / CB) * CB;
-      bool ok = m + row < m_end;
-      if (KS == 3) {
-        const int mm = min(m + row, M - 1), hw = rm.OH * rm.OW;
-        const int b = mm / hw, rem = mm - b * hw, oh = rem / rm.OW, ow = rem - oh * rm.OW;
-        const int ih = oh * rm.stride - 1 + tap_r, iw = ow * rm.stride - 1 + tap_s;
-        ok = ok && (unsigned)ih < (unsigned)rm.IH && (unsigned)iw < (unsigned)rm.IW;
-      }
-      *reinterpret_cast<u32x4*>(B + row * SB + c * 16) = ok ? sb[slot][i] : u32x4{0, 0, 0, 0};
+      *reinterpret_cast<u32x4*>(B + row * SB + c * 16) = m + row < m_end ? sb[slot][i] : u32x4{0, 0, 0, 0};
     }
   };
 
@@ -1275,8 +1253,7 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stri
     ensure_dyn_lds((const void*)kern, lds);
     hipLaunchKernelGGL(kern, dim3(S * tiles), dim3(256), lds, stream,
                        reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                       ws.data_ptr<float>(), (int)M, (int)N, (int)K, rm, ntiles, ktiles, (int)mchunk, y2p, cfp,
-                       (int)K);
+                       ws.data_ptr<float>(), (int)M, (int)N, (int)K, rm, ntiles, ktiles, (int)mchunk, y2p, cfp);
     XDDP_HIP_CHECK(hipGetLastError());
   };
   const bool strided = stride > 1;
@@ -1355,59 +1332,6 @@ std::vector<at::Tensor> conv1x1_bwd_fused(const at::Tensor& g, const at::Tensor&
   return {dx, dw};
 }
 
-// 3x3 (pad 1, stride 1/2) weight gradient: dy [B, N, OH, OW], x [B, C, IH, IW] (bf16
-// channels_last) -> dW [N, C, 3, 3] channels_last (OHWI memory) in w_like's dtype.
-at::Tensor conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like) {
-  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 &&
-                  dy.dim() == 4 && x.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
-                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "conv3x3_wgrad: bf16 channels_last 4-D GPU tensors expected");
-  TORCH_CHECK(stride == 1 || stride == 2, "conv3x3_wgrad: stride 1 or 2");
-  const int64_t B = x.size(0), C = x.size(1), IH = x.size(2), IW = x.size(3), N = dy.size(1);
-  const int64_t OH = (IH - 1) / stride + 1, OW = (IW - 1) / stride + 1;
-  TORCH_CHECK(dy.size(0) == B && dy.size(2) == OH && dy.size(3) == OW, "conv3x3_wgrad: dy/x shape mismatch");
-  TORCH_CHECK(N % 64 == 0 && C % 64 == 0, "conv3x3_wgrad: channel counts must be multiples of 64");
-  const int64_t M = B * OH * OW, K = 9 * C;
-  TORCH_CHECK(M > 0 && M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "conv3x3_wgrad: bad size");
-  const int TN = N % 128 == 0 ? 128 : 64, TK = C % 128 == 0 ? 128 : 64;  // a column tile stays in one tap
-  const int ntiles = (int)(N / TN), ktiles = (int)(K / TK), tiles = ntiles * ktiles;
-  const int64_t steps = (M + 63) / 64;
-  int S = (int)std::max<int64_t>(1, std::min<int64_t>(steps, (int64_t)num_cus() * 2 / tiles));
-  const int64_t mchunk = ((steps + S - 1) / S) * 64;
-  S = (int)((M + mchunk - 1) / mchunk);
-  auto ws = at::empty({S, N, K}, dy.options().dtype(at::kFloat));
-  auto dw = at::empty({N, C, 3, 3}, dy.options().dtype(w_like.scalar_type()).memory_format(at::MemoryFormat::ChannelsLast));
-  auto stream = c10::hip::getCurrentHIPStream(dy.device().index()).stream();
-  RowMap rm{(int)OH, (int)OW, (int)IH, (int)IW, (int)stride};
-  const size_t lds = 2 * (size_t)64 * ((TN * 2 + 32) + (TK * 2 + 32));
-  auto go = [&](auto kern) {
-    ensure_dyn_lds((const void*)kern, lds);
-    hipLaunchKernelGGL(kern, dim3(S * tiles), dim3(256), lds, stream,
-                       reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                       ws.data_ptr<float>(), (int)M, (int)N, (int)K, rm, ntiles, ktiles, (int)mchunk, nullptr, nullptr,
-                       (int)C);
-    XDDP_HIP_CHECK(hipGetLastError());
-  };
-  if (TN == 128 && TK == 128) go(conv1x1_wgrad_kernel<128, 128, false, 0, 3>);
-  else if (TN == 128) go(conv1x1_wgrad_kernel<128, 64, false, 0, 3>);
-  else if (TK == 128) go(conv1x1_wgrad_kernel<64, 128, false, 0, 3>);
-  else go(conv1x1_wgrad_kernel<64, 64, false, 0, 3>);
-  const int64_t nk = N * K;
-  const int grid = (int)((nk / 4 + 63) / 64);
-  auto red = [&](auto tag) {
-    using W = decltype(tag);
-    hipLaunchKernelGGL((wgrad_reduce_kernel<W>), dim3(grid), dim3(512), 0, stream, ws.data_ptr<float>(), S, nk,
-                       reinterpret_cast<W*>(dw.data_ptr()));
-    XDDP_HIP_CHECK(hipGetLastError());
-  };
-  switch (w_like.scalar_type()) {
-    case at::kBFloat16: red(dev::bf16_t{}); break;
-    case at::kFloat: red(float{}); break;
-    case at::kHalf: red(dev::f16_t{}); break;
-    default: TORCH_CHECK(false, "conv3x3_wgrad: unsupported weight dtype");
-  }
-  return dw;
-}
 
 // partials [groups, 3, N] (or [3, N, groups] when group_minor) -> (mean, invstd, scale_shift
 // [2, N]); updates running stats. M = rows behind the partials; M <= 0 = sum the partials' counts.

@@ -70,7 +70,6 @@ std::vector<at::Tensor> conv3x3_rot_weights(const std::vector<at::Tensor>& ws);
 at::Tensor conv3x3_dgrad_s2(const at::Tensor& dy, const at::Tensor& w_rot, int64_t H, int64_t W);
 at::Tensor conv3x3_dgrad_s2_gemm(const at::Tensor& dy, const at::Tensor& wr, int64_t XH, int64_t XW,
                                  const uint16_t* zeros);
-at::Tensor conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like);
 // 3x3 weight gradient over 8x8 output patches with a shared X halo (csrc/kernels/conv3x3_wgrad.hip)
 at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,
                                int64_t splits = -1);

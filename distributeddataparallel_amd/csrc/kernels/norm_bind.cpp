@@ -38,7 +38,6 @@ void bind_norm_kernels(py::module_& m) {
   m.def("conv3x3_band_forward", &conv3x3_band_forward, py::arg("x"), py::arg("w"), py::arg("stats"),
         py::arg("rows") = 0, py::arg("cfg") = -1);
   m.def("conv3x3_dgrad_s2", &conv3x3_dgrad_s2, py::arg("dy"), py::arg("w_rot"), py::arg("H"), py::arg("W"));
-  m.def("conv3x3_wgrad", &conv3x3_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"));
   m.def("conv3x3_wgrad_patch", &conv3x3_wgrad_patch, py::arg("dy"), py::arg("x"), py::arg("stride"), py::arg("w_like"),
         py::arg("splits") = -1);
   m.def("conv1x1_bwd_fused_supported", &conv1x1_bwd_fused_supported, py::arg("N"), py::arg("K"));

@@ -55,9 +55,9 @@ for cin, hw, cout, s, cnt in SHAPES:
         td = timeit(lambda: C.conv3x3_forward(dy, wt, 1, False))
     t.append(td)
     wref = cb(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
-    wgot = C.conv3x3_wgrad(dy, x, s, w)
+    wgot = C.conv3x3_wgrad_patch(dy, x, s, w)
     werr = (wgot.float() - wref.float()).norm().item() / wref.float().norm().item()
-    t.append(timeit(lambda: C.conv3x3_wgrad(dy, x, s, w)))
+    t.append(timeit(lambda: C.conv3x3_wgrad_patch(dy, x, s, w)))
     for i in range(5):
         tot[i] += (t[i] if t[i] == t[i] else t[1]) * cnt
     tot[5] += t[5] * cnt
