@@ -30,8 +30,12 @@
 //
 // Epilogue as conv3x3.hip: the bf16 C tile through LDS, 16-B row stores of the valid pixels (the
 // band's output pixels are contiguous in NHWC memory), BatchNorm (count, mean, M2) partials per
-// channel and tile, group-minor part[3][N][tiles].
+// channel and statistics group, group-minor part[3][N][groups]. With statistics the N = 64
+// configuration runs persistent blocks (two per CU, each walking bands wg, wg + grid, ...) whose
+// shifted sums stay in registers across bands: the cross-lane reduction and partial writes run
+// once per block instead of once per band (r5: 3584 -> 512 groups, C64 forward 108 -> 100 us).
 #include <c10/hip/HIPStream.h>
+#include <cstdlib>
 #include <torch/extension.h>
 
 #include "common.h"
@@ -79,7 +83,8 @@ __device__ __forceinline__ int band_hrow(int lr, int n0, int H) {
 template <int TM, int WM, int TN, int WN, bool STATS, int RING>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv3x3_band_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y,
-    const uint16_t* __restrict__ zeros, int N, BandGeo g, float* __restrict__ part, int ntiles, int hrows) {
+    const uint16_t* __restrict__ zeros, int N, BandGeo g, float* __restrict__ part, int ntiles, int mtiles,
+    int hrows) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
   constexpr int BI = BN / 8 / NW;  // weight DMA wave-instructions per tap
@@ -91,194 +96,204 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv3x3_band_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
   const int wg = dev::xcd_remap(blockIdx.x, gridDim.x);
-  const int nt = wg % ntiles, mt = wg / ntiles;
-  const int g0 = mt * g.R;                       // first output row of the band (flattened b·H + h)
-  const int b0 = g0 / g.H, h0 = g0 - b0 * g.H;
-  const int n0 = min(g.H - h0, g.R);             // rows of the first segment
-  const int rv = min(g.R, g.rows_total - g0);    // valid output rows of the band
-  const int valid = rv * g.W;
-  const int W2 = g.W + 2;
-  const int HP = (band_hrow(rv - 1, n0, g.H) + 3) * W2;  // halo pixels to stage
-  const int n0c = nt * BN, pos = lane & 7, cbn = g.C >> 6, K9 = 9 * g.C;
-
-  // this lane's MFMA A rows -> halo pixel of tap (0, 0) (rows past the band read a valid pixel)
-  int hb[TM], vb[TM];  // LDS row and virtual index (hswz) of the pixel's tap (0, 0) halo pixel
-  const int prow = kperm(lane & 15);
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = min(wm * TM * 16 + i * 16 + prow, valid - 1);
-    const int lr = m / g.W, hr = band_hrow(lr, n0, g.H), col = m - lr * g.W;
-    hb[i] = hr * W2 + col;
-    vb[i] = hr * g.W + col;
-  }
-  int boff[BI];  // (32-bit offsets: host-checked tensors < 2^31 elements)
-#pragma unroll
-  for (int j = 0; j < BI; ++j) {
-    const int row = (wid * BI + j) * 8 + (lane >> 3);
-    boff[j] = (n0c + row) * K9 + 8 * (pos ^ ((row >> 1) & 7));
-  }
-  auto issue_halo = [&](int cb) {
-    for (int k = wid; k * 8 < HP; k += NW) {  // per-wave counts differ: only count-free waits cover it
-      const int q = k * 8 + (lane >> 3), hr = q / W2, hc = q - hr * W2;
-      int b = b0, ih = h0 - 1 + hr;
-      if (hr >= n0 + 2) {  // a later image of the band
-        const int r2 = hr - (n0 + 2), kk = r2 / (g.H + 2);
-        b = b0 + 1 + kk;
-        ih = r2 - kk * (g.H + 2) - 1;
-      }
-      const int iw = hc - 1;
-      const bool ok = q < HP && b < g.B && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-      const uint16_t* src =
-          ok ? X + (((b * g.H + ih) * g.W + iw) * g.C + cb * 64 + 8 * (pos ^ (((hr * g.W + hc) >> 1) & 7))) : zeros;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(halo + k * 1024), 16, 0, 0);
-    }
-  };
-  auto issue_w = [&](int cb, int t, int slot) {
-    uint8_t* Bs = ring + slot * BN * 128;
-    const int wk = t * g.C + cb * 64;
-#pragma unroll
-    for (int j = 0; j < BI; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(Wt + boff[j] + wk), (lds_ptr_t)(Bs + (wid * BI + j) * 1024), 16,
-                                       0, 0);
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if constexpr (RING == 0) {
-    // B in registers: each wave loads its own TN column tiles straight from global memory (the
-    // weights are L2-resident), per 32-deep half step, three half steps deep; taps need no barrier
-    // and no ring, only the halo goes through LDS (one barrier per 64-channel step)
-    bf16x8 breg[3][TN];
-    const uint16_t* wl = Wt + (int64_t)(n0c + wn * TN * 16 + (lane & 15)) * K9 + (lane >> 4) * 8;
-    auto load_b = [&](int cb, int u, bf16x8 (&dst)[TN]) {  // half step u = 2·tap + half
-      const uint16_t* p = wl + (u >> 1) * g.C + cb * 64 + (u & 1) * 32;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) dst[j] = *reinterpret_cast<const bf16x8*>(p + j * 16 * K9);
-    };
-    issue_halo(0);
-    load_b(0, 0, breg[0]);
-    load_b(0, 1, breg[1]);
-    for (int cb = 0; cb < cbn; ++cb) {
-      if (cb > 0) {
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave is done with the halo
-        issue_halo(cb);
-      }
-      const bool last = cb + 1 == cbn;
-      // opaque per step: keeps the compiler from hoisting all 18 x TM LDS addresses of the unrolled
-      // half steps out of the channel loop (they are loop-invariant; live, they spill)
-#pragma unroll
-      for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(hb[i]), "+v"(vb[i]));
-#pragma unroll
-      for (int u = 0; u < 18; ++u) {
-        __builtin_amdgcn_sched_barrier(0);  // keep each half step's LDS reads in it (register pressure)
-        // half step u's B fragments (and at u = 0 the halo) must have landed; the loads issued after
-        // them (the next half step's B) may stay in flight
-        if (u == 0) {
-          if (cb == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TN) : "memory");
-          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          asm volatile("s_barrier" ::: "memory");  // every wave's halo DMA is visible
-        } else if (u == 17 && last) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TN) : "memory");
-        }
-        if (u + 2 < 18) load_b(cb, u + 2, breg[(u + 2) % 3]);
-        else if (!last) load_b(cb + 1, u - 16, breg[(u + 2) % 3]);
-        const int t = u >> 1, h = u & 1, r = t / 3, sx = t - 3 * r;
-        const int toff = r * W2 + sx, tv = r * g.W + sx, ch = h * 4 + (lane >> 4);
-        bf16x8 a[TM];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(halo + hswz(hb[i] + toff, vb[i] + tv, ch));
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(breg[u % 3][j], a[i], acc[i][j], 0, 0, 0);
-      }
-    }
-  } else {
-    for (int cb = 0; cb < cbn; ++cb) {
-      if (cb > 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // halo / ring reads done
-      issue_halo(cb);
-      issue_w(cb, 0, 0);
-      if (RING == 3) issue_w(cb, 1, 1);
-#pragma unroll 1
-      for (int t = 0; t < 9; ++t) {
-        // retire tap t's weights (at t = 0 also the halo issued before them); with three slots the
-        // next tap's weights may stay in flight
-        if (RING == 3 && t < 8) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BI) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (not unrolled: no cross-tap load hoisting)
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (t + RING - 1 < 9) issue_w(cb, t + RING - 1, (t + RING - 1) % RING);
-        const int r = t / 3, sx = t - 3 * r, toff = r * W2 + sx, tv = r * g.W + sx;
-        const uint8_t* Bs = ring + (t % RING) * BN * 128;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int ch = h * 4 + (lane >> 4);
-          bf16x8 a[TM], bb[TN];
-#pragma unroll
-          for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(halo + hswz(hb[i] + toff, vb[i] + tv, ch));
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            bb[j] = *reinterpret_cast<const bf16x8*>(Bs + swzb(wn * TN * 16 + j * 16 + (lane & 15), ch));
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j], a[i], acc[i][j], 0, 0, 0);
-        }
-      }
-    }
-  }
-
-  // ---- epilogue: bf16 C tile through LDS, 16-B row stores of the valid pixels (+ statistics) ----
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  constexpr int CST = BN * 2 + 16;
-  uint8_t* Cs = smem;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int row = wm * TM * 16 + i * 16 + prow;
-      const int col = wn * TN * 16 + j * 16 + (lane >> 4) * 4;
-      uint2 pk;
-      pk.x = dev::pack_bf16x2(acc[i][j][0], acc[i][j][1]);
-      pk.y = dev::pack_bf16x2(acc[i][j][2], acc[i][j][3]);
-      *reinterpret_cast<uint2*>(Cs + row * CST + col * 2) = pk;
-    }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  // persistent over tiles wg, wg + grid, ...: the grid is a multiple of ntiles, so a block keeps one
+  // channel tile nt and its statistics accumulate over its bands, reduced and written once
+  const int nt = wg % ntiles;
   constexpr int CPR = BN / 8;
   static_assert(NT % CPR == 0, "readout mapping needs a fixed chunk column per thread");
   const int cc = tid % CPR;
   float st_n = 0.f, st_s[8], st_ss[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) st_s[e] = st_ss[e] = 0.f;
-  const u32x4 st_k = *reinterpret_cast<const u32x4*>(Cs + cc * 16);  // row 0 (always valid): the shift
-  const int64_t y0 = (int64_t)g0 * g.W;                              // the band's first output pixel
-#pragma unroll 4
-  for (int q = tid; q < BM * CPR; q += NT) {
-    const int row = q / CPR;
-    if (row < valid) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + (y0 + row) * N + n0c + cc * 8));
-      if (STATS) {
-        st_n += 1.f;
+  u32x4 st_k = u32x4{0u, 0u, 0u, 0u};  // the shift: row 0 (always valid) of the block's first band
+  const int prow = kperm(lane & 15);
+  const int n0c = nt * BN, pos = lane & 7, cbn = g.C >> 6, K9 = 9 * g.C, W2 = g.W + 2;
+  constexpr bool PERSIST = STATS && RING != 0;  // (the register-B configuration has no room for it)
+  int wt = wg;
+  do {
+    const int mt = wt / ntiles;
+    if (wt != wg) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // last band's C tile read
+    const int g0 = mt * g.R;                       // first output row of the band (flattened b·H + h)
+    const int b0 = g0 / g.H, h0 = g0 - b0 * g.H;
+    const int n0 = min(g.H - h0, g.R);             // rows of the first segment
+    const int rv = min(g.R, g.rows_total - g0);    // valid output rows of the band
+    const int valid = rv * g.W;
+    const int HP = (band_hrow(rv - 1, n0, g.H) + 3) * W2;  // halo pixels to stage
+
+    // this lane's MFMA A rows -> halo pixel of tap (0, 0) (rows past the band read a valid pixel)
+    int hb[TM], vb[TM];  // LDS row and virtual index (hswz) of the pixel's tap (0, 0) halo pixel
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const float d0 = __uint_as_float(v[h] << 16) - __uint_as_float(st_k[h] << 16);
-          const float d1 = __uint_as_float(v[h] & 0xffff0000u) - __uint_as_float(st_k[h] & 0xffff0000u);
-          st_s[2 * h] += d0;
-          st_s[2 * h + 1] += d1;
-          st_ss[2 * h] = fmaf(d0, d0, st_ss[2 * h]);
-          st_ss[2 * h + 1] = fmaf(d1, d1, st_ss[2 * h + 1]);
+    for (int i = 0; i < TM; ++i) {
+      const int m = min(wm * TM * 16 + i * 16 + prow, valid - 1);
+      const int lr = m / g.W, hr = band_hrow(lr, n0, g.H), col = m - lr * g.W;
+      hb[i] = hr * W2 + col;
+      vb[i] = hr * g.W + col;
+    }
+    int boff[BI];  // (32-bit offsets: host-checked tensors < 2^31 elements)
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const int row = (wid * BI + j) * 8 + (lane >> 3);
+      boff[j] = (n0c + row) * K9 + 8 * (pos ^ ((row >> 1) & 7));
+    }
+    auto issue_halo = [&](int cb) {
+      for (int k = wid; k * 8 < HP; k += NW) {  // per-wave counts differ: only count-free waits cover it
+        const int q = k * 8 + (lane >> 3), hr = q / W2, hc = q - hr * W2;
+        int b = b0, ih = h0 - 1 + hr;
+        if (hr >= n0 + 2) {  // a later image of the band
+          const int r2 = hr - (n0 + 2), kk = r2 / (g.H + 2);
+          b = b0 + 1 + kk;
+          ih = r2 - kk * (g.H + 2) - 1;
+        }
+        const int iw = hc - 1;
+        const bool ok = q < HP && b < g.B && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        const uint16_t* src =
+            ok ? X + (((b * g.H + ih) * g.W + iw) * g.C + cb * 64 + 8 * (pos ^ (((hr * g.W + hc) >> 1) & 7))) : zeros;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(halo + k * 1024), 16, 0, 0);
+      }
+    };
+    auto issue_w = [&](int cb, int t, int slot) {
+      uint8_t* Bs = ring + slot * BN * 128;
+      const int wk = t * g.C + cb * 64;
+#pragma unroll
+      for (int j = 0; j < BI; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(Wt + boff[j] + wk), (lds_ptr_t)(Bs + (wid * BI + j) * 1024), 16,
+                                         0, 0);
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if constexpr (RING == 0) {
+      // B in registers: each wave loads its own TN column tiles straight from global memory (the
+      // weights are L2-resident), per 32-deep half step, three half steps deep; taps need no barrier
+      // and no ring, only the halo goes through LDS (one barrier per 64-channel step)
+      bf16x8 breg[3][TN];
+      const uint16_t* wl = Wt + (int64_t)(n0c + wn * TN * 16 + (lane & 15)) * K9 + (lane >> 4) * 8;
+      auto load_b = [&](int cb, int u, bf16x8 (&dst)[TN]) {  // half step u = 2·tap + half
+        const uint16_t* p = wl + (u >> 1) * g.C + cb * 64 + (u & 1) * 32;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) dst[j] = *reinterpret_cast<const bf16x8*>(p + j * 16 * K9);
+      };
+      issue_halo(0);
+      load_b(0, 0, breg[0]);
+      load_b(0, 1, breg[1]);
+      for (int cb = 0; cb < cbn; ++cb) {
+        if (cb > 0) {
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave is done with the halo
+          issue_halo(cb);
+        }
+        const bool last = cb + 1 == cbn;
+        // opaque per step: keeps the compiler from hoisting all 18 x TM LDS addresses of the unrolled
+        // half steps out of the channel loop (they are loop-invariant; live, they spill)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(hb[i]), "+v"(vb[i]));
+#pragma unroll
+        for (int u = 0; u < 18; ++u) {
+          __builtin_amdgcn_sched_barrier(0);  // keep each half step's LDS reads in it (register pressure)
+          // half step u's B fragments (and at u = 0 the halo) must have landed; the loads issued after
+          // them (the next half step's B) may stay in flight
+          if (u == 0) {
+            if (cb == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TN) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_barrier" ::: "memory");  // every wave's halo DMA is visible
+          } else if (u == 17 && last) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          } else {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TN) : "memory");
+          }
+          if (u + 2 < 18) load_b(cb, u + 2, breg[(u + 2) % 3]);
+          else if (!last) load_b(cb + 1, u - 16, breg[(u + 2) % 3]);
+          const int t = u >> 1, h = u & 1, r = t / 3, sx = t - 3 * r;
+          const int toff = r * W2 + sx, tv = r * g.W + sx, ch = h * 4 + (lane >> 4);
+          bf16x8 a[TM];
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            a[i] = *reinterpret_cast<const bf16x8*>(halo + hswz(hb[i] + toff, vb[i] + tv, ch));
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(breg[u % 3][j], a[i], acc[i][j], 0, 0, 0);
+        }
+      }
+    } else {
+      for (int cb = 0; cb < cbn; ++cb) {
+        if (cb > 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // halo / ring reads done
+        issue_halo(cb);
+        issue_w(cb, 0, 0);
+        if (RING == 3) issue_w(cb, 1, 1);
+#pragma unroll 1
+        for (int t = 0; t < 9; ++t) {
+          // retire tap t's weights (at t = 0 also the halo issued before them); with three slots the
+          // next tap's weights may stay in flight
+          if (RING == 3 && t < 8) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BI) : "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (not unrolled: no cross-tap load hoisting)
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          if (t + RING - 1 < 9) issue_w(cb, t + RING - 1, (t + RING - 1) % RING);
+          const int r = t / 3, sx = t - 3 * r, toff = r * W2 + sx, tv = r * g.W + sx;
+          const uint8_t* Bs = ring + (t % RING) * BN * 128;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int ch = h * 4 + (lane >> 4);
+            bf16x8 a[TM], bb[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+            a[i] = *reinterpret_cast<const bf16x8*>(halo + hswz(hb[i] + toff, vb[i] + tv, ch));
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              bb[j] = *reinterpret_cast<const bf16x8*>(Bs + swzb(wn * TN * 16 + j * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j], a[i], acc[i][j], 0, 0, 0);
+          }
         }
       }
     }
-  }
+
+    // ---- epilogue: bf16 C tile through LDS, 16-B row stores of the valid pixels (+ statistics) ----
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    constexpr int CST = BN * 2 + 16;
+    uint8_t* Cs = smem;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wm * TM * 16 + i * 16 + prow;
+        const int col = wn * TN * 16 + j * 16 + (lane >> 4) * 4;
+        uint2 pk;
+        pk.x = dev::pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+        pk.y = dev::pack_bf16x2(acc[i][j][2], acc[i][j][3]);
+        *reinterpret_cast<uint2*>(Cs + row * CST + col * 2) = pk;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (STATS && wt == wg) st_k = *reinterpret_cast<const u32x4*>(Cs + cc * 16);
+    const int64_t y0 = (int64_t)g0 * g.W;                              // the band's first output pixel
+#pragma unroll 4
+    for (int q = tid; q < BM * CPR; q += NT) {
+      const int row = q / CPR;
+      if (row < valid) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + (y0 + row) * N + n0c + cc * 8));
+        if (STATS) {
+          st_n += 1.f;
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const float d0 = __uint_as_float(v[h] << 16) - __uint_as_float(st_k[h] << 16);
+            const float d1 = __uint_as_float(v[h] & 0xffff0000u) - __uint_as_float(st_k[h] & 0xffff0000u);
+            st_s[2 * h] += d0;
+            st_s[2 * h + 1] += d1;
+            st_ss[2 * h] = fmaf(d0, d0, st_ss[2 * h]);
+            st_ss[2 * h + 1] = fmaf(d1, d1, st_ss[2 * h + 1]);
+          }
+        }
+      }
+    }
+  } while (PERSIST && (wt += gridDim.x) < mtiles * ntiles);
   if (!STATS) return;
   // every thread shifted by the same row-0 values, so the shifted sums add: lanes sharing cc, then
   // the waves through LDS; one (count, mean, M2) per channel and tile, part[q][N][tiles]
@@ -313,10 +328,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv3x3_band_kernel(
       ts += red[(w * 2 + 0) * BN + c];
       tss += red[(w * 2 + 1) * BN + c];
     }
-    const float mean_s = ts / tn;
-    part[((int64_t)0 * N + n0c + c) * G + mt] = tn;
-    part[((int64_t)1 * N + n0c + c) * G + mt] = redk[c] + mean_s;
-    part[((int64_t)2 * N + n0c + c) * G + mt] = fmaxf(tss - ts * mean_s, 0.f);
+    const float mean_s = tn > 0.f ? ts / tn : 0.f;  // (a block without bands: count 0, M2 0)
+    const int grp = wg / ntiles;
+    part[((int64_t)0 * N + n0c + c) * G + grp] = tn;
+    part[((int64_t)1 * N + n0c + c) * G + grp] = redk[c] + mean_s;
+    part[((int64_t)2 * N + n0c + c) * G + grp] = fmaxf(tss - ts * mean_s, 0.f);
   }
 }
 
@@ -381,7 +397,22 @@ std::vector<at::Tensor> conv3x3_band(const at::Tensor& x, const at::Tensor& w, b
   segs = (int)std::min<int64_t>(segs, B);
   const int hrows = (((R + 2 * segs) * ((int)W + 2) + 31) / 32) * 32;
   auto y = at::empty({B, N, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  auto part = stats ? at::empty({3, N, mtiles}, x.options().dtype(at::kFloat)) : at::empty({0}, x.options().dtype(at::kFloat));
+  // persistent blocks (stats only): two per CU, a multiple of ntiles, each a fixed channel tile and
+  // one statistics group; without statistics one block per tile
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 256;
+  }();
+  static const bool persist = [] {
+    const char* e = std::getenv("XDDP_BAND_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  const int64_t groups =
+      stats && persist && cf.ring != 0 ? std::min<int64_t>(mtiles, std::max(1, 2 * cus / ntiles)) : mtiles;
+  const auto fopt = x.options().dtype(at::kFloat);
+  auto part = stats ? at::empty({3, N, groups}, fopt) : at::empty({0}, fopt);
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();
   const BandGeo g{(int)B, (int)H, (int)W, (int)C, R, (int)rows_total};
   auto go = [&](auto kern, int ring) {
@@ -389,10 +420,10 @@ std::vector<at::Tensor> conv3x3_band(const at::Tensor& x, const at::Tensor& w, b
                                         (stats ? 0 : 0));
     TORCH_CHECK(lds <= 160 * 1024, "conv3x3_band: LDS budget exceeded (", lds, " B)");
     ensure_dyn_lds((const void*)kern, lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(mtiles * ntiles)), dim3(256), lds, stream,
+    hipLaunchKernelGGL(kern, dim3((unsigned)(groups * ntiles)), dim3(256), lds, stream,
                        reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()), zeros, (int)N, g,
-                       stats ? part.data_ptr<float>() : nullptr, ntiles, hrows);
+                       stats ? part.data_ptr<float>() : nullptr, ntiles, (int)mtiles, hrows);
     XDDP_HIP_CHECK(hipGetLastError());
   };
 #define XDDP_BAND(TM_, WM_, TN_, WN_, RING_)                                      \
