@@ -411,6 +411,19 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
                                                               const float* __restrict__ ss_copy = nullptr) {
   __shared__ float red[4][16];
   const int cv = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // the per-channel parameters are loaded up front, under the partials' loads (not a second
+  // dependent memory round trip after the reduction: the launch is latency-bound)
+  const int c = cv * 8 + (tid & 7);
+  float inv = 0.f, g = 1.f, fm = 0.f, ssc = 0.f, ssh = 0.f;
+  if (tid < 8) {
+    inv = invstd[c];
+    if (weight) g = Elem<W, float>::ld(weight, c);
+    if (fold_mean) fm = fold_mean[c];
+    if (ss_copy) {
+      ssc = ss_copy[c];
+      ssh = ss_copy[C + c];
+    }
+  }
   float acc[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) acc[j] = 0.f;
@@ -435,9 +448,6 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   if (tid >= 8) return;
   const float sd = (red[0][2 * tid] + red[1][2 * tid]) + (red[2][2 * tid] + red[3][2 * tid]);
   const float sdx = (red[0][2 * tid + 1] + red[1][2 * tid + 1]) + (red[2][2 * tid + 1] + red[3][2 * tid + 1]);
-  const int c = cv * 8 + tid;
-  const float inv = invstd[c];
-  const float g = weight ? Elem<W, float>::ld(weight, c) : 1.f;
   if (dweight) Elem<W, float>::st(dweight, c, sdx * inv);
   if (dbias) Elem<W, float>::st(dbias, c, sd);
   const float invM = 1.f / (float)M;
@@ -445,11 +455,11 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   coef[C + c] = -g * inv * inv * inv * sdx * invM;     // k2
   coef[2 * C + c] = -g * inv * sd * invM;              // k3
   // fold_mean: dx = k1·g + k2·x + (k3 - k2·mean), the form a consumer GEMM prologue applies
-  if (fold_mean) coef[2 * C + c] -= coef[C + c] * fold_mean[c];
+  if (fold_mean) coef[2 * C + c] -= coef[C + c] * fm;
   // ss_copy: rows 3-4 carry the forward scale / shift (the consumer recomputes the ReLU mask)
   if (ss_copy) {
-    coef[3 * C + c] = ss_copy[c];
-    coef[4 * C + c] = ss_copy[C + c];
+    coef[3 * C + c] = ssc;
+    coef[4 * C + c] = ssh;
   }
 }
 

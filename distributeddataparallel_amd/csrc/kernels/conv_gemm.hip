@@ -579,6 +579,17 @@ __global__ __launch_bounds__(256) void bn_partial_finalize_kernel(
   const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float* pc = part + (int64_t)c * cs;
   const float K = pc[ks];  // group 0's mean (group 0 always holds rows)
+  // thread 0's per-channel parameters load up front, under the partials (latency-bound launch)
+  float gm = 1.f, bb = 0.f, rm = 0.f, rv = 0.f, mom = momentum;
+  if (tid == 0) {
+    if (weight) gm = dev::Elem<W, float>::ld(weight, c);
+    if (bias) bb = dev::Elem<W, float>::ld(bias, c);
+    if (running_mean) {
+      rm = dev::Elem<W, float>::ld(running_mean, c);
+      rv = dev::Elem<W, float>::ld(running_var, c);
+      if (cma && nbt) mom = 1.f / (float)(nbt[0] + 1);
+    }
+  }
   float n = 0.f, s1 = 0.f, s2 = 0.f;
 #pragma unroll 4
   for (int gi = tid; gi < groups; gi += 256) {
@@ -609,16 +620,12 @@ __global__ __launch_bounds__(256) void bn_partial_finalize_kernel(
   const float inv = rsqrtf(var + eps);
   mean_out[c] = mean;
   invstd_out[c] = inv;
-  const float gm = weight ? dev::Elem<W, float>::ld(weight, c) : 1.f;
-  const float bb = bias ? dev::Elem<W, float>::ld(bias, c) : 0.f;
   scale[c] = gm * inv;
   shift[c] = bb - mean * gm * inv;
   if (running_mean) {
-    float mom = momentum;
-    if (cma && nbt) mom = 1.f / (float)(nbt[0] + 1);
     const float unbiased = Mf > 1.f ? var * Mf / (Mf - 1.f) : var;
-    dev::Elem<W, float>::st(running_mean, c, (1.f - mom) * dev::Elem<W, float>::ld(running_mean, c) + mom * mean);
-    dev::Elem<W, float>::st(running_var, c, (1.f - mom) * dev::Elem<W, float>::ld(running_var, c) + mom * unbiased);
+    dev::Elem<W, float>::st(running_mean, c, (1.f - mom) * rm + mom * mean);
+    dev::Elem<W, float>::st(running_var, c, (1.f - mom) * rv + mom * unbiased);
   }
 }
 
