@@ -42,6 +42,8 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels/dev_utils.h"
 
@@ -451,14 +453,14 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_kernel(
 // one 16 x 16 tile of that item's dQ^T = K^T · dS^T on mfma_f32_16x16x32_bf16 over all 256 keys
 // (d = 16 (w & 3).., q = 16 (w >> 2)..): no cross-wave reduction, no atomics. Both LDS images are [row][256] bf16 with the 16-B chunk index XOR'd by
 // row & 15, so the 16 rows a b128 lane group reads sit in 16 distinct bank groups.
-template <int D, bool CAUSAL, int KW, bool FQ = false>
-__global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
+template <int D, bool CAUSAL, int KW, bool FQ = false, int NG_ = 8 / KW>
+__global__ __launch_bounds__(64 * KW * NG_, 8 / (KW * NG_)) void fa_bwd_dkdv_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq, int Sk, int Hq, int Hkv, Strides qs, Strides ks,
     Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale, int nsplit,
     float* __restrict__ wsk, float* __restrict__ wsv, uint16_t* __restrict__ dQo, Strides dqs) {
-  constexpr int NG = 8 / KW, BK = 32 * KW;          // groups; keys per workgroup
+  constexpr int NG = NG_, BK = 32 * KW;             // groups; keys per workgroup
   constexpr int KS = D / 16, NT = D / 32, QB = 32;  // query rows per work item
   constexpr int TILE = QB * D * 2;                  // bytes of one Q (or dO) tile
   constexpr int STAGE = 2 * TILE + 2 * QB * 4;      // Q, dO, lse, delta
@@ -467,7 +469,7 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
   // waves issue one each)
   constexpr int RPI = 512 / D, NIT = QB / RPI, NI = NIT >= KW ? NIT / KW : 1;
   constexpr int ACC = NT * 16 * 64;                 // floats of one wave's dK^T (or dV^T)
-  static_assert(KW >= 2 && KW * NG == 8 && NIT % NI == 0 && (NIT < KW || NI * KW == NIT), "wave split");
+  static_assert(KW >= 2 && 8 % (KW * NG) == 0 && NIT % NI == 0 && (NIT < KW || NI * KW == NIT), "wave split");
   static_assert((NG - 1) * KW * ACC * 4 <= VBLK + 2 * NG * STAGE, "group reduction must fit the LDS");
   static_assert(!FQ || (KW == 8 && D == 64 && !CAUSAL), "fused dQ: one 256-key block, D = 64, non-causal");
   constexpr int DSB = QB * BK * 2;                   // (FQ) one dS [QB][BK] bf16 buffer
@@ -485,7 +487,8 @@ __global__ __launch_bounds__(512) void fa_bwd_dkdv_kernel(
   const int k0 = kb * BK, kw = k0 + 32 * wq, krow = kw + (lane & 31);
   uint8_t* Vblk = smem;
   {  // V rows [k0, k0 + BK) -> LDS (rows past Sk read row Sk - 1; their P, dS are masked to 0)
-    constexpr int VI = BK / RPI / 8;
+    constexpr int VI = BK / RPI / (KW * NG);  // per wave
+    static_assert(VI * KW * NG * RPI == BK, "the V block must split evenly over the waves");
     const uint16_t* Vb = V + b * vs.b + hk * vs.h;
 #pragma unroll
     for (int i = 0; i < VI; ++i) {
@@ -842,7 +845,14 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
     const int nkb = (int)((Sk + 32 * kwv - 1) / (32 * kwv));
     // GQA head split for causal attention (balance, see the kernel)
     const int grp = (int)(Hq / Hkv);
-    int nsplit = causal ? grp : 1;
+    // D = 128: one 4-wave group per workgroup, two workgroups per CU (NG = 1; r5: the per-item
+    // barrier of a two-group workgroup kept both groups' softmax phases in step, 1,435 vs 1,345 us
+    // at Llama B2 S4096), and the GQA heads split in two (1,311 us: half the fp32 partial traffic
+    // of a four-way split; a one-way split leaves the causal 2x work spread, 1,611 us)
+    static const int split_env = [] { const char* e = std::getenv("XDDP_FA_SPLIT"); return e ? std::atoi(e) : 0; }();
+    static const int ng_env = [] { const char* e = std::getenv("XDDP_FA_DKDV_NG"); return e ? std::atoi(e) : 1; }();
+    const int ng = D == 128 && kwv == 4 && ng_env == 1 ? 1 : 8 / kwv;
+    int nsplit = causal ? (split_env > 0 ? split_env : (ng == 1 ? 2 : grp)) : 1;
     if (nsplit < 1 || grp % nsplit != 0) nsplit = 1;
     at::Tensor wsk, wsv;
     if (nsplit > 1) {
@@ -851,7 +861,7 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
     }
     const dim3 grid((unsigned)(B * Hkv * nsplit), (unsigned)nkb);
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, grid, dim3(512), 0, stream, reinterpret_cast<const uint16_t*>(q.data_ptr()),
+      hipLaunchKernelGGL(kern, grid, dim3(64 * kwv * ng), 0, stream, reinterpret_cast<const uint16_t*>(q.data_ptr()),
                          reinterpret_cast<const uint16_t*>(k.data_ptr()), reinterpret_cast<const uint16_t*>(v.data_ptr()),
                          reinterpret_cast<const uint16_t*>(dout.data_ptr()), lse.data_ptr<float>(),
                          delta.data_ptr<float>(), reinterpret_cast<uint16_t*>(dk.data_ptr()),
@@ -862,7 +872,9 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
                          strides_of(dq));
       XDDP_HIP_CHECK(hipGetLastError());
     };
-    if (D == 128) { if (causal) go(fa_bwd_dkdv_kernel<128, true, 4>); else go(fa_bwd_dkdv_kernel<128, false, 4>); }
+    if (D == 128 && ng == 1) {
+      if (causal) go(fa_bwd_dkdv_kernel<128, true, 4, false, 1>); else go(fa_bwd_dkdv_kernel<128, false, 4, false, 1>);
+    } else if (D == 128) { if (causal) go(fa_bwd_dkdv_kernel<128, true, 4>); else go(fa_bwd_dkdv_kernel<128, false, 4>); }
     else if (kwv == 8) go(fa_bwd_dkdv_kernel<64, false, 8, true>);
     else { if (causal) go(fa_bwd_dkdv_kernel<64, true, 4>); else go(fa_bwd_dkdv_kernel<64, false, 4>); }
     if (nsplit > 1) {  // the split-sum writes dense [B, Sk, Hkv, D]: strided outputs get a copy
