@@ -42,10 +42,9 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
-#include <cstdlib>
-
 #include "common.h"
 #include "kernels/dev_utils.h"
+#include "kernels/norm.h"
 
 namespace xddp {
 namespace kernels {
@@ -453,13 +452,18 @@ __global__ __launch_bounds__(64 * NW) void fa_bwd_dq_kernel(
 // one 16 x 16 tile of that item's dQ^T = K^T · dS^T on mfma_f32_16x16x32_bf16 over all 256 keys
 // (d = 16 (w & 3).., q = 16 (w >> 2)..): no cross-wave reduction, no atomics. Both LDS images are [row][256] bf16 with the 16-B chunk index XOR'd by
 // row & 15, so the 16 rows a b128 lane group reads sit in 16 distinct bank groups.
+// FQ with dbp: the packed qkv projection's bias gradient too ([B][3][H][D] partials, the host sums
+// the batches): Σ dQ from the dQ tiles, Σ dV from the dV^T accumulators after they are stored,
+// Σ dK = 0 exactly (Σ_k dS[q][k] = δ_q - δ_q) — the separate pass re-read all of dQKV (r5: 62.5 us
+// per ViT-L layer against +12 us here).
 template <int D, bool CAUSAL, int KW, bool FQ = false, int NG_ = 8 / KW>
 __global__ __launch_bounds__(64 * KW * NG_, 8 / (KW * NG_)) void fa_bwd_dkdv_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ delta,
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int Sq, int Sk, int Hq, int Hkv, Strides qs, Strides ks,
     Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale, int nsplit,
-    float* __restrict__ wsk, float* __restrict__ wsv, uint16_t* __restrict__ dQo, Strides dqs) {
+    float* __restrict__ wsk, float* __restrict__ wsv, uint16_t* __restrict__ dQo, Strides dqs,
+    float* __restrict__ dbp) {
   constexpr int NG = NG_, BK = 32 * KW;             // groups; keys per workgroup
   constexpr int KS = D / 16, NT = D / 32, QB = 32;  // query rows per work item
   constexpr int TILE = QB * D * 2;                  // bytes of one Q (or dO) tile
@@ -548,6 +552,10 @@ __global__ __launch_bounds__(64 * KW * NG_, 8 / (KW * NG_)) void fa_bwd_dkdv_ker
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(S + 2 * TILE + wq * QB * 4), 4, 0, 0);
     }
   };
+  // (FQ, dbp) the qkv bias gradient's partial of this (batch, head): Σ dQ from the dQ tiles, Σ dV
+  // from the dV^T accumulators at the end, Σ dK = 0 (Σ_k dS = 0: a per-query constant added to the
+  // logits changes nothing)
+  float qsum[4] = {0.f, 0.f, 0.f, 0.f};
   // (FQ) dQ of item itq from its dS buffer: wave w owns the 16 x 16 tile d = 16 (w & 3).., q = 16 (w >> 2)..
   auto dq_tile = [&](int itq, const uint8_t* dsb) {
     const int d0 = 16 * (w & 3), q0 = 16 * (w >> 2), r16 = lane & 15, kq = lane >> 4;
@@ -566,6 +574,8 @@ __global__ __launch_bounds__(64 * KW * NG_, 8 / (KW * NG_)) void fa_bwd_dkdv_ker
       o.x = dev::pack_bf16x2(aq[0] * scale, aq[1] * scale);
       o.y = dev::pack_bf16x2(aq[2] * scale, aq[3] * scale);
       *reinterpret_cast<uint2*>(dQo + b * dqs.b + h * dqs.h + (int64_t)qrow * dqs.s + d0 + 4 * kq) = o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qsum[j] += aq[j] * scale;
     }
   };
   if (G < total) issue(G, 0);
@@ -659,8 +669,9 @@ __global__ __launch_bounds__(64 * KW * NG_, 8 / (KW * NG_)) void fa_bwd_dkdv_ker
         }
     }
   }
-  if (G != 0 || krow >= Sk) return;
-  if (nsplit > 1) {  // fp32 partials [split][B][Sk][Hkv][D], summed (and dK scaled) later
+  const bool rows_out = G == 0 && krow < Sk;  // (FQ with dbp: every lane goes on to the sums below)
+  if (!rows_out && !(FQ && dbp)) return;
+  if (rows_out && nsplit > 1) {  // fp32 partials [split][B][Sk][Hkv][D], summed (and dK scaled) later
     const int64_t base = ((((int64_t)split * (gridDim.x / nsplit) + bhk) / Hkv * Sk + krow) * Hkv + hk) * D;
     float* pk = wsk + base;
     float* pv = wsv + base;
@@ -673,22 +684,75 @@ __global__ __launch_bounds__(64 * KW * NG_, 8 / (KW * NG_)) void fa_bwd_dkdv_ker
         *reinterpret_cast<float4*>(pv + 32 * n + 4 * g + 8 * q) =
             make_float4(adv[n][4 * q], adv[n][4 * q + 1], adv[n][4 * q + 2], adv[n][4 * q + 3]);
       }
-    return;
+  } else if (rows_out) {
+    uint16_t* ok = dK + b * dks.b + hk * dks.h + (int64_t)krow * dks.s;
+    uint16_t* ov = dV + b * dvs.b + hk * dvs.h + (int64_t)krow * dvs.s;
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint2 a, c;
+        a.x = dev::pack_bf16x2(adk[n][4 * q] * scale, adk[n][4 * q + 1] * scale);
+        a.y = dev::pack_bf16x2(adk[n][4 * q + 2] * scale, adk[n][4 * q + 3] * scale);
+        c.x = dev::pack_bf16x2(adv[n][4 * q], adv[n][4 * q + 1]);
+        c.y = dev::pack_bf16x2(adv[n][4 * q + 2], adv[n][4 * q + 3]);
+        *reinterpret_cast<uint2*>(ok + 32 * n + 4 * g + 8 * q) = a;
+        *reinterpret_cast<uint2*>(ov + 32 * n + 4 * g + 8 * q) = c;
+      }
   }
-  uint16_t* ok = dK + b * dks.b + hk * dks.h + (int64_t)krow * dks.s;
-  uint16_t* ov = dV + b * dvs.b + hk * dvs.h + (int64_t)krow * dvs.s;
+  if constexpr (FQ) {
+    if (dbp) {
+      static_assert(NT * 16 == 32, "the key-sum butterfly below is written for D = 64");
+      // Σ_keys dV: halving butterfly over lane bits 0..4, in place on the (stored) accumulators,
+      // value j = adv[j >> 4][j & 15]: each exchange trades half the live values, so lane l ends with
+      // the 32-lane total of value index l & 31 in adv[0][0] (31 shuffles; keys past Sk hold zeros)
 #pragma unroll
-  for (int n = 0; n < NT; ++n)
+      for (int st = 0, width = 16; st < 5; ++st, width >>= 1) {
+        const int o = 16 >> st;
+        const bool hi = lane & o;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint2 a, c;
-      a.x = dev::pack_bf16x2(adk[n][4 * q] * scale, adk[n][4 * q + 1] * scale);
-      a.y = dev::pack_bf16x2(adk[n][4 * q + 2] * scale, adk[n][4 * q + 3] * scale);
-      c.x = dev::pack_bf16x2(adv[n][4 * q], adv[n][4 * q + 1]);
-      c.y = dev::pack_bf16x2(adv[n][4 * q + 2], adv[n][4 * q + 3]);
-      *reinterpret_cast<uint2*>(ok + 32 * n + 4 * g + 8 * q) = a;
-      *reinterpret_cast<uint2*>(ov + 32 * n + 4 * g + 8 * q) = c;
+        for (int i = 0; i < width; ++i) {
+          const float lo_v = adv[i >> 4][i & 15], hi_v = adv[(i + width) >> 4][(i + width) & 15];
+          const float recv = __shfl_xor(hi ? lo_v : hi_v, o, 64);
+          adv[i >> 4][i & 15] = (hi ? hi_v : lo_v) + recv;
+        }
+      }
+      // Σ_queries dQ: the 16 lanes r16 = lane & 15 of a dQ column set; bits 3, 2 halve the 4 values
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool hi = lane & 8;
+        const float recv = __shfl_xor(hi ? qsum[i] : qsum[i + 2], 8, 64);
+        qsum[i] = (hi ? qsum[i + 2] : qsum[i]) + recv;
+      }
+      {
+        const bool hi = lane & 4;
+        const float recv = __shfl_xor(hi ? qsum[0] : qsum[1], 4, 64);
+        qsum[0] = (hi ? qsum[1] : qsum[0]) + recv;
+      }
+      qsum[0] += __shfl_xor(qsum[0], 2, 64);
+      qsum[0] += __shfl_xor(qsum[0], 1, 64);
+      float* rb = reinterpret_cast<float*>(smem);  // [8][D] per-wave dV sums, [2][D] dQ sums (LDS idle)
+      {
+        const int j = lane & 31, n = j >> 4, i = j & 15;
+        rb[w * D + 32 * n + 8 * (i >> 2) + 4 * g + (i & 3)] = adv[0][0];
+      }
+      // lane (kq = lane >> 4) holds dQ column 16 (w & 3) + 4 kq + 2·(bit 3) + (bit 2) of query half w >> 2
+      if ((lane & 3) == 0)
+        rb[(8 + (w >> 2)) * D + 16 * (w & 3) + 4 * (lane >> 4) + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1)] = qsum[0];
+      __syncthreads();
+      if (tid < 3 * D) {
+        const int t = tid / D, d = tid - t * D;
+        float sum = 0.f;
+        if (t == 0) {
+          sum = rb[8 * D + d] + rb[9 * D + d];
+        } else if (t == 2) {
+#pragma unroll
+          for (int ww = 0; ww < 8; ++ww) sum += rb[ww * D + d];
+        }
+        dbp[((int64_t)b * 3 + t) * Hq * D + (int64_t)hk * D + d] = sum;
+      }
     }
+  }
 }
 
 // dK = scale · sum_s wsk[s], dV = sum_s wsv[s] (fp32 head-split partials, [nsplit][B·Sk·Hkv·D]);
@@ -777,7 +841,8 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
                                             const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse,
                                             bool causal, double scale, const c10::optional<at::Tensor>& dq_out,
                                             const c10::optional<at::Tensor>& dk_out,
-                                            const c10::optional<at::Tensor>& dv_out) {
+                                            const c10::optional<at::Tensor>& dv_out,
+                                            const c10::optional<at::Tensor>& bias_like) {
   const int64_t D = q.size(3);
   TORCH_CHECK(D == 64 || D == 128, "flash_attn: head dim 64 or 128");
   check_bshd(q, "q", D);
@@ -860,6 +925,13 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
       wsv = at::empty({nsplit, B, Sk, Hkv, D}, q.options().dtype(at::kFloat));
     }
     const dim3 grid((unsigned)(B * Hkv * nsplit), (unsigned)nkb);
+    // bias_like (the fused-dQ path: one workgroup per (batch, head), non-causal, every key in it): the
+    // column sums of dQ, dK, dV ([3][Hq][D], the packed qkv projection's bias gradient) from the kernel
+    const bool want_db =
+        bias_like.has_value() && bias_like->defined() && fused_dq && Hq == Hkv && nsplit == 1 && nkb == 1;
+    if (want_db)
+      TORCH_CHECK(bias_like->numel() == 3 * Hq * D, "flash_attn backward: bias_like must hold 3·H·D elements");
+    at::Tensor dbp = want_db ? at::empty({B, 3 * Hq * D}, q.options().dtype(at::kFloat)) : at::Tensor();
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, grid, dim3(64 * kwv * ng), 0, stream, reinterpret_cast<const uint16_t*>(q.data_ptr()),
                          reinterpret_cast<const uint16_t*>(k.data_ptr()), reinterpret_cast<const uint16_t*>(v.data_ptr()),
@@ -869,7 +941,7 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
                          strides_of(k), strides_of(v), strides_of(dout), strides_of(dk), strides_of(dv), sl2, sc,
                          nsplit, nsplit > 1 ? wsk.data_ptr<float>() : nullptr,
                          nsplit > 1 ? wsv.data_ptr<float>() : nullptr, reinterpret_cast<uint16_t*>(dq.data_ptr()),
-                         strides_of(dq));
+                         strides_of(dq), dbp.defined() ? dbp.data_ptr<float>() : nullptr);
       XDDP_HIP_CHECK(hipGetLastError());
     };
     if (D == 128 && ng == 1) {
@@ -887,6 +959,14 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
       XDDP_HIP_CHECK(hipGetLastError());
       if (!dk.is_same(dkc)) dk.copy_(dkc);
       if (!dv.is_same(dvc)) dv.copy_(dvc);
+    }
+    if (bias_like.has_value()) {  // a 4th output: the bias gradient, or None (not covered: bias_grad)
+      at::Tensor db;
+      if (want_db) {
+        db = at::empty({3 * Hq * D}, bias_like->options());
+        colsum_partials(dbp, db);
+      }
+      return {dq, dk, dv, db};
     }
   }
   return {dq, dk, dv};

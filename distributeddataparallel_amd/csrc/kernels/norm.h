@@ -124,7 +124,8 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
                                             const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse,
                                             bool causal, double scale, const c10::optional<at::Tensor>& dq_out,
                                             const c10::optional<at::Tensor>& dk_out,
-                                            const c10::optional<at::Tensor>& dv_out);
+                                            const c10::optional<at::Tensor>& dv_out,
+                                            const c10::optional<at::Tensor>& bias_like);
 
 void bind_norm_kernels(pybind11::module_& m);
 

@@ -57,7 +57,7 @@ void bind_norm_kernels(py::module_& m) {
         py::arg("scale"));
   m.def("flash_attn_backward", &flash_attn_backward, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
         py::arg("o"), py::arg("lse"), py::arg("causal"), py::arg("scale"), py::arg("dq_out") = py::none(),
-        py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none());
+        py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none(), py::arg("bias_like") = py::none());
   m.def("rope", &rope, py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("backward") = false);
   m.def("swiglu_forward", &swiglu_forward, py::arg("a"), py::arg("b"));
   m.def("swiglu_backward", &swiglu_backward, py::arg("grad"), py::arg("a"), py::arg("b"));

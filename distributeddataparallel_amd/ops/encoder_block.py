@@ -111,9 +111,12 @@ class _EncoderBlockFn(torch.autograd.Function):
         dw_o = _dw(g1, o.view(-1, D), p_o)
         dqkv = torch.empty_like(qkv)
         d5, q5 = dqkv.view(B, S, 3, heads, dh), qkv.view(B, S, 3, heads, dh)
-        C.flash_attn_backward(do.view(B, S, heads, dh), q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, lse, False,
-                              ctx.scale, d5[:, :, 0], d5[:, :, 1], d5[:, :, 2])
-        db_qkv, _ = C.bias_grad(dqkv, None, b_qkv)
+        # (with bias_like, the one-block ViT kernel also returns Σ rows of dQ, dK, dV = the qkv bias
+        # gradient from its own accumulators; None where it does not apply)
+        db_qkv = C.flash_attn_backward(do.view(B, S, heads, dh), q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, lse,
+                                       False, ctx.scale, d5[:, :, 0], d5[:, :, 1], d5[:, :, 2], b_qkv)[3]
+        if db_qkv is None:
+            db_qkv, _ = C.bias_grad(dqkv, None, b_qkv)
         dy1 = torch.mm(dqkv, w_qkv)
         dw_qkv = _dw(dqkv.view(-1, 3 * D), y1, p_qkv)
         # LN1 + residual: dx = g1 + LN1ᵀ(dy1)

@@ -86,6 +86,35 @@ def test_flash_backward_into_packed_gradient():
     assert torch.equal(d[:, :, 0], dq) and torch.equal(d[:, :, 1], dk) and torch.equal(d[:, :, 2], dv)
 
 
+@pytest.mark.parametrize("bias_dtype", [torch.bfloat16, torch.float32])
+def test_flash_backward_qkv_bias_gradient(bias_dtype):
+    """The one-block kernel's qkv bias gradient ([3][H][D]) against float sums of the bf16 dQ, dK, dV
+    it wrote: Σ dQ from its dQ tiles, Σ dV as Σ dO (softmax rows sum to 1), Σ dK exactly 0 (Σ_k dS = 0;
+    the summed bf16 dK is rounding noise, small against |dK|); dQ, dK, dV themselves are unchanged."""
+    C = load()
+    torch.manual_seed(3)
+    B, S, H, Dh = 3, 197, 16, 64
+    qkv = torch.randn(B, S, 3, H, Dh, device="cuda").bfloat16()
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    o, lse = C.flash_attn_forward(q, k, v, False, Dh ** -0.5)
+    do = torch.randn(B, S, H, Dh, device="cuda").bfloat16()
+    d = torch.empty_like(qkv)
+    bias = torch.zeros(3 * H * Dh, device="cuda", dtype=bias_dtype)
+    res = C.flash_attn_backward(do, q, k, v, o, lse, False, Dh ** -0.5, d[:, :, 0], d[:, :, 1], d[:, :, 2], bias)
+    assert len(res) == 4 and res[3] is not None and res[3].dtype == bias_dtype and res[3].shape == (3 * H * Dh,)
+    ref = d.float().sum((0, 1))  # [3, H, Dh]
+    got = res[3].float().view(3, H, Dh)
+    for t in (0, 2):
+        assert ((got[t] - ref[t]).norm() / ref[t].norm()).item() < 1e-2, t
+    assert torch.count_nonzero(got[1]) == 0
+    assert ref[1].norm() < 1e-2 * d[:, :, 1].float().abs().sum((0, 1)).norm()
+    dq, dk, dv = C.flash_attn_backward(do, q, k, v, o, lse, False, Dh ** -0.5)
+    assert torch.equal(d[:, :, 0], dq) and torch.equal(d[:, :, 1], dk) and torch.equal(d[:, :, 2], dv)
+    # a path the fused sums do not cover (causal): the 4th output is None
+    res = C.flash_attn_backward(do, q, k, v, o, lse, True, Dh ** -0.5, None, None, None, bias)
+    assert len(res) == 4 and res[3] is None
+
+
 def _run(blk, x, gout, fused_env):
     old = os.environ.get("XDDP_FUSED_BLOCK")
     os.environ["XDDP_FUSED_BLOCK"] = fused_env
