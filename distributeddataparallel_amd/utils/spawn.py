@@ -44,9 +44,22 @@ class ProcessExitedException(ProcessException):
 
 
 def free_port() -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    return free_ports(1)[0]
+
+
+def free_ports(n: int) -> list:
+    """n distinct free loopback ports: every socket stays bound until all are chosen (consecutive
+    single picks can return the same ephemeral port, and two stores then collide on it)."""
+    socks = []
+    try:
+        for _ in range(n):
+            s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            socks.append(s)
+            s.bind(("127.0.0.1", 0))
+        return [s.getsockname()[1] for s in socks]
+    finally:
+        for s in socks:
+            s.close()
 
 
 def _set_pdeathsig():

@@ -24,8 +24,9 @@ def _entry(rank, fn, world, backend, args):
 
 
 def run_ranks(fn, world=2, backend="cpu", args=(), env=None):
-    from distributeddataparallel_amd.utils.spawn import free_port, spawn
+    from distributeddataparallel_amd.utils.spawn import free_ports, spawn
 
-    env = {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port()), "OMP_NUM_THREADS": "1",
-           "XDDP_TEST_TORCH_PORT": str(free_port()), **(env or {})}
+    p_store, p_torch = free_ports(2)  # distinct: the xddp and torch stores each bind one
+    env = {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(p_store), "OMP_NUM_THREADS": "1",
+           "XDDP_TEST_TORCH_PORT": str(p_torch), **(env or {})}
     spawn(_entry, args=(fn, world, backend, args), nprocs=world, env=env)

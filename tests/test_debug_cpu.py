@@ -152,8 +152,8 @@ def _reinit_worker(rank, world, port):
 def test_reinit_over_persistent_store():
     """init / destroy three times over ONE store: each generation's keys (communicator bootstrap,
     init barrier) are its own, so no stale address or already-'done' barrier is read."""
-    from distributeddataparallel_amd.utils.spawn import free_port, spawn
+    from distributeddataparallel_amd.utils.spawn import free_ports, spawn
 
-    port = free_port()
+    port, master = free_ports(2)  # distinct: two stores bind them
     spawn(_reinit_worker, args=(2, port), nprocs=2,
-          env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(free_port()), "OMP_NUM_THREADS": "1"})
+          env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(master), "OMP_NUM_THREADS": "1"})
