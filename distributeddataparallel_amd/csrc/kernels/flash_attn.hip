@@ -912,12 +912,33 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
     const int grp = (int)(Hq / Hkv);
     // D = 128: one 4-wave group per workgroup, two workgroups per CU (NG = 1; r5: the per-item
     // barrier of a two-group workgroup kept both groups' softmax phases in step, 1,435 vs 1,345 us
-    // at Llama B2 S4096), and the GQA heads split in two (1,311 us: half the fp32 partial traffic
-    // of a four-way split; a one-way split leaves the causal 2x work spread, 1,611 us)
+    // at Llama B2 S4096). Causal: the smallest GQA head split that still gives two rounds of
+    // workgroups (heavy key blocks first, so the second round evens out the causal 2x work spread)
+    // — fewer fp32 partials to write and sum: B2 splits in two (1,311 vs 1,345 us four-way; one-way,
+    // a single round: 1,611), B1 (the Llama bench) in four (18,190 / 18,229 tok/s vs 17,629 /
+    // 17,658 two-way)
     static const int split_env = [] { const char* e = std::getenv("XDDP_FA_SPLIT"); return e ? std::atoi(e) : 0; }();
     static const int ng_env = [] { const char* e = std::getenv("XDDP_FA_DKDV_NG"); return e ? std::atoi(e) : 1; }();
+    static const int cus = [] {
+      int dev = 0, v = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+      return v > 0 ? v : 256;
+    }();
     const int ng = D == 128 && kwv == 4 && ng_env == 1 ? 1 : 8 / kwv;
-    int nsplit = causal ? (split_env > 0 ? split_env : (ng == 1 ? 2 : grp)) : 1;
+    int nsplit = 1;
+    if (causal && split_env > 0) {
+      nsplit = split_env;
+    } else if (causal && ng == 1) {
+      nsplit = grp;
+      for (int sp = 1; sp < grp; sp *= 2)
+        if (grp % sp == 0 && B * Hkv * sp * nkb >= 4LL * cus) {
+          nsplit = sp;
+          break;
+        }
+    } else if (causal) {
+      nsplit = grp;
+    }
     if (nsplit < 1 || grp % nsplit != 0) nsplit = 1;
     at::Tensor wsk, wsv;
     if (nsplit > 1) {
