@@ -35,7 +35,6 @@
 // shifted sums stay in registers across bands: the cross-lane reduction and partial writes run
 // once per block instead of once per band (r5: 3584 -> 512 groups, C64 forward 108 -> 100 us).
 #include <c10/hip/HIPStream.h>
-#include <cstdlib>
 #include <torch/extension.h>
 
 #include "common.h"
@@ -405,12 +404,8 @@ std::vector<at::Tensor> conv3x3_band(const at::Tensor& x, const at::Tensor& w, b
     (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
     return v > 0 ? v : 256;
   }();
-  static const bool persist = [] {
-    const char* e = std::getenv("XDDP_BAND_PERSIST");
-    return !(e && e[0] == '0');
-  }();
   const int64_t groups =
-      stats && persist && cf.ring != 0 ? std::min<int64_t>(mtiles, std::max(1, 2 * cus / ntiles)) : mtiles;
+      stats && cf.ring != 0 ? std::min<int64_t>(mtiles, std::max(1, 2 * cus / ntiles)) : mtiles;
   const auto fopt = x.options().dtype(at::kFloat);
   auto part = stats ? at::empty({3, N, groups}, fopt) : at::empty({0}, fopt);
   auto stream = c10::hip::getCurrentHIPStream(x.device().index()).stream();

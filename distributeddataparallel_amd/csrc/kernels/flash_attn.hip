@@ -26,9 +26,9 @@
 // * softmax in the exp2 domain (scale·log2 e folded in, v_exp_f32), LSE = m + log2(l) saved.
 //
 // Backward: preprocess delta = rowsum(dO·O); dK/dV kernel (one workgroup = 128 keys of one
-// (batch, kv head), two 4-wave groups splitting the (query head, 32-row query tile) items of the
-// GQA group and causal mask, LDS-DMA double-buffered Q / dO tiles; S = Q·K^T and dP = dO·V^T
-// with the KEY on the lane, so P and dS are directly the B operands of dV^T += dO^T·P and
+// (batch, kv head) and a share of the GQA group's query heads; D = 128: one 4-wave group, two
+// workgroups per CU; D = 64: two 4-wave groups splitting the (query head, 32-row query tile)
+// items), LDS-DMA double-buffered Q / dO tiles; S = Q·K^T and dP = dO·V^T with the KEY on the lane, so P and dS are directly the B operands of dV^T += dO^T·P and
 // dK^T += Q^T·dS); dQ kernel (8 waves x 32 query rows; S^T and dP^T with the query on the lane,
 // dQ^T += K^T·dS^T). No atomics: dQ and dK/dV are separate passes (S and dP are recomputed in
 // both), each bitwise reproducible — except when one workgroup holds every key of a head (D = 64,
@@ -917,19 +917,15 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
     // — fewer fp32 partials to write and sum: B2 splits in two (1,311 vs 1,345 us four-way; one-way,
     // a single round: 1,611), B1 (the Llama bench) in four (18,190 / 18,229 tok/s vs 17,629 /
     // 17,658 two-way)
-    static const int split_env = [] { const char* e = std::getenv("XDDP_FA_SPLIT"); return e ? std::atoi(e) : 0; }();
-    static const int ng_env = [] { const char* e = std::getenv("XDDP_FA_DKDV_NG"); return e ? std::atoi(e) : 1; }();
     static const int cus = [] {
       int dev = 0, v = 0;
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
       return v > 0 ? v : 256;
     }();
-    const int ng = D == 128 && kwv == 4 && ng_env == 1 ? 1 : 8 / kwv;
+    const int ng = D == 128 && kwv == 4 ? 1 : 8 / kwv;
     int nsplit = 1;
-    if (causal && split_env > 0) {
-      nsplit = split_env;
-    } else if (causal && ng == 1) {
+    if (causal && ng == 1) {
       nsplit = grp;
       for (int sp = 1; sp < grp; sp *= 2)
         if (grp % sp == 0 && B * Hkv * sp * nkb >= 4LL * cus) {
@@ -965,9 +961,9 @@ std::vector<at::Tensor> flash_attn_backward(const at::Tensor& dout, const at::Te
                          strides_of(dq), dbp.defined() ? dbp.data_ptr<float>() : nullptr);
       XDDP_HIP_CHECK(hipGetLastError());
     };
-    if (D == 128 && ng == 1) {
+    if (D == 128) {
       if (causal) go(fa_bwd_dkdv_kernel<128, true, 4, false, 1>); else go(fa_bwd_dkdv_kernel<128, false, 4, false, 1>);
-    } else if (D == 128) { if (causal) go(fa_bwd_dkdv_kernel<128, true, 4>); else go(fa_bwd_dkdv_kernel<128, false, 4>); }
+    }
     else if (kwv == 8) go(fa_bwd_dkdv_kernel<64, false, 8, true>);
     else { if (causal) go(fa_bwd_dkdv_kernel<64, true, 4>); else go(fa_bwd_dkdv_kernel<64, false, 4>); }
     if (nsplit > 1) {  // the split-sum writes dense [B, Sk, Hkv, D]: strided outputs get a copy
