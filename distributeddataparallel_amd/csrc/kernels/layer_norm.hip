@@ -21,6 +21,7 @@ namespace kernels {
 using dev::bf16_t;
 using dev::Elem;
 using dev::f16_t;
+using dev::u32x4;
 using dev::Vec8;
 
 namespace {
@@ -150,12 +151,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
         }
       }
     };
-    int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w;
-    float a[NV][8], d[NV][8], rv[NR][8], mean = 0.f, rstd = 0.f;
-    if (row < rows) load_row(row, a, d, rv, mean, rstd);
-    for (; row < rows; row += step) {
-      float na[NV][8], nd[NV][8], nr[NR][8], nmean = 0.f, nrstd = 0.f;
-      if (row + step < rows) load_row(row + step, na, nd, nr, nmean, nrstd);
+    // both passes of one row from registers: dx (+ res), the column partials
+    auto row_math = [&](int64_t row, const float (&a)[NV][8], const float (&d)[NV][8], const float (&rv)[NR][8],
+                        float mean, float rstd) {
       // pass 1: row reductions
       float s1 = 0.f, s2 = 0.f;
   #pragma unroll
@@ -176,8 +174,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
       for (int k = 0; k < NV; ++k) {
         const int c = (k * 64 + lane) * 8;
         if (c < D) {
-          float o[8];
-          if (RES && !RPF) Vec8<T>::ld(res + row * D + c, rv[0]);
+          float o[8], r1[8];
+          if (RES && !RPF) Vec8<T>::ld(res + row * D + c, r1);
   #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float xh = (a[k][j] - mean) * rstd;
@@ -188,9 +186,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
           if (RES) {
   #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              o[j] += rv[RPF ? k : 0][j];
+              const float rj = RPF ? rv[RPF ? k : 0][j] : r1[j];
+              o[j] += rj;
               if (SUMS) {
-                sr[SUMS ? k : 0][j] += rv[RPF ? k : 0][j];
+                sr[SUMS ? k : 0][j] += rj;
                 so[SUMS ? k : 0][j] += o[j];
               }
             }
@@ -198,16 +197,82 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
           Vec8<T>::st(dx + row * D + c, o);
         }
       }
+    };
+    int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w;
+    if constexpr (__is_same(T, bf16_t) && RPF) {
+      // bf16 residual form (ViT-L/16 rows): rows in flight as packed bf16, three slots rotating, so
+      // two rows' loads (12 KB per wave) are outstanding while one is reduced and written — one
+      // row of unpacked floats in flight left ~12 MB in flight chip-wide, short of the HBM latency
+      // x bandwidth product. Row indices clamp to the last row (the look-ahead past the end re-reads
+      // it), so the loads stay branch-free and the compiler's counted waits retire one slot at a time.
+      struct Slot {
+        u32x4 a[NV], d[NV], r[NV];
+        float mu, rs;
+      };
+      auto ld_slot = [&](int64_t r, Slot& sl) {
+        r = r < rows ? r : rows - 1;
+        sl.mu = RMS ? 0.f : mean_in[r];
+        sl.rs = rstd_in[r];
   #pragma unroll
-      for (int k = 0; k < NV; ++k)
-  #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          a[k][j] = na[k][j];
-          d[k][j] = nd[k][j];
-          if (RPF) rv[RPF ? k : 0][j] = nr[RPF ? k : 0][j];
+        for (int k = 0; k < NV; ++k) {
+          const int c = (k * 64 + lane) * 8;
+          if (c < D) {
+            sl.a[k] = *reinterpret_cast<const u32x4*>(x + r * D + c);
+            sl.d[k] = *reinterpret_cast<const u32x4*>(dy + r * D + c);
+            sl.r[k] = *reinterpret_cast<const u32x4*>(res + r * D + c);
+          }
         }
-      mean = nmean;
-      rstd = nrstd;
+      };
+      auto run = [&](int64_t r, const Slot& sl) {
+        float a[NV][8], d[NV][8], rv[NR][8];
+  #pragma unroll
+        for (int k = 0; k < NV; ++k)
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            a[k][2 * j] = __uint_as_float(sl.a[k][j] << 16);
+            a[k][2 * j + 1] = __uint_as_float(sl.a[k][j] & 0xffff0000u);
+            d[k][2 * j] = __uint_as_float(sl.d[k][j] << 16);
+            d[k][2 * j + 1] = __uint_as_float(sl.d[k][j] & 0xffff0000u);
+            rv[RPF ? k : 0][2 * j] = __uint_as_float(sl.r[k][j] << 16);
+            rv[RPF ? k : 0][2 * j + 1] = __uint_as_float(sl.r[k][j] & 0xffff0000u);
+          }
+        row_math(r, a, d, rv, sl.mu, sl.rs);
+      };
+      if (row < rows) {
+        Slot s0, s1, s2;
+        ld_slot(row, s0);
+        ld_slot(row + step, s1);
+        for (;;) {
+          ld_slot(row + 2 * step, s2);
+          run(row, s0);
+          if ((row += step) >= rows) break;
+          ld_slot(row + 2 * step, s0);
+          run(row, s1);
+          if ((row += step) >= rows) break;
+          ld_slot(row + 2 * step, s1);
+          run(row, s2);
+          if ((row += step) >= rows) break;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else {
+      float a[NV][8], d[NV][8], rv[NR][8], mean = 0.f, rstd = 0.f;
+      if (row < rows) load_row(row, a, d, rv, mean, rstd);
+      for (; row < rows; row += step) {
+        float na[NV][8], nd[NV][8], nr[NR][8], nmean = 0.f, nrstd = 0.f;
+        if (row + step < rows) load_row(row + step, na, nd, nr, nmean, nrstd);
+        row_math(row, a, d, rv, mean, rstd);
+  #pragma unroll
+        for (int k = 0; k < NV; ++k)
+  #pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            a[k][j] = na[k][j];
+            d[k][j] = nd[k][j];
+            if (RPF) rv[RPF ? k : 0][j] = nr[RPF ? k : 0][j];
+          }
+        mean = nmean;
+        rstd = nrstd;
+      }
     }
   } else {  // wide rows (D > 1024): the register-lean one-row-at-a-time loop (no spills)
     for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w; row < rows; row += (int64_t)gridDim.x * kRowsPerBlock) {
