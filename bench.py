@@ -40,8 +40,10 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
+FP32_DENSE_PEAK_TFLOPS = 157.3  # MI355X dense fp32 MFMA peak
 LR_WARMUP_STEPS = 30  # linear lr warmup (optimizer steps)
 LOSS_GUARD = 1.1  # warn when the final loss ends above 1.1x the first step's
+REPLICA_DIVERGED = 3  # exit code of a run whose ranks' parameters differ after the timed steps
 
 
 def parse(argv=None):
@@ -95,8 +97,22 @@ def parse(argv=None):
     ap.add_argument("--force-rccl-launch", type=int, default=0,
                     help="issue real RCCL kernels even at N=1 (XDDP_RCCL_FORCE_LAUNCH): the comm-stream "
                          "schedule becomes visible in a one-GPU kernel trace")
+    ap.add_argument("--dtype", choices=["auto", "bf16", "fp32"], default="auto",
+                    help="parameter / activation dtype (auto: bf16 on the GPU, fp32 on the CPU)")
+    ap.add_argument("--optimizer", choices=["auto", "sgd", "adamw"], default="auto",
+                    help="auto: SGD for the conv / MLP configs, AdamW for the transformers")
+    ap.add_argument("--lr", type=float, default=None, help="default 0.1 (SGD) / 1e-4 (AdamW)")
+    ap.add_argument("--momentum", type=float, default=0.9, help="SGD momentum")
+    ap.add_argument("--weight-decay", type=float, default=None, help="default 1e-4 (SGD) / 0.1 (AdamW)")
+    ap.add_argument("--lr-warmup", type=int, default=None,
+                    help=f"linear lr warmup steps (default {30}; 0 = constant lr)")
+    ap.add_argument("--recipe", choices=["default", "reference"], default="default",
+                    help="reference = the reference script's own recipe (ref:dpp.py:38-41): fp32, plain "
+                         "SGD(lr=0.01) without momentum / weight decay / master copy / warmup")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
+    if a.recipe == "reference":
+        a.dtype, a.optimizer, a.lr, a.momentum, a.weight_decay, a.lr_warmup = "fp32", "sgd", 0.01, 0.0, 0.0, 0
     if a.batch_size is None:
         # LM configs: one 4096-token sequence per rank (Llama-3-8B pure DDP sizing on 288 GB)
         a.batch_size = 1 if a.model.startswith("llama") else {"mlp": 64, "simplecnn": 32}.get(a.model, 256)
@@ -150,11 +166,15 @@ def self_launch(args, argv) -> int:
     failed = None
     while True:
         codes = [p.poll() for p in procs]
-        bad = [(i, c) for i, c in enumerate(codes) if c not in (None, 0)]
+        # 3 = the rank finished but the replicas diverged: every rank exits that way after the same
+        # collectives, so keep waiting for the others (rank 0 prints the JSON line) instead of killing
+        bad = [(i, c) for i, c in enumerate(codes) if c not in (None, 0, REPLICA_DIVERGED)]
         if bad:
             failed = bad[0]
             break
-        if all(c == 0 for c in codes):
+        if all(c is not None for c in codes):
+            diverged = [(i, c) for i, c in enumerate(codes) if c == REPLICA_DIVERGED]
+            failed = diverged[0] if diverged else None
             break
         if time.time() > deadline:
             failed = (-1, "timeout")
@@ -171,9 +191,12 @@ def self_launch(args, argv) -> int:
             except subprocess.TimeoutExpired:
                 p.kill()
                 p.wait()
-        print(f"[bench] rank {failed[0]} failed ({failed[1]}); all ranks stopped", file=sys.stderr, flush=True)
+        if failed[1] == REPLICA_DIVERGED:
+            print("[bench] the ranks' replicas diverged (exit 3; see replica_mismatch_ranks)", file=sys.stderr, flush=True)
+        else:
+            print(f"[bench] rank {failed[0]} failed ({failed[1]}); all ranks stopped", file=sys.stderr, flush=True)
     t.join(timeout=10)
-    if failed is None and json_lines:
+    if json_lines:  # (also after a failure: a diverged-replica run still reports its line)
         print(json_lines[-1], flush=True)
     if failed is not None:
         return 1 if failed[1] == "timeout" else (failed[1] if isinstance(failed[1], int) and failed[1] > 0 else 1)
@@ -355,7 +378,16 @@ def main(argv=None):
         torch.backends.cudnn.benchmark = bool(int(os.environ.get("XDDP_CUDNN_BENCHMARK", "0")))
     else:
         device = torch.device("cpu")
-    dtype = torch.bfloat16 if gpu else torch.float32
+    if args.dtype == "auto":
+        args.dtype = "bf16" if gpu else "fp32"
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    if args.optimizer == "auto":
+        args.optimizer = "sgd" if (is_conv(args) or args.model == "mlp") else "adamw"
+    sgd = args.optimizer == "sgd"
+    lr = args.lr if args.lr is not None else (0.1 if sgd else 1e-4)
+    wd = args.weight_decay if args.weight_decay is not None else (1e-4 if sgd else 0.1)
+    master = gpu and dtype != torch.float32  # fp32 master weights only for low-precision params
+    warmup_steps = LR_WARMUP_STEPS if args.lr_warmup is None else args.lr_warmup
 
     def sync():
         if gpu:
@@ -393,15 +425,18 @@ def main(argv=None):
         ddp = xddp.DDP(model, device_ids=[dev_index] if gpu else None, bucket_cap_mb=args.bucket_cap_mb,
                        bucket_policy=args.bucket_policy, gradient_as_bucket_view=bool(args.grad_as_bucket_view),
                        comm_dtype=comm_dtype)
-        if conv or args.model == "mlp":
-            opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, master_weights=gpu)
+        if sgd:
+            opt = FusedSGD(ddp.parameters(), lr=lr, momentum=args.momentum, weight_decay=wd, master_weights=master)
         else:
-            opt = FusedAdamW(ddp.parameters(), lr=1e-4, weight_decay=0.1, master_weights=True)
+            opt = FusedAdamW(ddp.parameters(), lr=lr, weight_decay=wd, master_weights=True)
     else:
         ddp = torch.nn.parallel.DistributedDataParallel(
             model, device_ids=[local_rank] if gpu else None, bucket_cap_mb=args.bucket_cap_mb or 25,
             gradient_as_bucket_view=bool(args.grad_as_bucket_view))
-        opt = torch.optim.SGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+        if sgd:
+            opt = torch.optim.SGD(ddp.parameters(), lr=lr, momentum=args.momentum, weight_decay=wd)
+        else:
+            opt = torch.optim.AdamW(ddp.parameters(), lr=lr, weight_decay=wd)
 
     B = args.batch_size
     micro = max(1, args.no_sync_accum)
@@ -456,7 +491,7 @@ def main(argv=None):
     n_opt_steps = [0]
 
     def set_lr():
-        f = min(1.0, (n_opt_steps[0] + 1) / LR_WARMUP_STEPS)
+        f = min(1.0, (n_opt_steps[0] + 1) / warmup_steps) if warmup_steps > 0 else 1.0
         for grp, lr in zip(opt.param_groups, base_lrs):
             grp["lr"] = lr * f
         n_opt_steps[0] += 1
@@ -508,9 +543,21 @@ def main(argv=None):
     loss_min, loss_max = float(lt.min()), float(lt.max())
     del traj
 
+    # ---------------- replica check (outside the timed region): every rank's parameters and
+    # buffers must be bit-identical after the timed steps (utils/replicas.py); a diverged run exits
+    # non-zero and names the ranks
+    replicas = None
+    if args.impl == "xddp":
+        if ddp.will_sync_module_buffers():
+            ddp._sync_buffers()  # BN running stats took local updates in the last forward
+        replicas = ddp.check_replicas(max_diff=world > 1)
+        if not replicas["replicas_identical"]:
+            print(f"[bench] rank {rank}: REPLICAS DIVERGED: ranks {replicas['mismatch_ranks']} disagree with the "
+                  f"majority (max |param - rank0 param| = {replicas['max_abs_diff']})", file=sys.stderr, flush=True)
+
     # ---------------- diagnostics (outside the timed region)
     diag = {}
-    if args.impl == "xddp":
+    if args.impl == "xddp" and replicas["replicas_identical"]:
         diag = diagnostics(args, ddp, step, sync, dist, device, world, overlap)
 
     ms = elapsed / args.steps * 1e3
@@ -560,8 +607,9 @@ def main(argv=None):
                 "impl": args.impl,
                 "backend": args.backend if args.impl == "xddp" else ("nccl" if gpu else "gloo"),
                 "norm": args.norm,
-                "optimizer": ("SGD(momentum=0.9, wd=1e-4)" + (" fp32 master weights" if gpu else "")
-                              if (conv or args.model == "mlp") else "AdamW(wd=0.1) fp32 master weights"),
+                "optimizer": (f"SGD(lr={lr:g}, momentum={args.momentum:g}, wd={wd:g})" if sgd
+                              else f"AdamW(lr={lr:g}, wd={wd:g})") + (" fp32 master weights" if master else ""),
+                "recipe": args.recipe,
                 "optimizer_schedule": args.overlap_schedule if overlap else "after backward",
                 "channels_last": bool(args.channels_last),
                 "comm_dtype": args.comm_dtype,
@@ -575,8 +623,11 @@ def main(argv=None):
             "final_loss": round(final_loss, 4),
             "loss_min": round(loss_min, 4),
             "loss_max": round(loss_max, 4),
-            "lr_warmup_steps": LR_WARMUP_STEPS if graphed is None else 0,
+            "lr_warmup_steps": warmup_steps if graphed is None else 0,
             "scaling_efficiency": eff,
+            "replicas_identical": None if replicas is None else replicas["replicas_identical"],
+            "replica_mismatch_ranks": None if replicas is None else replicas["mismatch_ranks"],
+            "replica_max_abs_diff": None if replicas is None else replicas["max_abs_diff"],
         }
         bad = [v for v in (final_loss, loss_max) if v != v or v in (float("inf"), float("-inf"))]
         if first_loss is not None and (bad or final_loss > LOSS_GUARD * first_loss):
@@ -587,7 +638,9 @@ def main(argv=None):
         if flops:
             tf = flops * per_step_samples / (ms * 1e-3) / 1e12
             out["model_tflops_per_gpu"] = round(tf / world, 1)
-            out["mfu"] = round(tf / world / BF16_DENSE_PEAK_TFLOPS, 4) if gpu else None
+            peak = BF16_DENSE_PEAK_TFLOPS if dtype == torch.bfloat16 else FP32_DENSE_PEAK_TFLOPS
+            out["mfu"] = round(tf / world / peak, 4) if gpu else None
+            out["mfu_peak_tflops"] = peak if gpu else None
         out.update(diag)
         line = json.dumps(out)
         print(line, flush=True)
@@ -595,6 +648,8 @@ def main(argv=None):
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     dist.destroy_process_group()  # (TunableOp writes its results file at process exit)
+    if replicas is not None and not replicas["replicas_identical"]:
+        return REPLICA_DIVERGED  # every rank: the run's parameters diverged (see the JSON line / stderr)
     return 0
 
 

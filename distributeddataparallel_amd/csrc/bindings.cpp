@@ -401,6 +401,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mt_l2norm", [](const std::vector<at::Tensor>& ts, at::Tensor out, double max_norm) {
         kernels::mt_l2norm(ts, out, max_norm, stream_of(out));
       }, py::arg("tensors"), py::arg("out"), py::arg("max_norm") = 0.0);
+  m.def("mt_checksum", [](const std::vector<at::Tensor>& ts) {
+        TORCH_CHECK(!ts.empty(), "mt_checksum: empty list");
+        return kernels::mt_checksum(ts, stream_of(ts[0]));
+      });
   m.def("mt_nonfinite", [](const std::vector<at::Tensor>& ts, at::Tensor out) {
         kernels::mt_nonfinite(ts, out, stream_of(out));
       });

@@ -36,6 +36,11 @@ void mt_l2norm(const std::vector<at::Tensor>& tensors, const at::Tensor& out, do
 // out[0] (int32) becomes 1 if any element of any tensor is NaN/Inf; 0 otherwise (zeroed here).
 void mt_nonfinite(const std::vector<at::Tensor>& tensors, const at::Tensor& out, hipStream_t stream);
 
+// Replica checksum of a list of dense device tensors (any dtypes): float64 [3] = (fp64 sum of the
+// values, low / high 32 bits of an XOR of per-element position-mixed raw-bit hashes). Bit-equal
+// inputs give bit-equal outputs (fixed-order merge); the DDP replica check compares it across ranks.
+at::Tensor mt_checksum(const std::vector<at::Tensor>& tensors, hipStream_t stream);
+
 // Fused SGD over a tensor list (torch.optim.SGD semantics).
 void fused_sgd_master(const std::vector<at::Tensor>& masters, const std::vector<at::Tensor>& grads,
                       const std::vector<at::Tensor>& momentum_bufs, const std::vector<at::Tensor>& model_params,

@@ -11,6 +11,7 @@
 #include <ATen/hip/HIPContext.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels/dev_utils.h"
@@ -378,6 +379,152 @@ void mt_nonfinite(const std::vector<at::Tensor>& tensors, const at::Tensor& out,
       XDDP_HIP_CHECK(hipGetLastError());
     });
   });
+}
+
+// ------------------------------------------------------------------------------------
+// replica checksum: fp64 sum of the values + XOR of a 64-bit mix of every element's raw bits with
+// its (tensor, index) position, over a list of tensors of any dtypes. Per-block partials are
+// written at fixed slots and merged by one block in a fixed order, so equal bytes on two ranks
+// give bit-equal checksums (the DDP replica check compares them across ranks).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {  // splitmix64 finalizer
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+template <typename T>
+__device__ __forceinline__ unsigned long long raw_bits(const T* x, int64_t k) {
+  if constexpr (sizeof(T) == 8) return reinterpret_cast<const unsigned long long*>(x)[k];
+  else if constexpr (sizeof(T) == 4) return reinterpret_cast<const uint32_t*>(x)[k];
+  else if constexpr (sizeof(T) == 2) return reinterpret_cast<const uint16_t*>(x)[k];
+  else return reinterpret_cast<const uint8_t*>(x)[k];
+}
+template <typename T>
+__device__ __forceinline__ double as_double(const T* x, int64_t k) {
+  if constexpr (std::is_same<T, bf16_t>::value || std::is_same<T, f16_t>::value) return (double)Elem<T, float>::ld(x, k);
+  else return (double)x[k];
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void checksum_kernel(SegTable<2> t, double* psum, unsigned long long* phash,
+                                                            int32_t off) {
+  __shared__ double ssum[kThreads / 64];
+  __shared__ unsigned long long shash[kThreads / 64];
+  const int s = find_seg(t, blockIdx.x);
+  const int64_t blk = blockIdx.x - (s ? t.blk_end[s - 1] : 0);
+  const T* x = reinterpret_cast<const T*>(t.ptr[0][s]);
+  const unsigned long long seed = mix64(reinterpret_cast<uintptr_t>(t.ptr[1][s]) + 0x9e3779b97f4a7c15ull);
+  const int64_t n = t.numel[s];
+  double acc = 0.0;
+  unsigned long long h = 0ull;
+  const int64_t end = std::min(n, (blk + 1) * kChunk);
+  for (int64_t k = blk * kChunk + threadIdx.x; k < end; k += kThreads) {
+    acc += as_double(x, k);
+    h ^= mix64(raw_bits(x, k) ^ mix64(seed + (unsigned long long)k));
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    acc += __shfl_xor(acc, o, 64);
+    h ^= __shfl_xor(h, o, 64);
+  }
+  if (lane == 0) {
+    ssum[wid] = acc;
+    shash[wid] = h;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0;
+    unsigned long long hh = 0ull;
+    for (int w = 0; w < kThreads / 64; ++w) {
+      a += ssum[w];
+      hh ^= shash[w];
+    }
+    psum[off + blockIdx.x] = a;
+    phash[off + blockIdx.x] = hh;
+  }
+}
+
+// one block, fixed order: out = [sum, hash low 32 bits, hash high 32 bits] as float64 (exact)
+__global__ __launch_bounds__(kThreads) void checksum_finalize_kernel(const double* psum, const unsigned long long* phash,
+                                                                     int64_t n, double* out) {
+  __shared__ double ssum[kThreads];
+  __shared__ unsigned long long shash[kThreads];
+  double a = 0.0;
+  unsigned long long h = 0ull;
+  for (int64_t i = threadIdx.x; i < n; i += kThreads) {
+    a += psum[i];
+    h ^= phash[i];
+  }
+  ssum[threadIdx.x] = a;
+  shash[threadIdx.x] = h;
+  __syncthreads();
+  for (int st = kThreads / 2; st > 0; st >>= 1) {
+    if (threadIdx.x < st) {
+      ssum[threadIdx.x] += ssum[threadIdx.x + st];
+      shash[threadIdx.x] ^= shash[threadIdx.x + st];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = ssum[0];
+    out[1] = (double)(shash[0] & 0xffffffffull);
+    out[2] = (double)(shash[0] >> 32);
+  }
+}
+
+at::Tensor mt_checksum(const std::vector<at::Tensor>& tensors, hipStream_t stream) {
+  TORCH_CHECK(!tensors.empty(), "checksum of an empty tensor list");
+  const auto dev = tensors[0].device();
+  auto out = at::zeros({3}, at::TensorOptions().dtype(at::kDouble).device(dev));
+  int64_t total_blocks = 0;
+  for (auto& x : tensors) {
+    TORCH_CHECK(x.device() == dev && x.is_non_overlapping_and_dense(), "checksum: dense tensors on one device");
+    total_blocks += (x.numel() + kChunk - 1) / kChunk;
+  }
+  auto psum = at::empty({std::max<int64_t>(total_blocks, 1)}, out.options());
+  auto phash = at::empty({std::max<int64_t>(total_blocks, 1)}, out.options().dtype(at::kLong));
+  int32_t off = 0;
+  // one table per dtype; the tensor's position in the list seeds its mix (order-sensitive)
+  std::vector<at::ScalarType> seen;
+  for (auto& x0 : tensors)
+    if (std::find(seen.begin(), seen.end(), x0.scalar_type()) == seen.end()) seen.push_back(x0.scalar_type());
+  for (auto st : seen) {
+    std::vector<std::array<void*, 2>> ptrs;
+    std::vector<int64_t> numels;
+    for (size_t i = 0; i < tensors.size(); ++i) {
+      if (tensors[i].scalar_type() != st) continue;
+      ptrs.push_back({const_cast<void*>(tensors[i].data_ptr()), reinterpret_cast<void*>((uintptr_t)(i + 1))});
+      numels.push_back(tensors[i].numel());
+    }
+    auto launch = [&](auto tag) {
+      using T = decltype(tag);
+      for_each_table<2>(ptrs, numels, [&](const SegTable<2>& t, int32_t nb) {
+        hipLaunchKernelGGL((checksum_kernel<T>), dim3(nb), dim3(kThreads), 0, stream, t, psum.data_ptr<double>(),
+                           reinterpret_cast<unsigned long long*>(phash.data_ptr<int64_t>()), off);
+        XDDP_HIP_CHECK(hipGetLastError());
+        off += nb;
+      });
+    };
+    switch (st) {
+      case at::kFloat: launch(float{}); break;
+      case at::kBFloat16: launch(bf16_t{}); break;
+      case at::kHalf: launch(f16_t{}); break;
+      case at::kDouble: launch(double{}); break;
+      case at::kLong: launch(int64_t{}); break;
+      case at::kInt: launch(int32_t{}); break;
+      case at::kShort: launch(int16_t{}); break;
+      case at::kByte: launch(uint8_t{}); break;
+      case at::kChar: launch(int8_t{}); break;
+      case at::kBool: launch(uint8_t{}); break;
+      default: TORCH_CHECK(false, "checksum: unsupported dtype ", st);
+    }
+  }
+  hipLaunchKernelGGL(checksum_finalize_kernel, dim3(1), dim3(kThreads), 0, stream, psum.data_ptr<double>(),
+                     reinterpret_cast<const unsigned long long*>(phash.data_ptr<int64_t>()), (int64_t)off,
+                     out.data_ptr<double>());
+  XDDP_HIP_CHECK(hipGetLastError());
+  return out;
 }
 
 // ------------------------------------------------------------------------------------

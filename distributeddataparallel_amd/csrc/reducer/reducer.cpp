@@ -152,9 +152,22 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t
     for (auto& e : gpu_ev_) XDDP_HIP_CHECK(hipEventCreate(&e));
   }
   cpu_ts_.assign(5, 0);
+  if (const char* f = std::getenv("XDDP_FAULT_CORRUPT")) {
+    std::string spec(f);
+    auto field = [&](const char* key) -> int64_t {
+      const std::string k = std::string(key) + "=";
+      const auto pos = spec.find(k);
+      return pos == std::string::npos ? -1 : std::atoll(spec.c_str() + pos + k.size());
+    };
+    fault_rank_ = static_cast<int>(field("rank"));
+    fault_iter_ = field("iter");
+  }
+  const char* c = std::getenv("XDDP_TSAN_CANARY");
+  tsan_canary_ = c && std::string(c) == "1";
 }
 
 Reducer::~Reducer() {
+  if (canary_thread_.joinable()) canary_thread_.join();
   remove_autograd_hooks();
   for (auto e : gpu_ev_) (void)hipEventDestroy(e);
 }
@@ -372,6 +385,7 @@ void Reducer::check_finalized() const {
 
 void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs) {
   std::lock_guard<std::mutex> g(mu_);
+  if (tsan_canary_) canary_count_ += 1;  // races the canary thread's write (never joined before here)
   if (require_finalize_) {
     std::ostringstream os;
     os << "Expected to have finished reduction in the prior iteration before starting a new one. "
@@ -446,6 +460,8 @@ void Reducer::search_unused_parameters(const std::vector<at::Tensor>& outputs) {
 void Reducer::autograd_hook(int64_t index) {
   std::lock_guard<std::mutex> g(mu_);
   if (!expect_hooks_) return;  // no_sync(), or a backward not prepared by the DDP forward
+  if (tsan_canary_ && !canary_thread_.joinable())
+    canary_thread_ = std::thread([this] { canary_count_ += 1; });  // hook-side write, no lock (canary)
   if (opts_.find_unused_parameters || opts_.static_graph) local_used_.data_ptr<int>()[index] = 1;
   const bool static_first = opts_.static_graph && !static_first_iter_done_;
   if (!has_rebuilt_ && (!opts_.find_unused_parameters || opts_.static_graph) &&
@@ -664,6 +680,13 @@ void Reducer::finalize_backward() {
       bk.work.reset();
     }
     if (result.defined() && !result.is_same(bk.comm)) bk.comm.view(-1).copy_(result.reshape(-1));
+  }
+  if (fault_rank_ >= 0 && comm_->rank() == fault_rank_ && num_iterations_ == fault_iter_) {
+    for (auto& bk : buckets_) {
+      if (bk.sparse || bk.skipped) continue;
+      bk.comm.view(-1).narrow(0, 0, 1).add_(1.0);  // injected post-all-reduce corruption (one rank)
+      break;
+    }
   }
   // sparse gradients: all-gather (indices, values), sum, scale (same divide rule as dense)
   for (auto& bk : buckets_) {

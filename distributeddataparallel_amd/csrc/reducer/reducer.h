@@ -24,6 +24,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <set>
 #include <string>
 #include <unordered_map>
@@ -222,6 +223,19 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<std::pair<int64_t, std::shared_ptr<Work>>> timed_works_;
   std::vector<double> bucket_comm_sum_;  // ns, per launch index
   void harvest_timings();
+
+  // fault injection (tests of the replica check): XDDP_FAULT_CORRUPT="rank=R,iter=I" adds 1 to the
+  // first element of the first dense bucket AFTER its all-reduce completed, on rank R in iteration I
+  // — a silent transport / ordering bug that leaves the loss falling and replicas diverging
+  int fault_rank_ = -1;
+  int64_t fault_iter_ = -1;
+  // XDDP_TSAN_CANARY=1 (ThreadSanitizer self-test, tests/test_sanitizers_cpu.py): a counter written
+  // by the hook side on another thread (as the autograd engine's device thread runs the hooks of
+  // GPU parameters) and by prepare_for_backward, with no lock in common — a real data race the TSan
+  // run must report, proving reports from the Reducer's hook path are not suppressed
+  bool tsan_canary_ = false;
+  int64_t canary_count_ = 0;
+  std::thread canary_thread_;
 };
 
 // Bucket assignment with the reference stack's semantics: group by

@@ -518,32 +518,42 @@ def _group_rank(pg: ProcessGroup, global_rank: int) -> int:
 # ---------------------------------------------------------------------------------------
 # functional collectives
 # ---------------------------------------------------------------------------------------
-_coalesce_pending: List[list] = []  # per open coalescing() block: blocking collectives issued inside
+_coalesce_pending: List[tuple] = []  # per open coalescing() block: (its group, blocking works issued inside)
 
 
-def _ret(work: Work, async_op: bool):
+def _ret(work: Work, async_op: bool, pg=None):
     if async_op:
         return work
-    if _coalesce_pending:
-        # inside coalescing() the collective is only launched when the outermost block closes
-        # (one RCCL group launch): the blocking call's wait happens there
-        _coalesce_pending[-1].append(work)
-        return None
+    for opg, works in reversed(_coalesce_pending):
+        if opg is pg:
+            # inside coalescing() on this group the collective is only launched when the outermost
+            # block closes (one RCCL group launch): the blocking call's wait happens there.
+            # Collectives on other groups are not part of that launch and wait as usual.
+            works.append(work)
+            return None
+    if pg is not None and pg.backend == "rccl" and any(opg.backend == "rccl" for opg, _ in _coalesce_pending):
+        # ncclGroupStart is per thread, not per communicator: this collective is held back until the
+        # open block closes too, but that block's launch does not track it, so it cannot be waited on
+        raise RuntimeError("a blocking collective on another RCCL group inside an open coalescing() block "
+                           "cannot complete before the block closes; issue it with async_op=True and wait "
+                           "after the block, or outside the block")
     work.wait()
     return None
 
 
 def all_reduce(tensor, op=ReduceOp.SUM, group=None, async_op=False):
-    return _ret(_resolve(group).allreduce(tensor, op), async_op)
+    pg = _resolve(group)
+    return _ret(pg.allreduce(tensor, op), async_op, pg)
 
 
 def broadcast(tensor, src=0, group=None, async_op=False):
     pg = _resolve(group)
-    return _ret(pg.broadcast(tensor, _group_rank(pg, src)), async_op)
+    return _ret(pg.broadcast(tensor, _group_rank(pg, src)), async_op, pg)
 
 
 def all_gather_into_tensor(output_tensor, input_tensor, group=None, async_op=False):
-    return _ret(_resolve(group).allgather_into_tensor(output_tensor, input_tensor), async_op)
+    pg = _resolve(group)
+    return _ret(pg.allgather_into_tensor(output_tensor, input_tensor), async_op, pg)
 
 
 def all_gather(tensor_list, tensor, group=None, async_op=False):
@@ -558,11 +568,12 @@ def all_gather(tensor_list, tensor, group=None, async_op=False):
     w = pg.allgather_into_tensor(flat, src)
     w._post = post
     w._outputs = tensor_list
-    return _ret(w, async_op)
+    return _ret(w, async_op, pg)
 
 
 def reduce_scatter_tensor(output, input, op=ReduceOp.SUM, group=None, async_op=False):
-    return _ret(_resolve(group).reduce_scatter_tensor(output, input, op), async_op)
+    pg = _resolve(group)
+    return _ret(pg.reduce_scatter_tensor(output, input, op), async_op, pg)
 
 
 def all_to_all_single(output, input, output_split_sizes=None, input_split_sizes=None, group=None, async_op=False):
@@ -574,7 +585,7 @@ def all_to_all_single(output, input, output_split_sizes=None, input_split_sizes=
     the imbalance, and the launch count stays at two collectives whatever W is."""
     pg = _resolve(group)
     if output_split_sizes is None and input_split_sizes is None:
-        return _ret(pg.alltoall_base(output, input), async_op)
+        return _ret(pg.alltoall_base(output, input), async_op, pg)
     W = pg.size()
     n_in, n_out = input.shape[0], output.shape[0]
     ins = list(input_split_sizes) if input_split_sizes is not None else [n_in // W] * W
@@ -597,7 +608,7 @@ def all_to_all_single(output, input, output_split_sizes=None, input_split_sizes=
 
     w._post = post
     w._outputs = [output]
-    return _ret(w, async_op)
+    return _ret(w, async_op, pg)
 
 
 def send(tensor, dst, group=None):
@@ -622,7 +633,8 @@ def irecv(tensor, src, group=None) -> Work:
 
 
 def barrier(group=None, async_op=False, device_ids=None):
-    return _ret(_resolve(group).barrier(), async_op)
+    pg = _resolve(group)
+    return _ret(pg.barrier(), async_op, pg)
 
 
 def monitored_barrier(group=None, timeout=None, wait_all_ranks=False):
@@ -659,16 +671,17 @@ def coalescing(group=None):
     ``async_op=True`` calls may only be waited on after that)."""
     pg = _resolve(group)
     pg.comm.group_start()
-    _coalesce_pending.append([])
+    _coalesce_pending.append((pg, []))
     ok = False
     try:
         yield
         ok = True
     finally:
-        works = _coalesce_pending.pop()
+        _, works = _coalesce_pending.pop()
         pg.comm.group_end()
-        if _coalesce_pending:
-            _coalesce_pending[-1].extend(works)
+        outer = next((w for opg, w in reversed(_coalesce_pending) if opg is pg), None)
+        if outer is not None:
+            outer.extend(works)
         elif ok:
             for w in works:
                 w.wait()

@@ -16,7 +16,8 @@ init (outside any timed region):
    makes every rank close its lanes and keep RCCL, and the reason is reported. On the ``peer``
    backend the base path is the one-shot lane itself, so a failed self-check raises on every rank
    (there is no path left to fall back to); lanes armed without probation
-   (``XDDP_PEER_ALLREDUCE=1/2``) are timed but not self-checked.
+   (``XDDP_PEER_ALLREDUCE=1/2``) get the same data self-check under their configured timeout, and a
+   wrong result raises on every rank (nothing to fall back to without ending the communicator).
 2. **Timings.** Each route is timed at each probe size (2 warm-up + ``iters`` back-to-back calls,
    host clock around a device sync, so the launch cost is part of alpha); the timing matrix is
    MAX-reduced, so every rank holds identical numbers.
@@ -215,17 +216,20 @@ def calibrate(pg, sizes: Sequence[int], dtype=torch.bfloat16, iters: int = 5) ->
     sizes = sorted({int(s) for s in sizes})
     # 1. self-check of the peer lanes, agreed by all ranks
     has_peer = bool(list(comm.routes()))
-    # Only lanes on probation can be self-checked safely: their failures are not communicator
-    # errors and closing them leaves a working base path. RCCL with XDDP_PEER_ALLREDUCE=1/2 arms the
-    # lanes at init (a self-check timeout would abort the communicator): the user chose them, they
-    # are timed but not self-checked. The peer backend has no other path: a failed self-check there
-    # is fatal (raised on every rank below).
+    # Lanes on probation are self-checked under a short timeout: their failures are not
+    # communicator errors and closing them leaves a working base path. RCCL with
+    # XDDP_PEER_ALLREDUCE=1/2 arms the lanes at init: they get the same data self-check under their
+    # configured (communicator) timeout — a short one would abort the communicator — and a wrong
+    # result is fatal on every rank (there is no probation to end, and a lane that maps but reduces
+    # wrongly must never carry a gradient). The peer backend has no other path: a failed self-check
+    # there is fatal as well (raised on every rank below).
     on_probation = pg.backend == "peer" or comm.info().get("peer_probation", "0") == "1"
+    armed = has_peer and not on_probation
     if has_peer and on_probation:
         comm.set_peer_timeout_ms(float(os.environ.get("XDDP_CALIBRATE_TIMEOUT_MS", "5000")))
         ok, reason = self_check(pg)
     elif has_peer:
-        ok, reason = True, "lanes armed by XDDP_PEER_ALLREDUCE (no probation): timed, not self-checked"
+        ok, reason = self_check(pg)
     else:
         ok, reason = False, "peer lanes not created (XDDP_PEER_ALLREDUCE unset or IPC mapping failed)"
     fail = torch.tensor([0 if ok else 1], dtype=torch.int32, device=pg.device)
@@ -234,6 +238,9 @@ def calibrate(pg, sizes: Sequence[int], dtype=torch.bfloat16, iters: int = 5) ->
     all_ok = has_peer and int(fail.item()) == 0
     if has_peer and ok and not all_ok:
         reason = "another rank's self-check failed"
+    if armed and not all_ok:
+        raise RuntimeError(f"xddp calibrate: the peer lanes armed by XDDP_PEER_ALLREDUCE failed their self-check "
+                           f"on rank {pg.rank()} ({reason}); unset XDDP_PEER_ALLREDUCE or use 'auto' (probation)")
     if pg.backend == "peer" and not (ok and all_ok):
         # the verdict all-reduce itself ran on the lane under test; with no fallback path the only
         # safe outcome is to stop every rank before a gradient is all-reduced on it

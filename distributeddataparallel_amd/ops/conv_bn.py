@@ -379,7 +379,6 @@ class _Conv3x3BNReLU(torch.autograd.Function):
     def forward(ctx, x, w, weight, bias, running_mean, running_var, nbt, momentum, cma, eps, stride, pend_out):
         C = load()
         ctx.set_materialize_grads(False)
-        _rot_mark(w)
         y, part = C.conv3x3_forward(x, w, stride, True)
         M = y.numel() // y.size(1)
         mean, invstd, ss = C.bn_stats_from_partials(part, M, weight, bias, running_mean, running_var, nbt, momentum,
@@ -466,6 +465,11 @@ def conv3x3_bn_relu(x: torch.Tensor, conv: nn.Conv2d, bn: nn.Module, pending: bo
     if not (_conv3x3() and conv.kernel_size == (3, 3) and conv_bn_supported(x, conv, bn)):
         return bn(conv(x), relu=True)
     pend = [] if (pending and _pending_apply()) else None
+    if torch.is_grad_enabled() and x.requires_grad:
+        # only a forward whose backward reads the rotated weight (the input gradient) marks it:
+        # no_grad forwards of other models (an EMA / teacher copy) would otherwise be rotated and
+        # pinned every step
+        _rot_mark(conv.weight)
     out = _Conv3x3BNReLU.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                bn.num_batches_tracked, float(bn.momentum), False, float(bn.eps), int(conv.stride[0]),
                                pend)

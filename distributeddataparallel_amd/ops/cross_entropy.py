@@ -9,6 +9,11 @@ kernel makes that row's loss NaN (so the step's loss shows it at once), gives it
 sets a per-device flag; the flag is copied to pinned host memory behind the kernel and read at
 the next call (or by :func:`check_targets`), which raises ``IndexError`` — no host sync per step.
 ``XDDP_XENT_CHECK=sync`` checks right after the forward instead (a sync per call).
+
+Under HIP-graph capture (``bench.py --graphs``, ``utils/graphs.py``) the host-side check, the flag
+copy and the event are skipped: an event query or record inside a capture is not allowed, and a
+replay could not run the host check anyway. The device flag is still set and the row's loss is
+still NaN, so a bad target shows in the replayed loss; the next eager call raises as usual.
 """
 from __future__ import annotations
 
@@ -53,13 +58,16 @@ class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target, ignore_index):
         C = load()
-        check_targets()  # an earlier call's invalid target surfaces here, without a sync
+        capturing = torch.cuda.is_current_stream_capturing()
+        if not capturing:
+            check_targets()  # an earlier call's invalid target surfaces here, without a sync
         flag, host, ev = _flag(logits.device)
         loss_rows, lse = C.cross_entropy_forward(logits, target, ignore_index, flag)
-        host.copy_(flag, non_blocking=True)
-        ev.record()
-        if os.environ.get("XDDP_XENT_CHECK") == "sync":
-            check_targets(block=True)
+        if not capturing:
+            host.copy_(flag, non_blocking=True)
+            ev.record(torch.cuda.current_stream(logits.device))
+            if os.environ.get("XDDP_XENT_CHECK") == "sync":
+                check_targets(block=True)
         count = (target != ignore_index).sum().clamp_min(1).to(torch.float32)
         ctx.save_for_backward(logits, target, lse, count)
         ctx.ignore_index = ignore_index

@@ -39,6 +39,7 @@ from .. import distributed as xdist
 from .._native import load
 from ..ops import linear as _linear_ops
 from ..utils import fault as _fault
+from ..utils import replicas as _replicas
 from . import bucket_policy as _bp
 from .join import Join, Joinable, JoinHook
 
@@ -244,6 +245,9 @@ class DistributedDataParallel(nn.Module, Joinable):
         self.require_forward_param_sync = True
         self.static_graph = False
         self._divide_by_initial_world_size = True
+        # XDDP_CHECK_REPLICAS=N: every N-th forward compares a checksum of every parameter (and of the
+        # synced buffers) across ranks and raises naming the diverged ranks (utils/replicas.py)
+        self._check_replicas_every = int(os.environ.get("XDDP_CHECK_REPLICAS", "0") or 0)
         self.mixed_precision = mixed_precision
         if mixed_precision is not None:
             self._setup_mixed_precision(module, mixed_precision)
@@ -581,10 +585,17 @@ class DistributedDataParallel(nn.Module, Joinable):
             # registration is claimed by one backward, so it is renewed every forward; the views
             # themselves only change when the buckets are rebuilt.
             if rebuilt or getattr(self, "_grad_target_views", None) is None:
+                _linear_ops.clear_grad_targets(self._module_parameters)  # views of the old layout
                 self._grad_target_views = self.reducer.param_bucket_views()
             _linear_ops.set_grad_targets(self._module_parameters, self._grad_target_views)
         if self._check_sync_bufs_pre_fwd():
             self._sync_buffers()
+        n = getattr(self, "_check_replicas_every", 0)
+        if n > 0 and self._forward_count % n == 0 and torch.is_grad_enabled():
+            rep = self.check_replicas(max_diff=False)
+            if not rep["replicas_identical"]:
+                raise RuntimeError(f"xddp DDP: model replicas diverged before forward {self._forward_count}: ranks "
+                                   f"{rep['mismatch_ranks']} disagree with the majority (XDDP_CHECK_REPLICAS)")
         if self._join_config.enable:
             # tell joined ranks whether this iteration's backward syncs (their shadow collectives)
             self._check_global_requires_backward_grad_sync(is_joined_rank=False)
@@ -592,6 +603,19 @@ class DistributedDataParallel(nn.Module, Joinable):
             inputs = _to_device(inputs, self.device_ids[0])
             kwargs = _to_device(kwargs, self.device_ids[0])
         return inputs, kwargs
+
+    def check_replicas(self, max_diff: bool = True) -> dict:
+        """Collective: compare every parameter (and, when buffers are broadcast every forward, every
+        buffer) across the ranks of this DDP's group by one native checksum pass per rank
+        (``utils/replicas.py``). Returns ``{"replicas_identical", "mismatch_ranks", "max_abs_diff",
+        "checksum"}``. Buffers take local updates inside a forward (BatchNorm running stats) and are
+        re-synced from rank 0 at the next one, so call this right after a buffer sync (as the
+        per-forward check does) or pass through :meth:`_sync_buffers` first."""
+        tensors = list(self._module_parameters)
+        if self.will_sync_module_buffers():
+            tensors += [b for b in self._buffers_list if b.numel() > 0]
+        with torch.no_grad():
+            return _replicas.check_replicas(tensors, self.process_group, max_diff=max_diff)
 
     def _check_global_requires_backward_grad_sync(self, is_joined_rank: bool):
         flag = not is_joined_rank and torch.is_grad_enabled() and self.require_backward_grad_sync
@@ -894,6 +918,8 @@ class DistributedDataParallel(nn.Module, Joinable):
 
     def _remove_autograd_hooks(self):
         self.reducer.remove_autograd_hooks()
+        _linear_ops.clear_grad_targets(self._module_parameters)  # no weight gradient into our buckets
+        self._grad_target_views = None
         for h in self._accum_grad_hooks:
             h.remove()
         self._accum_grad_hooks = []

@@ -29,6 +29,8 @@ from distributeddataparallel_amd.utils.checkpoint import load_checkpoint, save_c
 
 def train(rank, args):
     backend = args.backend or ("rccl" if torch.cuda.is_available() else "cpu")
+    if args.impl == "torch":  # the reference's own stack, for parity runs (torch DDP + torch BN, NCHW)
+        return train_torch(rank, args, backend)
     dist.init_process_group(backend)
     world = dist.get_world_size()
     torch.manual_seed(0)
@@ -65,7 +67,7 @@ def train(rank, args):
             loss = criterion(model(data), target)
             loss.backward()
             optimizer.step()
-            if batch_idx % 100 == 0 and dist.get_rank() == 0:
+            if batch_idx % args.log_every == 0 and dist.get_rank() == 0:
                 print(f"Epoch {epoch}, Batch {batch_idx}, Loss: {loss.item()}", flush=True)
             step += 1
             if args.max_steps and step >= args.max_steps:
@@ -73,6 +75,44 @@ def train(rank, args):
         if args.checkpoint:
             save_checkpoint(args.checkpoint, model, optimizer, step=epoch)
     dist.destroy_process_group()
+
+
+def train_torch(rank, args, backend):
+    """The same loop on torch.nn.parallel.DistributedDataParallel over torch.distributed (nccl =
+    RCCL on ROCm, or gloo), with torch's BatchNorm2d in NCHW: the reference script's stack."""
+    import torch.distributed as tdist
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29512")
+    gpu = backend != "cpu"
+    tdist.init_process_group("nccl" if gpu else "gloo", rank=int(os.environ.get("RANK", rank)),
+                             world_size=int(os.environ.get("WORLD_SIZE", 1)))
+    world = tdist.get_world_size()
+    torch.manual_seed(0)
+    dataset = CIFAR10Binary(args.data) if CIFAR10Binary.available(args.data) else SyntheticImages(
+        length=args.synthetic_len, shape=(3, 32, 32))
+    sampler = DistributedSampler(dataset, num_replicas=world, rank=tdist.get_rank(), shuffle=True)
+    loader = DataLoader(dataset, batch_size=args.batch_size, sampler=sampler, num_workers=args.workers)
+    device = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
+    model = torch.nn.parallel.DistributedDataParallel(SimpleCNN().to(device),
+                                                      device_ids=[device.index] if gpu else None)
+    criterion = nn.CrossEntropyLoss()
+    optimizer = torch.optim.SGD(model.parameters(), lr=args.lr)
+    step = 0
+    for epoch in range(args.epochs):
+        sampler.set_epoch(epoch)
+        for batch_idx, (data, target) in enumerate(loader):
+            data, target = data.to(device), target.to(device)
+            optimizer.zero_grad()
+            loss = criterion(model(data), target)
+            loss.backward()
+            optimizer.step()
+            if batch_idx % args.log_every == 0 and tdist.get_rank() == 0:
+                print(f"Epoch {epoch}, Batch {batch_idx}, Loss: {loss.item()}", flush=True)
+            step += 1
+            if args.max_steps and step >= args.max_steps:
+                break
+    tdist.destroy_process_group()
 
 
 def main():
@@ -88,6 +128,9 @@ def main():
     ap.add_argument("--max-steps", type=int, default=0)
     ap.add_argument("--checkpoint", default=None)
     ap.add_argument("--resume", default=None)
+    ap.add_argument("--log-every", type=int, default=100, help="rank-0 loss print interval (reference: 100)")
+    ap.add_argument("--impl", choices=["xddp", "torch"], default="xddp",
+                    help="torch = torch DDP + torch BatchNorm (the reference stack), for parity runs")
     args = ap.parse_args()
     if args.spawn:
         from distributeddataparallel_amd.utils.spawn import spawn

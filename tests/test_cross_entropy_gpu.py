@@ -59,3 +59,37 @@ def test_cross_entropy_out_of_range_target_raises():
     torch.cuda.synchronize()
     with pytest.raises(IndexError):
         cross_entropy(x, torch.zeros(8, dtype=torch.long, device="cuda"))  # raised lazily by the next call
+
+
+def test_cross_entropy_captures_in_hip_graph():
+    """The fused cross-entropy inside a HIP-graph capture (bench.py --graphs on an LM config): no
+    event query / record or host copy during capture, and replays reproduce the eager loss and
+    gradient for new data copied into the static inputs."""
+    torch.manual_seed(2)
+    rows, vocab = 32, 2048
+    x = (torch.randn(rows, vocab, device="cuda") * 2).to(torch.bfloat16).requires_grad_(True)
+    t = torch.randint(0, vocab, (rows,), device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm up outside the capture
+        for _ in range(2):
+            x.grad = None
+            cross_entropy(x, t).backward()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    x.grad = None
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        loss = cross_entropy(x, t)
+        loss.backward()
+    for seed in (3, 4):
+        torch.manual_seed(seed)
+        with torch.no_grad():
+            x.copy_((torch.randn(rows, vocab, device="cuda") * 2).to(torch.bfloat16))
+        t.copy_(torch.randint(0, vocab, (rows,), device="cuda"))
+        g.replay()
+        torch.cuda.synchronize()
+        b = x.detach().clone().requires_grad_(True)
+        ref = F.cross_entropy(b.float(), t)
+        ref.backward()
+        torch.testing.assert_close(loss, ref, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(x.grad.float(), b.grad.float(), rtol=2e-2, atol=1e-2 * b.grad.abs().max().item())

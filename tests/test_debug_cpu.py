@@ -157,3 +157,25 @@ def test_reinit_over_persistent_store():
     port, master = free_ports(2)  # distinct: two stores bind them
     spawn(_reinit_worker, args=(2, port), nprocs=2,
           env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(master), "OMP_NUM_THREADS": "1"})
+
+
+def _w_coalescing_other_group(rank, world):
+    """A blocking collective on another (CPU) group inside an open coalescing() block is not part of
+    that block's launch: it completes before returning, and an object collective reads its result."""
+    from distributeddataparallel_amd import distributed as d
+
+    other = d.new_group([0, 1])
+    a = torch.full((4,), float(rank + 1))
+    with d.coalescing():
+        d.all_reduce(a)  # deferred: waited when the block closes
+        b = torch.full((3,), float(rank + 10))
+        assert d.all_reduce(b, group=other) is None
+        assert torch.equal(b, torch.full((3,), 21.0)), b  # completed already
+        objs = [None, None]
+        d.all_gather_object(objs, {"r": rank}, group=other)
+        assert objs == [{"r": 0}, {"r": 1}], objs
+    assert torch.equal(a, torch.full((4,), 3.0))
+
+
+def test_coalescing_defers_only_its_own_group():
+    run_ranks(_w_coalescing_other_group, world=2)
