@@ -18,7 +18,13 @@ for spec in "$@"; do
   secs=${rest%%|*}
   cmd=${rest#*|}
   echo "== $name (limit ${secs}s): $cmd"
-  if [ "${cmd#prof }" != "$cmd" ]; then
+  if [ "${cmd#pmcpass }" != "$cmd" ]; then
+    # "pmcpass <counters>": one rocprofv3 counter pass over $PMC_PROG (default scripts/pmc_wgrad.py)
+    ctrs=${cmd#pmcpass }
+    # shellcheck disable=SC2086
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL "$secs" rocprofv3 --pmc $ctrs --kernel-trace -d "$ROOT/gpurun_out/$name" \
+      -o pmc --output-format csv -- python3 "$ROOT/${PMC_PROG:-scripts/pmc_wgrad.py}") > "$ROOT/gpurun_out/$name.log" 2>&1
+  elif [ "${cmd#prof }" != "$cmd" ]; then
     prog=${cmd#prof }
     prog=${prog//@R@/$ROOT}
     # shellcheck disable=SC2086

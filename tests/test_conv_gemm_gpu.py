@@ -59,6 +59,39 @@ def test_conv1x1_wgrad_matches_fp32(b, cin, h, w, cout, s, wdt):
     torch.testing.assert_close(dw.float(), ref, rtol=tol, atol=tol * ref.abs().max().item())
 
 
+@pytest.mark.parametrize("b,cin,h,w,cout,s,pro", [
+    (4, 256, 14, 14, 1024, 1, 0),   # layer-3 conv3 shape class, M = 784: 12.25 pixel steps per range
+    (2, 512, 7, 7, 2048, 1, 0),     # 64 tiles, one pixel step per slice
+    (3, 1024, 13, 13, 512, 2, 0),   # strided rows (downsample), odd input size
+    (5, 128, 11, 9, 256, 1, 2),     # BN-backward prologue, ragged tail (M = 495)
+    (3, 256, 13, 13, 128, 1, 3),    # prologue with the ReLU mask recomputed from Y2
+    (64, 128, 14, 14, 128, 1, 0),   # one tile over 256 slices (M = 12544, slab sum of 196)
+])
+def test_conv1x1_wgrad_deep_shapes_match_fp32(b, cin, h, w, cout, s, pro):
+    """The 128 x 128-tile weight gradient (layer 2-4 shape classes) against fp32 einsum, with the
+    BN-backward prologue dY = k1·G + k2·Y2 + k3 (masked by Y2·s + t > 0 for pro = 3) formed while
+    staging; ragged pixel tails and many slices; bitwise repeatable."""
+    torch.manual_seed(6)
+    x = _x(b, cin, h, w)
+    oh, ow = (h - 1) // s + 1, (w - 1) // s + 1
+    like = torch.empty(cout, cin, 1, 1, device="cuda", dtype=torch.bfloat16)
+    if pro:
+        g, y2 = _x(b, cout, oh, ow), _x(b, cout, oh, ow)
+        coef = torch.randn(5 if pro == 3 else 3, cout, device="cuda")
+        v = lambda i: coef[i].view(1, -1, 1, 1)  # noqa: E731
+        gm = torch.where(y2.float() * v(3) + v(4) > 0, g.float(), 0.0) if pro == 3 else g.float()
+        dyf = (v(0) * gm + v(1) * y2.float() + v(2)).to(torch.bfloat16).float()
+        dw = C.conv1x1_wgrad(g, x, 1, like, y2, coef)
+    else:
+        dy = _x(b, cout, oh, ow)
+        dyf = dy.float()
+        dw = C.conv1x1_wgrad(dy, x, s, like)
+    ref = torch.einsum("bnhw,bkhw->nk", dyf, x.float()[:, :, ::s, ::s]).view(cout, cin, 1, 1)
+    torch.testing.assert_close(dw.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+    again = C.conv1x1_wgrad(g, x, 1, like, y2, coef) if pro else C.conv1x1_wgrad(dy, x, s, like)
+    assert torch.equal(again, dw)  # fixed-order slab sum: bitwise deterministic
+
+
 @pytest.mark.parametrize("offset", [0.0, 300.0])
 def test_epilogue_stats_match_torch(offset):
     """Epilogue partials -> mean/var equal torch's over the stored bf16 output, also when
