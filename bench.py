@@ -109,6 +109,9 @@ def parse(argv=None):
     ap.add_argument("--recipe", choices=["default", "reference"], default="default",
                     help="reference = the reference script's own recipe (ref:dpp.py:38-41): fp32, plain "
                          "SGD(lr=0.01) without momentum / weight decay / master copy / warmup")
+    ap.add_argument("--accurate-convs", type=int, default=0,
+                    help="fp32: MIOpen's implicit-GEMM conv solvers off (fp32-accurate weight gradients, but the "
+                         "channels_last fallback runs ~6x slower; utils/precision.py)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     if a.recipe == "reference":
@@ -364,6 +367,11 @@ def main(argv=None):
         _install_miopen_tuning()
     tunableop = _install_tunableop(args)
     sys.path.insert(0, REPO)
+    if args.device == "cuda" and args.dtype == "fp32" and is_conv(args) and args.accurate_convs:
+        # fp32 runs take MIOpen's convolutions: optionally fp32-accurate ones (utils/precision.py), both impls
+        from distributeddataparallel_amd.utils.precision import accurate_fp32_convs
+
+        accurate_fp32_convs()
 
     import torch
     import torch.nn.functional as F
@@ -610,6 +618,7 @@ def main(argv=None):
                 "optimizer": (f"SGD(lr={lr:g}, momentum={args.momentum:g}, wd={wd:g})" if sgd
                               else f"AdamW(lr={lr:g}, wd={wd:g})") + (" fp32 master weights" if master else ""),
                 "recipe": args.recipe,
+                "miopen_implicit_gemm": os.environ.get("MIOPEN_DEBUG_CONV_IMPLICIT_GEMM", "default"),
                 "optimizer_schedule": args.overlap_schedule if overlap else "after backward",
                 "channels_last": bool(args.channels_last),
                 "comm_dtype": args.comm_dtype,

@@ -220,6 +220,171 @@ __global__ __launch_bounds__(NB * 4, ST == 1 ? 2 : 1) void conv3x3_wgrad_kernel(
       }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Stride-1 weight gradient on ROW BANDS (r6): the reduction runs over runs of 224
+// consecutive output pixels of the flattened (batch x height) row space — R = 224 / W whole rows
+// (W = 56 / 28 / 14 / 7: R = 4 / 8 / 16 / 32; 224 = 7 MFMA k-steps of 32 pixels), bands crossing
+// images as in conv3x3_band.hip — instead of 8 x 8 patches, which computed 1.306x the pixels at
+// W = 28 / 14 / 7 (a 4 x 4 patch grid over 28 x 28, ...). A band stages its dY rows (224 x 64 n)
+// and its input halo (R + 2·segments rows of W + 2 pixels, zero padding rows at image edges, zero
+// columns) once per 64 x 64 channel tile, and every tap reads its shifted pixel window from the
+// halo: 63 (k-step, tap) steps of 4 MFMAs per wave per band (7x the patch kernel's MFMAs per
+// barrier). One 4-wave block per CU, persistent over a contiguous range of bands, two LDS stages
+// (the next band's DMA under this band's 252 MFMAs per wave), both by inline-asm LDS-DMA (hipcc
+// cannot tell the stages apart and would drain the prefetch before every fragment read).
+// LDS image: 128-B rows (one pixel, 64 channels); the 32-B chunk PAIR (16 channels, one wave's or
+// one fragment's) of a row is XOR-swizzled by f(v) = ((v >> 1) & 1) | ((v >> 2) & 2) of the pixel's
+// virtual index v (dY: the band pixel m; halo: hr·W + hc, which runs on consecutively over the
+// output-row wraps of a fragment, and has the parity of the LDS row): the 8 rows one
+// ds_read_b64_tr_b16 half-wave reads (two 4-pixel groups 8 pixels apart) land on 8 distinct bank
+// octets for any start (checked exhaustively). Same slab layout / slab_sum_kernel as the patch kernel.
+__device__ __forceinline__ int bfz(int v) { return ((v >> 1) & 1) | ((v >> 2) & 2); }
+
+// halo row of band-relative output row lr (tap row 0) — conv3x3_band.hip band_hrow
+__device__ __forceinline__ int wb_hrow(int lr, int n0, int H) {
+  if (lr < n0) return lr;
+  const int k = (lr - n0) / H;
+  return n0 + 2 + k * (H + 2) + (lr - n0 - k * H);
+}
+
+__global__ __launch_bounds__(256, 1) void conv3x3_wgrad_band_kernel(
+    const uint16_t* __restrict__ dY, const uint16_t* __restrict__ X, float* __restrict__ ws,
+    const uint16_t* __restrict__ zeros, int N, int C, int B, int H, int W, int R, int nbands, int ntiles, int splits,
+    int hpix) {
+  constexpr int BP = 224;  // band pixels (7 k-steps)
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int STAGE = (BP + hpix) * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wg = dev::xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wg % ntiles, sidx = wg / ntiles;  // XCD neighbours: same bands, other tiles
+  const int ctiles = C >> 6;
+  const int n0c = (tile / ctiles) * 64, c0 = (tile % ctiles) * 64;
+  const int bb = (int)((int64_t)nbands * sidx / splits), be = (int)((int64_t)nbands * (sidx + 1) / splits);
+  const int W2 = W + 2, rows_total = B * H;
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem);
+  const int uwid = __builtin_amdgcn_readfirstlane(wid);
+  auto glds16 = [](const void* gsrc, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+  };
+  const int pos = lane & 7;  // 16-B slot of the lane's 128-B LDS row in a DMA piece (8 rows)
+
+  auto issue = [&](int band, int slot) {
+    const uint32_t st = lbase + slot * STAGE;
+    const int g0 = band * R, b0 = g0 / H, h0 = g0 - b0 * H;
+    const int n0 = min(H - h0, R), rv = min(R, rows_total - g0), valid = rv * W;
+    // dY: 28 pieces of 8 pixel rows; wave w takes pieces w, w + 4, ...
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int m = (uwid + 4 * k) * 8 + (lane >> 3);
+      const bool ok = m < valid;
+      const uint16_t* src = ok ? dY + ((int64_t)g0 * W + m) * N + n0c + 8 * (pos ^ (2 * bfz(m))) : zeros;
+      glds16(src, __builtin_amdgcn_readfirstlane(st + (uwid + 4 * k) * 1024));
+    }
+    // halo: hpix / 8 pieces (a multiple of 4), rows past the band's halo read the zero line
+    for (int k = uwid; k * 8 < hpix; k += 4) {
+      const int q = k * 8 + (lane >> 3), hr = q / W2, hc = q - hr * W2;
+      int b = b0, ih = h0 - 1 + hr;
+      if (hr >= n0 + 2) {  // a later image of the band
+        const int r2 = hr - (n0 + 2), kk = r2 / (H + 2);
+        b = b0 + 1 + kk;
+        ih = r2 - kk * (H + 2) - 1;
+      }
+      const int iw = hc - 1, hlast = wb_hrow(rv - 1, n0, H) + 2;
+      const bool ok = hr <= hlast && b < B && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      const uint16_t* src =
+          ok ? X + (((int64_t)b * H + ih) * W + iw) * C + c0 + 8 * (pos ^ (2 * bfz(hr * W + hc))) : zeros;
+      glds16(src, __builtin_amdgcn_readfirstlane(st + (BP + k * 8) * 128));
+    }
+  };
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed reads: group gq = lane >> 4, lane 4q + p supplies pixel 8gq + q (+4) of the k-step and
+  // bytes 8p of its 32-B chunk pair
+  const int gq = lane >> 4, q4 = (lane >> 2) & 3, p8 = 8 * (lane & 3);
+  if (bb < be) {
+    issue(bb, 0);
+    for (int band = bb; band < be; ++band) {
+      const int slot = (band - bb) & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                 // this wave's pieces of the band
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // everyone's; the other slot is free
+      issue(band + 1 < be ? band + 1 : band, slot ^ 1);                // (past the end: a re-stage, unused)
+      const uint8_t* A = smem + slot * STAGE;
+      const uint8_t* Hs = A + BP * 128;
+      const int g0 = band * R, b0 = g0 / H, h0 = g0 - b0 * H;
+      const int n0 = min(H - h0, R), rv = min(R, rows_total - g0), valid = rv * W;
+      // this lane's halo pixel (tap (0, 0)) of pixel m: LDS row and virtual index; past the band's
+      // pixels a valid one (its dY row is zero)
+      auto hpx = [&](int m, int& hq, int& hv) {
+        const int mm = min(m, valid - 1), lr = mm / W, col = mm - lr * W, hr = wb_hrow(lr, n0, H);
+        hq = hr * W2 + col;
+        hv = hr * W + col;
+      };
+      auto read_a = [&](int ks, bf16x8 (&a)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v4s v8[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int m = ks * 32 + 8 * gq + q4 + 4 * h;
+            v8[h] = lds_tr16(A + m * 128 + 32 * (i ^ bfz(m)) + p8);
+          }
+          a[i] = __builtin_bit_cast(bf16x8, v8);
+        }
+      };
+      int hq[2], hv[2];
+      auto set_k = [&](int ks) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) hpx(ks * 32 + 8 * gq + q4 + 4 * h, hq[h], hv[h]);
+      };
+      auto read_b = [&](int t) {
+        const int r = t / 3, sx = t - 3 * r;
+        v4s v8[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int q = hq[h] + r * W2 + sx, v = hv[h] + r * W + sx;
+          v8[h] = lds_tr16(Hs + q * 128 + 32 * (wid ^ bfz(v)) + p8);
+        }
+        return __builtin_bit_cast(bf16x8, v8);
+      };
+#pragma unroll 1
+      for (int ks = 0; ks < 7; ++ks) {
+        bf16x8 a[4];
+        read_a(ks, a);
+        set_k(ks);
+        bf16x8 b = read_b(0);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          bf16x8 bn = b;
+          if (t < 8) bn = read_b(t + 1);  // the next tap's fragment under this tap's MFMAs
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][t], 0, 0, 0);
+          b = bn;
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-stage lands before exit
+  }
+  // fp32 slab ws[sidx][n][tap][c] as the patch kernel: lane holds n = n0c + 16i + 4(lane >> 4) + r,
+  // c = c0 + 16 wid + (lane & 15)
+  float* out = ws + (int64_t)sidx * N * 9 * C;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0c + 16 * i + 4 * (lane >> 4) + r;
+        out[((int64_t)n * 9 + t) * C + c0 + 16 * wid + (lane & 15)] = acc[i][t][r];
+      }
+}
+
 // dW = sum of the S slabs, cast to the weight dtype (4 elements per lane, slab sum split 8 ways)
 template <typename W>
 __global__ __launch_bounds__(512) void slab_sum_kernel(const float* __restrict__ ws, int S, int64_t nk,
@@ -270,8 +435,64 @@ int cu_count() {
 
 }  // namespace
 
+namespace {
+// XDDP_WGRAD3_BAND=0: the 8 x 8 patch kernel at stride 1 too (A/B switch)
+bool band_wgrad() {
+  static const bool v = [] { const char* e = std::getenv("XDDP_WGRAD3_BAND"); return !(e && e[0] == '0'); }();
+  return v;
+}
+
+template <typename F>
+void slab_sum(const at::Tensor& ws, int splits, int64_t nk, const at::Tensor& dw, hipStream_t stream, F&&) {
+  const int grid = (int)((nk / 4 + 63) / 64);
+  auto red = [&](auto tag) {
+    using W = decltype(tag);
+    hipLaunchKernelGGL((slab_sum_kernel<W>), dim3(grid), dim3(512), 0, stream, ws.data_ptr<float>(), splits, nk,
+                       reinterpret_cast<W*>(dw.data_ptr()));
+    XDDP_HIP_CHECK(hipGetLastError());
+  };
+  switch (dw.scalar_type()) {
+    case at::kBFloat16: red(dev::bf16_t{}); break;
+    case at::kFloat: red(float{}); break;
+    case at::kHalf: red(dev::f16_t{}); break;
+    default: TORCH_CHECK(false, "conv3x3_wgrad: unsupported weight dtype");
+  }
+}
+
+at::Tensor conv3x3_wgrad_band(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w_like) {
+  const int64_t B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), N = dy.size(1);
+  const int R = (int)(224 / W);
+  const int64_t rows_total = B * H, nbands = (rows_total + R - 1) / R;
+  TORCH_CHECK(nbands < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "conv3x3_wgrad_band: too large");
+  // halo pixels: the most a band needs (a segment per image it touches, two padding rows each)
+  int segs = 1;
+  for (int64_t k = 0; k < H; ++k) {
+    const int64_t h0 = (k * R) % H, n0 = std::min<int64_t>(H - h0, R);
+    segs = std::max<int>(segs, (int)(1 + (R - n0 + H - 1) / H));
+  }
+  segs = (int)std::min<int64_t>(segs, B);
+  const int hpix = (int)((((R + 2 * segs) * (W + 2)) + 31) / 32 * 32);
+  const size_t lds = (size_t)2 * (224 + hpix) * 128;
+  TORCH_CHECK(lds <= 160 * 1024, "conv3x3_wgrad_band: LDS budget exceeded (", lds, " B)");
+  const int ntiles = (int)((N / 64) * (C / 64));
+  const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(nbands, std::max(1, cu_count() / ntiles)));
+  auto ws = at::empty({splits, N, 9, C}, dy.options().dtype(at::kFloat));
+  auto dw = at::empty({N, C, 3, 3}, dy.options().dtype(w_like.scalar_type()).memory_format(at::MemoryFormat::ChannelsLast));
+  auto stream = c10::hip::getCurrentHIPStream(dy.device().index()).stream();
+  ensure_dyn_lds((const void*)conv3x3_wgrad_band_kernel, lds);
+  hipLaunchKernelGGL(conv3x3_wgrad_band_kernel, dim3(ntiles * splits), dim3(256), lds, stream,
+                     reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                     ws.data_ptr<float>(), zero_line_w(x), (int)N, (int)C, (int)B, (int)H, (int)W, R, (int)nbands, ntiles,
+                     splits, hpix);
+  XDDP_HIP_CHECK(hipGetLastError());
+  slab_sum(ws, splits, N * 9 * C, dw, stream, 0);
+  return dw;
+}
+}  // namespace
+
 // dy [B, N, OH, OW], x [B, C, IH, IW] (bf16 channels_last, pad 1, stride 1|2) -> dW [N, C, 3, 3]
-// channels_last (OHWI memory) in w_like's dtype.
+// channels_last (OHWI memory) in w_like's dtype. Stride 1 with 224 % W == 0 runs the band kernel
+// (splits_req >= 0 forces the patch kernel, 0 with its default split: timing scripts / tests).
 at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,
                                int64_t splits_req) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 &&
@@ -286,6 +507,7 @@ at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_
   TORCH_CHECK(x.numel() < (int64_t(1) << 40) && dy.numel() < (int64_t(1) << 40), "conv3x3_wgrad_patch: too large");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) % 16) == 0 && (reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16) == 0,
               "conv3x3_wgrad_patch: 16-B aligned operands required");
+  if (stride == 1 && 224 % OW == 0 && band_wgrad() && splits_req < 0) return conv3x3_wgrad_band(dy, x, w_like);
   const int pgh = (int)((OH + kP - 1) / kP), pgw = (int)((OW + kP - 1) / kP);
   const int64_t npatch64 = B * pgh * pgw;
   TORCH_CHECK(npatch64 > 0 && npatch64 < (int64_t(1) << 31), "conv3x3_wgrad_patch: bad patch count");

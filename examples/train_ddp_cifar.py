@@ -25,10 +25,13 @@ from distributeddataparallel_amd import distributed as dist  # noqa: E402
 from distributeddataparallel_amd.data import CIFAR10Binary, DistributedSampler, SyntheticImages  # noqa: E402
 from distributeddataparallel_amd.models import SimpleCNN  # noqa: E402
 from distributeddataparallel_amd.utils.checkpoint import load_checkpoint, save_checkpoint  # noqa: E402
+from distributeddataparallel_amd.utils.precision import accurate_fp32_convs  # noqa: E402
 
 
 def train(rank, args):
     backend = args.backend or ("rccl" if torch.cuda.is_available() else "cpu")
+    if backend != "cpu" and args.accurate_convs:
+        accurate_fp32_convs()  # fp32-accurate MIOpen convolutions (utils/precision.py), before the first conv
     if args.impl == "torch":  # the reference's own stack, for parity runs (torch DDP + torch BN, NCHW)
         return train_torch(rank, args, backend)
     dist.init_process_group(backend)
@@ -129,6 +132,9 @@ def main():
     ap.add_argument("--checkpoint", default=None)
     ap.add_argument("--resume", default=None)
     ap.add_argument("--log-every", type=int, default=100, help="rank-0 loss print interval (reference: 100)")
+    ap.add_argument("--accurate-convs", action="store_true",
+                    help="MIOpen's implicit-GEMM fp32 conv solvers off: fp32-accurate weight gradients, slower "
+                         "channels_last convs (utils/precision.py)")
     ap.add_argument("--impl", choices=["xddp", "torch"], default="xddp",
                     help="torch = torch DDP + torch BatchNorm (the reference stack), for parity runs")
     args = ap.parse_args()

@@ -1,11 +1,11 @@
 bash scripts/gpu_steps.sh \
- "ringtest|300|python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_conv_gemm_gpu.py -k wgrad" \
- "wg_ring|200|python -u scripts/wgrad1x1_time.py" \
- "r50ring_a|240|python -u bench.py --steps 30 --warmup 10 --json-out gpurun_out/r50ring_a.json" \
- "r50old_a|240|XDDP_WGRAD_RING=0 python -u bench.py --steps 30 --warmup 10 --json-out gpurun_out/r50old_a.json" \
- "r50ring_b|240|python -u bench.py --steps 30 --warmup 10 --json-out gpurun_out/r50ring_b.json" \
- "r50old_b|240|XDDP_WGRAD_RING=0 python -u bench.py --steps 30 --warmup 10 --json-out gpurun_out/r50old_b.json" \
- "reftf_def|200|python -u tests/_ref_teacher_forced.py 8" \
- "reftf_det|200|XDDP_TEST_CUDNN_DETERMINISTIC=1 python -u tests/_ref_teacher_forced.py 8" \
- "reftf_nowino|200|MIOPEN_DEBUG_CONV_WINOGRAD=0 python -u tests/_ref_teacher_forced.py 8" \
- "reftf_noimpl|200|MIOPEN_DEBUG_CONV_IMPLICIT_GEMM=0 python -u tests/_ref_teacher_forced.py 8"
+ "r50|240|python -u bench.py --json-out gpurun_out/r50.json" \
+ "ref_x1|200|python -u bench.py --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --json-out gpurun_out/ref_x1.json" \
+ "ref_t1|200|python -u bench.py --impl torch --norm torch --channels-last 0 --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --json-out gpurun_out/ref_t1.json" \
+ "ref_xf1|200|python -u bench.py --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --fast-convs 1 --json-out gpurun_out/ref_xf1.json" \
+ "ref_tf1|200|python -u bench.py --impl torch --norm torch --channels-last 0 --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --fast-convs 1 --json-out gpurun_out/ref_tf1.json" \
+ "ref_x2|200|python -u bench.py --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --json-out gpurun_out/ref_x2.json" \
+ "ref_t2|200|python -u bench.py --impl torch --norm torch --channels-last 0 --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --json-out gpurun_out/ref_t2.json" \
+ "ref_xf2|200|python -u bench.py --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --fast-convs 1 --json-out gpurun_out/ref_xf2.json" \
+ "ref_tf2|200|python -u bench.py --impl torch --norm torch --channels-last 0 --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --fast-convs 1 --json-out gpurun_out/ref_tf2.json" \
+ "reftest|400|python -u -m pytest -v -s --timeout 300 --timeout-method thread tests/test_reference_workload_gpu.py"

@@ -195,6 +195,31 @@ def test_conv3x3_wgrad_patch_matches_conv2d(b, cin, h, w, cout, s):
     torch.testing.assert_close(dw32, ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
 
 
+@pytest.mark.parametrize("b,cin,h,w,cout", [
+    (2, 64, 56, 56, 64),     # W = 56: 4-row bands inside one image
+    (3, 128, 28, 28, 128),   # W = 28: 8-row bands, every 4th crosses two images; 84 rows -> a partial last band
+    (5, 256, 14, 14, 128),   # W = 14: 16-row bands over 2-3 images, 2 n-tiles x 4 c-tiles
+    (9, 128, 7, 7, 256),     # W = 7: 32-row bands over up to 6 images (halo segments), 63 rows -> partial
+    (1, 64, 9, 7, 64),       # a single partial band (9 rows < R = 32)
+])
+def test_conv3x3_wgrad_band_matches_conv2d_and_patch(b, cin, h, w, cout):
+    """Stride-1 weight gradient on 224-pixel row bands (conv3x3_wgrad_band_kernel: the default when
+    224 % W == 0) vs fp32 PyTorch, and vs the 8x8-patch kernel (splits = 0) with fp32 output."""
+    torch.manual_seed(7)
+    x = _cl(torch.randn(b, cin, h, w, device="cuda"))
+    dy = _cl(torch.randn(b, cout, h, w, device="cuda"))
+    wt = _cl(torch.randn(cout, cin, 3, 3, device="cuda"))
+    ref = torch.nn.grad.conv2d_weight(x.float(), wt.shape, dy.float(), stride=1, padding=1)
+    band = C.conv3x3_wgrad_patch(dy, x, 1, wt.float())
+    patch = C.conv3x3_wgrad_patch(dy, x, 1, wt.float(), 0)
+    torch.testing.assert_close(band, ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
+    torch.testing.assert_close(band, patch, rtol=1e-5, atol=1e-5 * ref.abs().max().item())
+    bb = C.conv3x3_wgrad_patch(dy, x, 1, wt)
+    assert bb.dtype == torch.bfloat16 and bb.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(bb.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+    assert torch.equal(C.conv3x3_wgrad_patch(dy, x, 1, wt), bb)  # fixed-order slab sum: bitwise repeatable
+
+
 @pytest.mark.parametrize("b,cin,h,w,cout,rows,cfg,off", [
     (2, 64, 56, 56, 64, 4, 0, 30.0),     # layer-1 band: 4 rows = 224 pixels, N = 64 tiles, weight ring
     (3, 128, 28, 28, 128, 7, 1, 0.0),    # layer-2 band: 7 rows = 196 pixels, 208-row tile, B in registers
