@@ -229,9 +229,11 @@ __global__ __launch_bounds__(NB * 4, ST == 1 ? 2 : 1) void conv3x3_wgrad_kernel(
 // and its input halo (R + 2·segments rows of W + 2 pixels, zero padding rows at image edges, zero
 // columns) once per 64 x 64 channel tile, and every tap reads its shifted pixel window from the
 // halo: 63 (k-step, tap) steps of 4 MFMAs per wave per band (7x the patch kernel's MFMAs per
-// barrier). One 4-wave block per CU, persistent over a contiguous range of bands, two LDS stages
-// (the next band's DMA under this band's 252 MFMAs per wave), both by inline-asm LDS-DMA (hipcc
-// cannot tell the stages apart and would drain the prefetch before every fragment read).
+// barrier). One block per CU, persistent over a contiguous range of bands, two LDS stages (the next
+// band's DMA under this band's MFMAs), both by inline-asm LDS-DMA (hipcc cannot tell the stages apart
+// and would drain the prefetch before every fragment read). Eight waves, two per SIMD, split each
+// band's 7 k-steps by parity (4 + 3, alternating by band): the first version (4 waves, one per SIMD)
+// exposed every fragment-read and DMA-issue latency and ran 137-147 us per ResNet-50 shape.
 // LDS image: 128-B rows (one pixel, 64 channels); the 32-B chunk PAIR (16 channels, one wave's or
 // one fragment's) of a row is XOR-swizzled by f(v) = ((v >> 1) & 1) | ((v >> 2) & 2) of the pixel's
 // virtual index v (dY: the band pixel m; halo: hr·W + hc, which runs on consecutively over the
@@ -247,7 +249,7 @@ __device__ __forceinline__ int wb_hrow(int lr, int n0, int H) {
   return n0 + 2 + k * (H + 2) + (lr - n0 - k * H);
 }
 
-__global__ __launch_bounds__(256, 1) void conv3x3_wgrad_band_kernel(
+__global__ __launch_bounds__(512, 2) void conv3x3_wgrad_band_kernel(
     const uint16_t* __restrict__ dY, const uint16_t* __restrict__ X, float* __restrict__ ws,
     const uint16_t* __restrict__ zeros, int N, int C, int B, int H, int W, int R, int nbands, int ntiles, int splits,
     int hpix) {
@@ -255,6 +257,10 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_band_kernel(
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int STAGE = (BP + hpix) * 128;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // 8 waves, two per SIMD: wave w owns c slice cw = w & 3 (16 channels) for all 64 n and 9 taps, and
+  // k-step parity group grp = w >> 2 of each band (the two groups alternate the 4-step share by band
+  // parity); the groups' accumulators are summed through LDS once, at the end
+  const int cw = wid & 3, grp = wid >> 2;
   const int wg = dev::xcd_remap(blockIdx.x, gridDim.x);
   const int tile = wg % ntiles, sidx = wg / ntiles;  // XCD neighbours: same bands, other tiles
   const int ctiles = C >> 6;
@@ -274,16 +280,16 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_band_kernel(
     const uint32_t st = lbase + slot * STAGE;
     const int g0 = band * R, b0 = g0 / H, h0 = g0 - b0 * H;
     const int n0 = min(H - h0, R), rv = min(R, rows_total - g0), valid = rv * W;
-    // dY: 28 pieces of 8 pixel rows; wave w takes pieces w, w + 4, ...
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      const int m = (uwid + 4 * k) * 8 + (lane >> 3);
+    // dY: 28 pieces of 8 pixel rows; wave w takes pieces w, w + 8, ...
+    for (int k = uwid; k < 28; k += 8) {
+      const int m = k * 8 + (lane >> 3);
       const bool ok = m < valid;
       const uint16_t* src = ok ? dY + ((int64_t)g0 * W + m) * N + n0c + 8 * (pos ^ (2 * bfz(m))) : zeros;
-      glds16(src, __builtin_amdgcn_readfirstlane(st + (uwid + 4 * k) * 1024));
+      glds16(src, __builtin_amdgcn_readfirstlane(st + k * 1024));
     }
     // halo: hpix / 8 pieces (a multiple of 4), rows past the band's halo read the zero line
-    for (int k = uwid; k * 8 < hpix; k += 4) {
+    const int hlast = wb_hrow(rv - 1, n0, H) + 2;
+    for (int k = uwid; k * 8 < hpix; k += 8) {
       const int q = k * 8 + (lane >> 3), hr = q / W2, hc = q - hr * W2;
       int b = b0, ih = h0 - 1 + hr;
       if (hr >= n0 + 2) {  // a later image of the band
@@ -291,7 +297,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_band_kernel(
         b = b0 + 1 + kk;
         ih = r2 - kk * (H + 2) - 1;
       }
-      const int iw = hc - 1, hlast = wb_hrow(rv - 1, n0, H) + 2;
+      const int iw = hc - 1;
       const bool ok = hr <= hlast && b < B && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
       const uint16_t* src =
           ok ? X + (((int64_t)b * H + ih) * W + iw) * C + c0 + 8 * (pos ^ (2 * bfz(hr * W + hc))) : zeros;
@@ -349,12 +355,12 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_band_kernel(
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int q = hq[h] + r * W2 + sx, v = hv[h] + r * W + sx;
-          v8[h] = lds_tr16(Hs + q * 128 + 32 * (wid ^ bfz(v)) + p8);
+          v8[h] = lds_tr16(Hs + q * 128 + 32 * (cw ^ bfz(v)) + p8);
         }
         return __builtin_bit_cast(bf16x8, v8);
       };
 #pragma unroll 1
-      for (int ks = 0; ks < 7; ++ks) {
+      for (int ks = grp ^ ((band - bb) & 1); ks < 7; ks += 2) {
         bf16x8 a[4];
         read_a(ks, a);
         set_k(ks);
@@ -371,8 +377,22 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_band_kernel(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-stage lands before exit
   }
-  // fp32 slab ws[sidx][n][tap][c] as the patch kernel: lane holds n = n0c + 16i + 4(lane >> 4) + r,
-  // c = c0 + 16 wid + (lane & 15)
+  // group 1's accumulators -> LDS (144 x 256 floats, element-major: lanes on consecutive words), group 0
+  // adds them in a fixed order and writes the fp32 slab ws[sidx][n][tap][c] as the patch kernel: lane
+  // holds n = n0c + 16i + 4(lane >> 4) + r, c = c0 + 16 cw + (lane & 15)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float* xr = reinterpret_cast<float*>(smem);
+  const int xl = cw * 64 + lane;
+  if (grp == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xr[((i * 9 + t) * 4 + r) * 256 + xl] = acc[i][t][r];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (grp == 1) return;
   float* out = ws + (int64_t)sidx * N * 9 * C;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -381,7 +401,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_band_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n0c + 16 * i + 4 * (lane >> 4) + r;
-        out[((int64_t)n * 9 + t) * C + c0 + 16 * wid + (lane & 15)] = acc[i][t][r];
+        out[((int64_t)n * 9 + t) * C + c0 + 16 * cw + (lane & 15)] = acc[i][t][r] + xr[((i * 9 + t) * 4 + r) * 256 + xl];
       }
 }
 
@@ -436,9 +456,10 @@ int cu_count() {
 }  // namespace
 
 namespace {
-// XDDP_WGRAD3_BAND=0: the 8 x 8 patch kernel at stride 1 too (A/B switch)
+// XDDP_WGRAD3_BAND=1: the row-band kernel for stride-1 weight gradients (opt-in: it measured 137-147 us
+// vs the patch kernel's 82-87 us per call at every ResNet-50 stage shape, profiles/r6_wgrad3_band_ab.txt)
 bool band_wgrad() {
-  static const bool v = [] { const char* e = std::getenv("XDDP_WGRAD3_BAND"); return !(e && e[0] == '0'); }();
+  static const bool v = [] { const char* e = std::getenv("XDDP_WGRAD3_BAND"); return e && e[0] == '1'; }();
   return v;
 }
 
@@ -472,7 +493,8 @@ at::Tensor conv3x3_wgrad_band(const at::Tensor& dy, const at::Tensor& x, const a
   }
   segs = (int)std::min<int64_t>(segs, B);
   const int hpix = (int)((((R + 2 * segs) * (W + 2)) + 31) / 32 * 32);
-  const size_t lds = (size_t)2 * (224 + hpix) * 128;
+  // two stages; at the end the k-step groups' accumulators are exchanged through the same LDS
+  const size_t lds = std::max<size_t>((size_t)2 * (224 + hpix) * 128, (size_t)144 * 256 * sizeof(float));
   TORCH_CHECK(lds <= 160 * 1024, "conv3x3_wgrad_band: LDS budget exceeded (", lds, " B)");
   const int ntiles = (int)((N / 64) * (C / 64));
   const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(nbands, std::max(1, cu_count() / ntiles)));
@@ -480,7 +502,7 @@ at::Tensor conv3x3_wgrad_band(const at::Tensor& dy, const at::Tensor& x, const a
   auto dw = at::empty({N, C, 3, 3}, dy.options().dtype(w_like.scalar_type()).memory_format(at::MemoryFormat::ChannelsLast));
   auto stream = c10::hip::getCurrentHIPStream(dy.device().index()).stream();
   ensure_dyn_lds((const void*)conv3x3_wgrad_band_kernel, lds);
-  hipLaunchKernelGGL(conv3x3_wgrad_band_kernel, dim3(ntiles * splits), dim3(256), lds, stream,
+  hipLaunchKernelGGL(conv3x3_wgrad_band_kernel, dim3(ntiles * splits), dim3(512), lds, stream,
                      reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
                      ws.data_ptr<float>(), zero_line_w(x), (int)N, (int)C, (int)B, (int)H, (int)W, R, (int)nbands, ntiles,
                      splits, hpix);
@@ -491,8 +513,9 @@ at::Tensor conv3x3_wgrad_band(const at::Tensor& dy, const at::Tensor& x, const a
 }  // namespace
 
 // dy [B, N, OH, OW], x [B, C, IH, IW] (bf16 channels_last, pad 1, stride 1|2) -> dW [N, C, 3, 3]
-// channels_last (OHWI memory) in w_like's dtype. Stride 1 with 224 % W == 0 runs the band kernel
-// (splits_req >= 0 forces the patch kernel, 0 with its default split: timing scripts / tests).
+// channels_last (OHWI memory) in w_like's dtype. splits_req: < 0 the default kernel (the patch kernel; the
+// band kernel at stride 1 with 224 % W == 0 under XDDP_WGRAD3_BAND=1), -2 forces the band kernel there,
+// >= 0 forces the patch kernel (0 with its default split): timing scripts / tests.
 at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_t stride, const at::Tensor& w_like,
                                int64_t splits_req) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 &&
@@ -507,7 +530,8 @@ at::Tensor conv3x3_wgrad_patch(const at::Tensor& dy, const at::Tensor& x, int64_
   TORCH_CHECK(x.numel() < (int64_t(1) << 40) && dy.numel() < (int64_t(1) << 40), "conv3x3_wgrad_patch: too large");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) % 16) == 0 && (reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16) == 0,
               "conv3x3_wgrad_patch: 16-B aligned operands required");
-  if (stride == 1 && 224 % OW == 0 && band_wgrad() && splits_req < 0) return conv3x3_wgrad_band(dy, x, w_like);
+  if (stride == 1 && 224 % OW == 0 && (splits_req == -2 || (band_wgrad() && splits_req < 0)))
+    return conv3x3_wgrad_band(dy, x, w_like);
   const int pgh = (int)((OH + kP - 1) / kP), pgw = (int)((OW + kP - 1) / kP);
   const int64_t npatch64 = B * pgh * pgw;
   TORCH_CHECK(npatch64 > 0 && npatch64 < (int64_t(1) << 31), "conv3x3_wgrad_patch: bad patch count");

@@ -203,21 +203,22 @@ def test_conv3x3_wgrad_patch_matches_conv2d(b, cin, h, w, cout, s):
     (1, 64, 9, 7, 64),       # a single partial band (9 rows < R = 32)
 ])
 def test_conv3x3_wgrad_band_matches_conv2d_and_patch(b, cin, h, w, cout):
-    """Stride-1 weight gradient on 224-pixel row bands (conv3x3_wgrad_band_kernel: the default when
-    224 % W == 0) vs fp32 PyTorch, and vs the 8x8-patch kernel (splits = 0) with fp32 output."""
+    """Stride-1 weight gradient on 224-pixel row bands (conv3x3_wgrad_band_kernel, splits_req = -2; opt-in
+    by XDDP_WGRAD3_BAND=1, slower than the patch kernel) vs fp32 PyTorch, and vs the 8x8-patch kernel
+    (splits = 0) with fp32 output."""
     torch.manual_seed(7)
     x = _cl(torch.randn(b, cin, h, w, device="cuda"))
     dy = _cl(torch.randn(b, cout, h, w, device="cuda"))
     wt = _cl(torch.randn(cout, cin, 3, 3, device="cuda"))
     ref = torch.nn.grad.conv2d_weight(x.float(), wt.shape, dy.float(), stride=1, padding=1)
-    band = C.conv3x3_wgrad_patch(dy, x, 1, wt.float())
+    band = C.conv3x3_wgrad_patch(dy, x, 1, wt.float(), -2)
     patch = C.conv3x3_wgrad_patch(dy, x, 1, wt.float(), 0)
     torch.testing.assert_close(band, ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
     torch.testing.assert_close(band, patch, rtol=1e-5, atol=1e-5 * ref.abs().max().item())
-    bb = C.conv3x3_wgrad_patch(dy, x, 1, wt)
+    bb = C.conv3x3_wgrad_patch(dy, x, 1, wt, -2)
     assert bb.dtype == torch.bfloat16 and bb.is_contiguous(memory_format=torch.channels_last)
     torch.testing.assert_close(bb.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
-    assert torch.equal(C.conv3x3_wgrad_patch(dy, x, 1, wt), bb)  # fixed-order slab sum: bitwise repeatable
+    assert torch.equal(C.conv3x3_wgrad_patch(dy, x, 1, wt, -2), bb)  # fixed-order slab sum: bitwise repeatable
 
 
 @pytest.mark.parametrize("b,cin,h,w,cout,rows,cfg,off", [
