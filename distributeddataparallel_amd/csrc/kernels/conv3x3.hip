@@ -210,27 +210,40 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv3x3_fwd_kernel(
 #pragma unroll
   for (int e = 0; e < 8; ++e) st_s[e] = st_ss[e] = 0.f;
   const u32x4 st_k = *reinterpret_cast<const u32x4*>(Cs + cc * 16);  // row 0 (always valid): the shift
-#pragma unroll 4
-  for (int q = tid; q < BM * CPR; q += NT) {
-    const int row = q / CPR;
-    if (row < rows_valid) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
-      int64_t yrow = m0 + row;
-      if (DG2) {  // phase pixel -> dX pixel (2p + a, 2q + b)
-        const int hw = PH * PW, m = m0 + row, b = m / hw, rem = m - b * hw, p = rem / PW, q = rem - p * PW;
-        yrow = ((int64_t)b * dg.H + 2 * p + pa) * dg.W + 2 * q + pb;
-      }
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + yrow * N + n0 + cc * 8));
-      if (STATS) {
-        st_n += 1.f;
+  // rows tid / CPR + (NT / CPR)·i; each batch's LDS reads issued before its stores (rows past M read
+  // row rows_valid - 1 and are not stored): a read-then-use per row inside `if (row < rows_valid)`
+  // compiled to one ds_read + s_waitcnt lgkmcnt(0) round trip per row
+  constexpr int NIT = BM * CPR / NT, RSTR = NT / CPR, EB = NIT < 4 ? NIT : 4;
+  static_assert(BM * CPR % NT == 0, "readout rows must divide evenly over the threads");
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const float d0 = __uint_as_float(v[h] << 16) - __uint_as_float(st_k[h] << 16);
-          const float d1 = __uint_as_float(v[h] & 0xffff0000u) - __uint_as_float(st_k[h] & 0xffff0000u);
-          st_s[2 * h] += d0;
-          st_s[2 * h + 1] += d1;
-          st_ss[2 * h] = fmaf(d0, d0, st_ss[2 * h]);
-          st_ss[2 * h + 1] = fmaf(d1, d1, st_ss[2 * h + 1]);
+  for (int i0 = 0; i0 < NIT; i0 += EB) {
+    u32x4 vv[EB];
+#pragma unroll
+    for (int j = 0; j < EB; ++j)
+      if (i0 + j < NIT)
+        vv[j] = *reinterpret_cast<const u32x4*>(Cs + min(tid / CPR + RSTR * (i0 + j), rows_valid - 1) * CST + cc * 16);
+#pragma unroll
+    for (int j = 0; j < EB; ++j) {
+      const int row = tid / CPR + RSTR * (i0 + j);
+      if (i0 + j < NIT && row < rows_valid) {
+        const u32x4 v = vv[j];
+        int64_t yrow = m0 + row;
+        if (DG2) {  // phase pixel -> dX pixel (2p + a, 2q + b)
+          const int hw = PH * PW, m = m0 + row, b = m / hw, rem = m - b * hw, p = rem / PW, q = rem - p * PW;
+          yrow = ((int64_t)b * dg.H + 2 * p + pa) * dg.W + 2 * q + pb;
+        }
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + yrow * N + n0 + cc * 8));
+        if (STATS) {
+          st_n += 1.f;
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const float d0 = __uint_as_float(v[h] << 16) - __uint_as_float(st_k[h] << 16);
+            const float d1 = __uint_as_float(v[h] & 0xffff0000u) - __uint_as_float(st_k[h] & 0xffff0000u);
+            st_s[2 * h] += d0;
+            st_s[2 * h + 1] += d1;
+            st_ss[2 * h] = fmaf(d0, d0, st_ss[2 * h]);
+            st_ss[2 * h + 1] = fmaf(d1, d1, st_ss[2 * h + 1]);
+          }
         }
       }
     }

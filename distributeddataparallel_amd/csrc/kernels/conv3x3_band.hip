@@ -79,6 +79,11 @@ __device__ __forceinline__ int band_hrow(int lr, int n0, int H) {
   return n0 + 2 + k * (H + 2) + (lr - n0 - k * H);
 }
 
+// readout rows per batch of LDS reads in the epilogue (issued together, then stored)
+#ifndef XDDP_BAND_RB
+#define XDDP_BAND_RB 4
+#endif
+
 template <int TM, int WM, int TN, int WN, bool STATS, int RING>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv3x3_band_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y,
@@ -272,22 +277,34 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv3x3_band_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (STATS && wt == wg) st_k = *reinterpret_cast<const u32x4*>(Cs + cc * 16);
     const int64_t y0 = (int64_t)g0 * g.W;                              // the band's first output pixel
-#pragma unroll 4
-    for (int q = tid; q < BM * CPR; q += NT) {
-      const int row = q / CPR;
-      if (row < valid) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + (y0 + row) * N + n0c + cc * 8));
-        if (STATS) {
-          st_n += 1.f;
+    // rows tid / CPR + (NT / CPR)·i; each batch's LDS reads issued before its stores (rows past the
+    // band read row valid - 1 and are not stored): a read-then-use per row inside `if (row < valid)`
+    // compiled to one ds_read + s_waitcnt lgkmcnt(0) round trip per row
+    constexpr int NIT = BM * CPR / NT, RSTR = NT / CPR, EB = NIT < XDDP_BAND_RB ? NIT : XDDP_BAND_RB;
+    static_assert(BM * CPR % NT == 0, "readout rows must divide evenly over the threads");
 #pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            const float d0 = __uint_as_float(v[h] << 16) - __uint_as_float(st_k[h] << 16);
-            const float d1 = __uint_as_float(v[h] & 0xffff0000u) - __uint_as_float(st_k[h] & 0xffff0000u);
-            st_s[2 * h] += d0;
-            st_s[2 * h + 1] += d1;
-            st_ss[2 * h] = fmaf(d0, d0, st_ss[2 * h]);
-            st_ss[2 * h + 1] = fmaf(d1, d1, st_ss[2 * h + 1]);
+    for (int i0 = 0; i0 < NIT; i0 += EB) {
+      u32x4 vv[EB];
+#pragma unroll
+      for (int j = 0; j < EB; ++j)
+        if (i0 + j < NIT) vv[j] = *reinterpret_cast<const u32x4*>(Cs + min(tid / CPR + RSTR * (i0 + j), valid - 1) * CST + cc * 16);
+#pragma unroll
+      for (int j = 0; j < EB; ++j) {
+        const int row = tid / CPR + RSTR * (i0 + j);
+        if (i0 + j < NIT && row < valid) {
+          const u32x4 v = vv[j];
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + (y0 + row) * N + n0c + cc * 8));
+          if (STATS) {
+            st_n += 1.f;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              const float d0 = __uint_as_float(v[h] << 16) - __uint_as_float(st_k[h] << 16);
+              const float d1 = __uint_as_float(v[h] & 0xffff0000u) - __uint_as_float(st_k[h] & 0xffff0000u);
+              st_s[2 * h] += d0;
+              st_s[2 * h + 1] += d1;
+              st_ss[2 * h] = fmaf(d0, d0, st_ss[2 * h]);
+              st_ss[2 * h + 1] = fmaf(d1, d1, st_ss[2 * h + 1]);
+            }
           }
         }
       }

@@ -424,26 +424,38 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
         sk[0] = __uint_as_float(k << 16);
         sk[1] = __uint_as_float(k & 0xffff0000u);
       }
+      // full tiles: every row's LDS read issued before the first use, from one base address plus
+      // immediate offsets (a read-then-use per row inside `if (row < rows_valid)` compiled to 16
+      // serialized ds_read + s_waitcnt lgkmcnt(0) round trips per tile); the partial last tile
+      // keeps the per-row form
+      constexpr int NSR = BM / SRS;
+      const uint8_t* sbase = Cs + (tid / SPR) * CST + sp * 4;
+      auto add_stat = [&](uint32_t v) {
+        const float d0 = __uint_as_float(v << 16) - sk[0], d1 = __uint_as_float(v & 0xffff0000u) - sk[1];
+        sn += 1.f;
+        ssum[0] += d0;
+        ssum[1] += d1;
+        ssq[0] = fmaf(d0, d0, ssq[0]);
+        ssq[1] = fmaf(d1, d1, ssq[1]);
+      };
+      if (rows_valid == BM) {
+        uint32_t sv[NSR];
 #pragma unroll
-      for (int i = 0; i < BM / SRS; ++i) {
-        const int row = tid / SPR + SRS * i;
-        if (row < rows_valid) {
-          const uint32_t v = *reinterpret_cast<const uint32_t*>(Cs + row * CST + sp * 4);
-          const float d0 = __uint_as_float(v << 16) - sk[0], d1 = __uint_as_float(v & 0xffff0000u) - sk[1];
-          sn += 1.f;
-          ssum[0] += d0;
-          ssum[1] += d1;
-          ssq[0] = fmaf(d0, d0, ssq[0]);
-          ssq[1] = fmaf(d1, d1, ssq[1]);
-        }
+        for (int i = 0; i < NSR; ++i) sv[i] = *reinterpret_cast<const uint32_t*>(sbase + SRS * i * CST);
+#pragma unroll
+        for (int i = 0; i < NSR; ++i) add_stat(sv[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < NSR; ++i)
+          if (tid / SPR + SRS * i < rows_valid) add_stat(*reinterpret_cast<const uint32_t*>(sbase + SRS * i * CST));
       }
     }
+    if constexpr (EPI) {
 #pragma unroll
-    for (int it = 0; it < RIT; ++it) {
-      const int row = (tid + NT * it) / CPR;
-      if (row < rows_valid) {
-        u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
-        if (EPI) {
+      for (int it = 0; it < RIT; ++it) {
+        const int row = (tid + NT * it) / CPR;
+        if (row < rows_valid) {
+          u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
           const u32x4 yv = e_y[EPI ? it : 0], ad = e_ad[EPI ? it : 0];
           const uint32_t mb = e_mb[EPI ? it : 0];
           const bool form1 = epi.bits != nullptr;
@@ -469,9 +481,32 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv1x1_gemm_kernel(
             st_ss[2 * h] = fmaf(g0, __uint_as_float(yv[h] << 16) - mu.x, st_ss[2 * h]);
             st_ss[2 * h + 1] = fmaf(g1, __uint_as_float(yv[h] & 0xffff0000u) - mu.y, st_ss[2 * h + 1]);
           }
+          if (NTSTORE) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + (m0 + row) * N + n0 + cc * 8));
+          else *reinterpret_cast<u32x4*>(Y + (m0 + row) * N + n0 + cc * 8) = v;
         }
+      }
+    } else {
+      // readout of full tiles: every row's LDS read issued before the first store (thread row
+      // tid / CPR + (NT / CPR)·it, chunk cc) in the statistics instances; the partial last tile and the
+      // other instances keep the per-row form (their batch spilled VGPRs: the BN-backward prologue
+      // forms, and the EPI instances with their epilogue operands live)
+      constexpr int RSTR = NT / CPR;
+      auto st_row = [&](int row, const u32x4& v) {
         if (NTSTORE) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(Y + (m0 + row) * N + n0 + cc * 8));
         else *reinterpret_cast<u32x4*>(Y + (m0 + row) * N + n0 + cc * 8) = v;
+      };
+      if (STATS && rows_valid == BM) {
+        u32x4 rv[RIT];
+#pragma unroll
+        for (int it = 0; it < RIT; ++it) rv[it] = *reinterpret_cast<const u32x4*>(Cs + (tid / CPR + RSTR * it) * CST + cc * 16);
+#pragma unroll
+        for (int it = 0; it < RIT; ++it) st_row(tid / CPR + RSTR * it, rv[it]);
+      } else {
+#pragma unroll
+        for (int it = 0; it < RIT; ++it) {
+          const int row = (tid + NT * it) / CPR;
+          if (row < rows_valid) st_row(row, *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16));
+        }
       }
     }
     lds_barrier();  // Cs aliases the operand buffers the next tile stores into

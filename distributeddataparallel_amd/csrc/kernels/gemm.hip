@@ -354,11 +354,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
     for (int e = 0; e < 8; ++e) cssq[e] = 0.f;
     st_k = *reinterpret_cast<const u32x4*>(Cs + cc * 16);
   }
-#pragma unroll 4
-  for (int q = tid; q < kBM * CPR; q += kThreads) {
-    const int row = q / CPR;
-    if (row >= rows_valid) continue;
-    u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CST + cc * 16);
+  // rows tid / CPR + (kThreads / CPR)·i; each batch's LDS reads issued before its stores (rows past M
+  // read row rows_valid - 1 and are skipped): a read-then-use per row compiled to one ds_read +
+  // s_waitcnt lgkmcnt(0) round trip per row
+  auto out_row = [&](int row, u32x4 v) {
     int64_t off = (int64_t)(m0 + row) * N + n0 + cc * 8;
     if constexpr (MODE == kModeDgS2) {  // dY-grid pixel (b, i, j) -> dX pixel (b, 2i + ph, 2j + pw)
       const int m = m0 + row, hw = cg.OH * cg.OW, b = m / hw, rem = m - b * hw, y = rem / cg.OW, x = rem - y * cg.OW;
@@ -411,6 +410,21 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
       *reinterpret_cast<u32x4*>(Y + off) = v;
     } else {
       *reinterpret_cast<u32x4*>(Y + off) = v;
+    }
+  };
+  constexpr int NIT = kBM * CPR / kThreads, RSTR = kThreads / CPR, EB = NIT < 4 ? NIT : 4;
+  static_assert(kBM * CPR % kThreads == 0, "readout rows must divide evenly over the threads");
+#pragma unroll
+  for (int i0 = 0; i0 < NIT; i0 += EB) {
+    u32x4 vv[EB];
+#pragma unroll
+    for (int j = 0; j < EB; ++j)
+      if (i0 + j < NIT)
+        vv[j] = *reinterpret_cast<const u32x4*>(Cs + min(tid / CPR + RSTR * (i0 + j), rows_valid - 1) * CST + cc * 16);
+#pragma unroll
+    for (int j = 0; j < EB; ++j) {
+      const int row = tid / CPR + RSTR * (i0 + j);
+      if (i0 + j < NIT && row < rows_valid) out_row(row, vv[j]);
     }
   }
   if (EPI == kEpiStats) {
