@@ -14,7 +14,11 @@
 // Forward statistics are sums of (x - K_c) with one shared per-channel shift K_c = x[0, c],
 // so partials add exactly like the backward's and large |mean|/std does not cancel.
 #include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
+
+#include <atomic>
+#include <cstdlib>
 #include <torch/extension.h>
 
 #include "common.h"
@@ -269,6 +273,125 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
   }
 }
 
+// Counters of the finalize folded into the reduce kernels (dev::tail_arrive): per launch slot and
+// channel group an (arrival, departure) pair. Zero at code-object load, zeroed again by each
+// launch's last reducer; a launch takes the next slot round-robin, so launches in flight on
+// different streams do not share counters.
+constexpr int kTailSlots = 64, kTailGroups = 64;
+__device__ unsigned g_bn_tail_ctr[kTailSlots * kTailGroups * 2];
+__device__ unsigned g_bn_tail_timeout;
+
+struct BwdFin {
+  int slot;       // folded form: this launch's counter slot in g_bn_tail_ctr (-1: separate kernel)
+  int S;          // folded form: reducer blocks per channel group
+  int wdt;
+  int64_t M;
+  const void* weight;
+  const float* invstd;
+  void* dweight;
+  void* dbias;
+  float* coef;
+  const float* fold_mean;
+  const float* ss_copy;
+  int dbg = 0;  // (timing only, XDDP_BN_TAIL_DBG: 1 = stop after the partial stores, 3 = after the poll)
+};
+
+__device__ __forceinline__ float ld_w(const void* p, int wdt, int c) {
+  return wdt == 1 ? Elem<bf16_t, float>::ld(static_cast<const bf16_t*>(p), c)
+                  : (wdt == 2 ? Elem<f16_t, float>::ld(static_cast<const f16_t*>(p), c) : static_cast<const float*>(p)[c]);
+}
+__device__ __forceinline__ void st_w(void* p, int wdt, int c, float v) {
+  if (wdt == 1) Elem<bf16_t, float>::st(static_cast<bf16_t*>(p), c, v);
+  else if (wdt == 2) Elem<f16_t, float>::st(static_cast<f16_t*>(p), c, v);
+  else static_cast<float*>(p)[c] = v;
+}
+
+// per channel: dgamma, dbeta; dx = k1*dy_eff + k2*(x-mean) + k3, for the 8-channel vector cv, by
+// 256 threads. The vector's partials are 64 B per row block (16 floats); thread t reads float4 q =
+// t & 3 of row blocks t >> 2, t >> 2 + 64, ..., so one wave load covers 16 whole 64-B segments
+// (a row-per-lane layout would fetch every line 16 times over when the loads bypass L1). The 4
+// sums per lane reduce over the lanes sharing q (4 xor steps), then over the 4 waves through LDS
+// (red: 64 floats), in a fixed order. SC1: the partials were handed over inside this launch (the
+// folded form) and every read of them is an sc1 load (16-B buffer loads); the additions are the
+// same in the same order, so both forms give bitwise the same results.
+template <bool SC1>
+__device__ __forceinline__ void bwd_finalize_vec(const float* __restrict__ part, int rblocks, int C, int cv,
+                                                 const BwdFin& f, float* red) {
+  const int tid = threadIdx.x + blockDim.x * threadIdx.y, lane = tid & 63, wid = tid >> 6;
+  const int q = tid & 3, rr = tid >> 2;
+  // the per-channel parameters are loaded up front, under the partials' loads (not a second
+  // dependent memory round trip after the reduction: the launch is latency-bound)
+  const int c = cv * 8 + (tid & 7);
+  float inv = 0.f, g = 1.f, fm = 0.f, ssc = 0.f, ssh = 0.f;
+  if (tid < 8) {
+    inv = f.invstd[c];
+    if (f.weight) g = ld_w(f.weight, f.wdt, c);
+    if (f.fold_mean) fm = f.fold_mean[c];
+    if (f.ss_copy) {
+      ssc = f.ss_copy[c];
+      ssh = f.ss_copy[C + c];
+    }
+  }
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t rstride = (int64_t)C * 2;           // floats per row block
+  const int64_t off0 = (int64_t)cv * 16 + q * 4;     // this thread's float4 within a row block
+  if (SC1) {
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(part), (short)0,
+                                                        (int)(rblocks * rstride * 4), 0x00020000);
+#pragma unroll 8
+    for (int b = rr; b < rblocks; b += 64) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)((b * rstride + off0) * 4), 0, 16);  // sc1
+      acc[0] += __uint_as_float(v[0]);
+      acc[1] += __uint_as_float(v[1]);
+      acc[2] += __uint_as_float(v[2]);
+      acc[3] += __uint_as_float(v[3]);
+    }
+  } else {
+#pragma unroll 8
+    for (int b = rr; b < rblocks; b += 64) {
+      const float4 v = *reinterpret_cast<const float4*>(part + b * rstride + off0);
+      acc[0] += v.x;
+      acc[1] += v.y;
+      acc[2] += v.z;
+      acc[3] += v.w;
+    }
+  }
+#pragma unroll
+  for (int o = 4; o < 64; o <<= 1)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
+  if (lane < 4) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[wid * 16 + lane * 4 + k] = acc[k];
+  }
+  __syncthreads();
+  if (tid < 8) {
+    const float sd = (red[2 * tid] + red[16 + 2 * tid]) + (red[32 + 2 * tid] + red[48 + 2 * tid]);
+    const float sdx = (red[2 * tid + 1] + red[16 + 2 * tid + 1]) + (red[32 + 2 * tid + 1] + red[48 + 2 * tid + 1]);
+    if (f.dweight) st_w(f.dweight, f.wdt, c, sdx * inv);
+    if (f.dbias) st_w(f.dbias, f.wdt, c, sd);
+    const float invM = 1.f / (float)f.M;
+    float* coef = f.coef;
+    coef[c] = g * inv;                                   // k1
+    coef[C + c] = -g * inv * inv * inv * sdx * invM;     // k2
+    coef[2 * C + c] = -g * inv * sd * invM;              // k3
+    // fold_mean: dx = k1·g + k2·x + (k3 - k2·mean), the form a consumer GEMM prologue applies
+    if (f.fold_mean) coef[2 * C + c] -= coef[C + c] * fm;
+    // ss_copy: rows 3-4 carry the forward scale / shift (the consumer recomputes the ReLU mask)
+    if (f.ss_copy) {
+      coef[3 * C + c] = ssc;
+      coef[4 * C + c] = ssh;
+    }
+  }
+}
+
+// The separate finalize: one 256-thread block per 8-channel vector.
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int rblocks, int C,
+                                                              BwdFin f) {
+  __shared__ float red[64];
+  bwd_finalize_vec<false>(part, rblocks, C, blockIdx.x, f, red);
+}
+
 // ---------------------------------------------------------------- backward reduce
 // part layout [rblocks][C][2] = (sum dy_eff, sum dy_eff*(x-mean))
 // MASK: 0 = no ReLU, 1 = ReLU mask from the saved output y, 2 = ReLU mask recomputed from x
@@ -286,7 +409,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
                                                                int64_t M, int C, int64_t rows_per,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ ss,
-                                                               float* __restrict__ part) {
+                                                               float* __restrict__ part, BwdFin fin) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
   const int c0 = (blockIdx.x * TX + tx) * 8;
@@ -371,95 +494,26 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
   }
   if (ty == 0) {
     float* dst = part + ((int64_t)blockIdx.y * C + c0) * 2;
+    if (fin.slot >= 0) {
+      float v[16];  // (all LDS reads first: an atomic store between them would serialize each)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) dst[j] = my[j];
-  }
-}
-
-// per channel: dgamma, dbeta; dx = k1*dy_eff + k2*(x-mean) + k3. Same single-wave shape as the
-// stats finalize: lanes stride over row-block partials, then a shuffle butterfly.
-// 16 per-lane sums reduced over a wave in 17 shuffles (halving butterfly: each exchange step
-// trades half of the live values, so lane l ends holding the wave total of value index
-// 8·b5 + 4·b4 + 2·b3 + b2, where b_k is bit k of l; every group of 4 lanes holds the same one).
-__device__ __forceinline__ float wave_reduce16(float (&v)[16], int lane) {
+      for (int j = 0; j < 16; ++j) v[j] = my[j];
 #pragma unroll
-  for (int step = 0, width = 8; step < 4; ++step, width >>= 1) {
-    const int o = 32 >> step;
-    const bool hi = lane & o;
+      for (int j = 0; j < 16; ++j) dev::st_sc1(dst + j, v[j]);
+    } else {
 #pragma unroll
-    for (int i = 0; i < width; ++i) {
-      const float send = hi ? v[i] : v[i + width];
-      const float recv = __shfl_xor(send, o, 64);
-      v[i] = (hi ? v[i + width] : v[i]) + recv;
+      for (int j = 0; j < 16; ++j) dst[j] = my[j];
     }
   }
-  float r = v[0];
-  r += __shfl_xor(r, 2, 64);
-  r += __shfl_xor(r, 1, 64);
-  return r;
-}
-
-// per channel: dgamma, dbeta; dx = k1*dy_eff + k2*(x-mean) + k3. One 256-thread block per
-// 8-channel vector: threads stride over the row-block partials (16 floats each, 4 float4 loads),
-// the 16 sums reduce per wave in 17 shuffles, then across the 4 waves through LDS.
-template <typename W>
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int rblocks, int C,
-                                                              int64_t M, const W* __restrict__ weight,
-                                                              const float* __restrict__ invstd, W* dweight,
-                                                              W* dbias, float* __restrict__ coef,
-                                                              const float* __restrict__ fold_mean,
-                                                              const float* __restrict__ ss_copy = nullptr) {
-  __shared__ float red[4][16];
-  const int cv = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // the per-channel parameters are loaded up front, under the partials' loads (not a second
-  // dependent memory round trip after the reduction: the launch is latency-bound)
-  const int c = cv * 8 + (tid & 7);
-  float inv = 0.f, g = 1.f, fm = 0.f, ssc = 0.f, ssh = 0.f;
-  if (tid < 8) {
-    inv = invstd[c];
-    if (weight) g = Elem<W, float>::ld(weight, c);
-    if (fold_mean) fm = fold_mean[c];
-    if (ss_copy) {
-      ssc = ss_copy[c];
-      ssh = ss_copy[C + c];
-    }
-  }
-  float acc[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-#pragma unroll 2
-  for (int b = tid; b < rblocks; b += 256) {
-    const float4* p = reinterpret_cast<const float4*>(part + ((int64_t)b * C + cv * 8) * 2);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 v = p[q];
-      acc[4 * q] += v.x;
-      acc[4 * q + 1] += v.y;
-      acc[4 * q + 2] += v.z;
-      acc[4 * q + 3] += v.w;
-    }
-  }
-  const float r = wave_reduce16(acc, lane);
-  if ((lane & 3) == 0) {
-    const int j = ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
-    red[wid][j] = r;
-  }
-  __syncthreads();
-  if (tid >= 8) return;
-  const float sd = (red[0][2 * tid] + red[1][2 * tid]) + (red[2][2 * tid] + red[3][2 * tid]);
-  const float sdx = (red[0][2 * tid + 1] + red[1][2 * tid + 1]) + (red[2][2 * tid + 1] + red[3][2 * tid + 1]);
-  if (dweight) Elem<W, float>::st(dweight, c, sdx * inv);
-  if (dbias) Elem<W, float>::st(dbias, c, sd);
-  const float invM = 1.f / (float)M;
-  coef[c] = g * inv;                                   // k1
-  coef[C + c] = -g * inv * inv * inv * sdx * invM;     // k2
-  coef[2 * C + c] = -g * inv * sd * invM;              // k3
-  // fold_mean: dx = k1·g + k2·x + (k3 - k2·mean), the form a consumer GEMM prologue applies
-  if (fold_mean) coef[2 * C + c] -= coef[C + c] * fm;
-  // ss_copy: rows 3-4 carry the forward scale / shift (the consumer recomputes the ReLU mask)
-  if (ss_copy) {
-    coef[3 * C + c] = ssc;
-    coef[4 * C + c] = ssh;
+  if (fin.slot < 0 || fin.dbg == 1) return;
+  // the finalize, folded into the last arrivals of this channel group: fin.S reducer blocks, each
+  // finalizing every fin.S-th of the group's TX channel vectors (dev::tail_arrive)
+  const int rank = dev::tail_arrive(g_bn_tail_ctr + ((int64_t)fin.slot * kTailGroups + blockIdx.x) * 2, gridDim.y,
+                                    fin.S, reinterpret_cast<int*>(lds), &g_bn_tail_timeout);
+  if (rank < 0 || fin.dbg == 3) return;
+  for (int v = rank; v < TX; v += fin.S) {
+    bwd_finalize_vec<true>(part, gridDim.y, C, blockIdx.x * TX + v, fin, lds + 64);
+    __syncthreads();  // (red is rewritten by the next vector)
   }
 }
 
@@ -550,7 +604,38 @@ W* opt_ptr(const c10::optional<at::Tensor>& t) {
   return (t.has_value() && t->defined()) ? reinterpret_cast<W*>(t->data_ptr()) : nullptr;
 }
 
+int wdt_code(at::ScalarType st) {
+  TORCH_CHECK(st == at::kFloat || st == at::kBFloat16 || st == at::kHalf, "xddp batch_norm: unsupported weight dtype ", st);
+  return st == at::kBFloat16 ? 1 : (st == at::kHalf ? 2 : 0);
+}
+
+// XDDP_BN_TAIL=1 runs the BN-backward finalize in the reduce kernel's last arrivals (BwdFin,
+// dev::tail_arrive) instead of a separate launch. Opt-in: measured slower (profiles/
+// r6_bn_finalize_fold.txt): the arrival fan-in and the reducers' poll cost 3.5-6 us per launch and
+// the reduction after the last arrival 2-3 us, against 2.6-3.3 us for the whole separate finalize
+// (one launch, coalesced 16-B partial reads); the headline step lost 1.1 %.
+bool bn_tail_enabled() {
+  const char* e = std::getenv("XDDP_BN_TAIL");  // (read per call: tests switch it in-process)
+  return e && e[0] == '1';
+}
+
+int next_tail_slot() {
+  static std::atomic<unsigned> n{0};
+  return (int)(n.fetch_add(1, std::memory_order_relaxed) % kTailSlots);
+}
+
 }  // namespace
+
+// Whether any folded finalize hit its spin bound (a producer never arrived) since the last call;
+// clears the flag. Device-synchronizing: for tests and diagnostics.
+bool bn_tail_timeouts(int64_t device) {
+  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  unsigned v = 0, z = 0;
+  XDDP_HIP_CHECK(hipDeviceSynchronize());
+  XDDP_HIP_CHECK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_bn_tail_timeout), sizeof(v), 0, hipMemcpyDeviceToHost));
+  XDDP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_bn_tail_timeout), &z, sizeof(z), 0, hipMemcpyHostToDevice));
+  return v != 0;
+}
 
 // returns (y, mean, invstd)
 std::vector<at::Tensor> bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& weight,
@@ -667,7 +752,7 @@ at::Tensor bn_grad_partials(const at::Tensor& dy_in, const at::Tensor& x, const 
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, 0, false, false>), dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds,
                        stream, reinterpret_cast<const T*>(dy.data_ptr()), nullptr,
                        reinterpret_cast<const T*>(x.data_ptr()), nullptr, nullptr, nullptr, M, (int)C, g.rows_per,
-                       mean.data_ptr<float>(), nullptr, part.data_ptr<float>());
+                       mean.data_ptr<float>(), nullptr, part.data_ptr<float>(), BwdFin{-1});
     XDDP_HIP_CHECK(hipGetLastError());
   });
   return part;
@@ -774,10 +859,17 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
   // need_dres: the reduce pass writes g = mask*(dy+dy2) into dres; the elementwise pass then
   // reads (g, x) with no mask and no second gradient
   const bool wg = need_dres;
+  // the finalize runs in the reduce kernel's last arrivals when the grid allows it (the whole
+  // grid resident: ~512 blocks; at most kTailGroups channel groups)
+  const bool tail = bn_tail_enabled() && g.cblocks <= kTailGroups && (int64_t)g.cblocks * g.rblocks <= 1024;
+  BwdFin fin{tail ? next_tail_slot() : -1, std::min(g.tx, g.rblocks), wdt_code(wdt), M,
+             has_w ? weight->data_ptr() : nullptr, invstd.data_ptr<float>(), dw.defined() ? dw.data_ptr() : nullptr,
+             db.defined() ? db.data_ptr() : nullptr, coef.data_ptr<float>(), coef_only ? mean.data_ptr<float>() : nullptr,
+             coef_only && coef_mask ? ss->data_ptr<float>() : nullptr};
+  if (const char* e = std::getenv("XDDP_BN_TAIL_DBG")) fin.dbg = std::atoi(e);
   dispatch_act(x.scalar_type(), [&](auto tag_t) {
     using T = decltype(tag_t);
-    dispatch_w(wdt, [&](auto tag_w) {
-      using W = decltype(tag_w);
+    {
       const T* yp = mask == 1 ? reinterpret_cast<const T*>(y->data_ptr()) : nullptr;
       const float* ssp = mask == 2 ? ss->data_ptr<float>() : nullptr;
       const uint8_t* mbp = mask == 3 ? mask_bits->data_ptr<uint8_t>() : nullptr;
@@ -787,7 +879,8 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
       auto launch_red = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(g.cblocks, g.rblocks), dim3(g.tx, g.ty), lds, stream,
                            reinterpret_cast<const T*>(dy.data_ptr()), d2p, reinterpret_cast<const T*>(x.data_ptr()),
-                           yp, mbp, gp, M, (int)C, g.rows_per, mean.data_ptr<float>(), ssp, part.data_ptr<float>());
+                           yp, mbp, gp, M, (int)C, g.rows_per, mean.data_ptr<float>(), ssp, part.data_ptr<float>(),
+                           fin);
       };
 #define XDDP_BN_RED(MK)                                                                           \
   if (dual) { if (wg) launch_red(bn_bwd_reduce_kernel<T, MK, true, true>);                        \
@@ -800,14 +893,11 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
       else { XDDP_BN_RED(0) }
 #undef XDDP_BN_RED
       XDDP_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(256), 0, stream,
-                         part.data_ptr<float>(), g.rblocks, (int)C, M,
-                         has_w ? reinterpret_cast<const W*>(weight->data_ptr()) : nullptr, invstd.data_ptr<float>(),
-                         dw.defined() ? reinterpret_cast<W*>(dw.data_ptr()) : nullptr,
-                         db.defined() ? reinterpret_cast<W*>(db.data_ptr()) : nullptr, coef.data_ptr<float>(),
-                         coef_only ? mean.data_ptr<float>() : nullptr,
-                         coef_only && coef_mask ? ss->data_ptr<float>() : nullptr);
-      XDDP_HIP_CHECK(hipGetLastError());
+      if (!tail) {
+        hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(256), 0, stream, part.data_ptr<float>(),
+                           g.rblocks, (int)C, fin);
+        XDDP_HIP_CHECK(hipGetLastError());
+      }
       const int64_t nvec = M * C / 8;
       if (coef_only) {  // nothing more: the consumer applies the coefficients
       } else if (wg) {
@@ -832,7 +922,7 @@ std::vector<at::Tensor> bn_backward(const at::Tensor& dy_in, const at::Tensor& x
 #undef XDDP_BN_ELEM
       }
       XDDP_HIP_CHECK(hipGetLastError());
-    });
+    }
   });
   return {coef_only ? coef : dx, dw, db, dres};
 }
@@ -853,15 +943,12 @@ std::vector<at::Tensor> bn_backward_from_partials(const at::Tensor& part, int64_
   const auto wdt = has_w ? weight->scalar_type() : at::kFloat;
   at::Tensor dw = (has_w && need_dweight) ? at::empty({C}, weight->options()) : at::Tensor();
   at::Tensor db = (has_w && need_dweight) ? at::empty({C}, weight->options()) : at::Tensor();
-  dispatch_w(wdt, [&](auto tag_w) {
-    using W = decltype(tag_w);
-    hipLaunchKernelGGL((bn_bwd_finalize_kernel<W>), dim3(C / 8), dim3(256), 0, stream, part.data_ptr<float>(),
-                       (int)part.size(0), (int)C, M, has_w ? reinterpret_cast<const W*>(weight->data_ptr()) : nullptr,
-                       invstd.data_ptr<float>(), dw.defined() ? reinterpret_cast<W*>(dw.data_ptr()) : nullptr,
-                       db.defined() ? reinterpret_cast<W*>(db.data_ptr()) : nullptr, coef.data_ptr<float>(),
-                       fold_mean ? mean.data_ptr<float>() : nullptr);
-    XDDP_HIP_CHECK(hipGetLastError());
-  });
+  const BwdFin fin{-1, 0, wdt_code(wdt), M, has_w ? weight->data_ptr() : nullptr, invstd.data_ptr<float>(),
+                   dw.defined() ? dw.data_ptr() : nullptr, db.defined() ? db.data_ptr() : nullptr, coef.data_ptr<float>(),
+                   fold_mean ? mean.data_ptr<float>() : nullptr, nullptr};
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C / 8), dim3(256), 0, stream, part.data_ptr<float>(),
+                     (int)part.size(0), (int)C, fin);
+  XDDP_HIP_CHECK(hipGetLastError());
   return {coef, dw, db};
 }
 

@@ -231,6 +231,60 @@ __device__ __forceinline__ T block_sum(T v, T* scratch) {
   return r;
 }
 
+// ---- in-launch hand-off to the last arrivals (a finalize folded into its producer) ------------
+// The producing blocks store their partials write-through (st_sc1: global_store … sc1), then
+// arrive: every wave drains its stores (s_waitcnt vmcnt(0)), the workgroup barrier, one lane adds
+// to the arrival counter (relaxed, agent scope). The last S arrivals become the reducers: one lane
+// polls the counter with relaxed sc1 loads until every producer has arrived, the barrier releases
+// the other waves, and every read of the partials is an sc1 load (ld_sc1). This is the
+// write-through form of the guide's inter-workgroup hand-off (cdna_hip_programming.md §6 Guideline
+// 16; MI355X_MICROARCH.md "Valid forms", row 1: atomic-add counter, sc1 poll, barrier, sc1 stores
+// and loads), so neither a release nor an acquire fence is needed, and it holds for any placement
+// of the blocks over CUs and XCDs. The reducers are arrivals, so every other block has finished
+// its work: at most S - 1 blocks are still running, and spinning never starves them of a slot.
+// Each reducer adds to the departure counter once its poll matched; the one whose add comes last
+// zeroes both counters, so the next launch in stream order (and every graph replay) starts from
+// zero with no memset. The spin is bounded: after ~1 s it sets *timeout and goes on.
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __uint_as_float(
+      __hip_atomic_load(const_cast<unsigned*>(reinterpret_cast<const unsigned*>(p)), __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Returns this block's reducer rank in [0, S), or -1 (no finalize work). Called by every thread;
+// `word` is one int of LDS that no thread reads between this call's barriers.
+__device__ __forceinline__ int tail_arrive(unsigned* ctr, int nblocks, int S, int* word, unsigned* timeout) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  const int tid = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z);
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int rank = (int)t - (nblocks - S);
+    if (rank >= 0) {
+      for (unsigned spins = 0;
+           __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nblocks;) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 24)) {
+          __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      if (__hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S - 1)) {
+        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    *word = rank;
+  }
+  __syncthreads();
+  const int rank = *word;
+  __syncthreads();  // (the caller may reuse the word's LDS)
+  return rank;
+}
+
 // XCD-aware remap (bijective for any grid): consecutive logical tiles land on one XCD's L2.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;

@@ -45,6 +45,7 @@ std::vector<at::Tensor> bn_backward_from_partials(const at::Tensor& part, int64_
                                                   const at::Tensor& invstd, bool need_dweight, bool fold_mean);
 // dx = k1·g + k2·(x - mean) + k3 per channel (coef [3, C] unfolded): the BN-backward elementwise
 // pass on an already-masked gradient g
+bool bn_tail_timeouts(int64_t device);
 at::Tensor bn_backward_elem(const at::Tensor& g, const at::Tensor& x, const at::Tensor& mean, const at::Tensor& coef);
 // 3x3 pad-1 conv (stride 1/2) as an implicit MFMA GEMM (csrc/kernels/conv3x3.hip)
 // Transformer linear layers (gemm.hip): y = a · wᵀ with epilogue 0 none | 1 + bias |

@@ -25,6 +25,8 @@ void bind_norm_kernels(py::module_& m) {
         py::arg("pro_nbt") = py::none(), py::arg("pro_res_nbt") = py::none());
   m.def("bn_backward_from_partials", &bn_backward_from_partials, py::arg("partials"), py::arg("M"), py::arg("weight"),
         py::arg("mean"), py::arg("invstd"), py::arg("need_dweight"), py::arg("fold_mean") = true);
+  m.def("bn_tail_timeouts", &bn_tail_timeouts, py::arg("device"),
+        "whether a folded BN finalize hit its spin bound since the last call (clears the flag; synchronizes)");
   m.def("bn_backward_elem", &bn_backward_elem, py::arg("g"), py::arg("x"), py::arg("mean"), py::arg("coef"));
   m.def("bn_moments", &bn_moments, py::arg("x"));
   m.def("cross_entropy_forward", &cross_entropy_forward, py::arg("logits"), py::arg("target"),

@@ -1,11 +1,7 @@
 bash scripts/gpu_steps.sh \
- "r50|240|python -u bench.py --json-out gpurun_out/r50.json" \
- "ref_x1|200|python -u bench.py --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --json-out gpurun_out/ref_x1.json" \
- "ref_t1|200|python -u bench.py --impl torch --norm torch --channels-last 0 --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --json-out gpurun_out/ref_t1.json" \
- "ref_xf1|200|python -u bench.py --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --fast-convs 1 --json-out gpurun_out/ref_xf1.json" \
- "ref_tf1|200|python -u bench.py --impl torch --norm torch --channels-last 0 --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --fast-convs 1 --json-out gpurun_out/ref_tf1.json" \
- "ref_x2|200|python -u bench.py --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --json-out gpurun_out/ref_x2.json" \
- "ref_t2|200|python -u bench.py --impl torch --norm torch --channels-last 0 --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --json-out gpurun_out/ref_t2.json" \
- "ref_xf2|200|python -u bench.py --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --fast-convs 1 --json-out gpurun_out/ref_xf2.json" \
- "ref_tf2|200|python -u bench.py --impl torch --norm torch --channels-last 0 --model simplecnn --batch-size 32 --image-size 32 --recipe reference --steps 300 --warmup 30 --fast-convs 1 --json-out gpurun_out/ref_tf2.json" \
- "reftest|400|python -u -m pytest -v -s --timeout 300 --timeout-method thread tests/test_reference_workload_gpu.py"
+ "tailtest|300|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_bn_tail_gpu.py tests/test_norm_gpu.py" \
+ "tailtime|200|PYTHONPATH=. python -u scripts/bn_tail_time.py" \
+ "r50_t1|200|python -u bench.py --steps 30 --warmup 10 --diag-steps 0 --json-out gpurun_out/r50_t1.json" \
+ "r50_t0|200|XDDP_BN_TAIL=0 python -u bench.py --steps 30 --warmup 10 --diag-steps 0 --json-out gpurun_out/r50_t0.json" \
+ "r50_t1b|200|python -u bench.py --steps 30 --warmup 10 --diag-steps 0 --json-out gpurun_out/r50_t1b.json" \
+ "r50_t0b|200|XDDP_BN_TAIL=0 python -u bench.py --steps 30 --warmup 10 --diag-steps 0 --json-out gpurun_out/r50_t0b.json"
