@@ -95,19 +95,27 @@ def fit_alpha_busbw(sizes: Sequence[int], times_s: Sequence[float], world: int) 
     return round(alpha * 1e6, 3), round(bw / 1e9, 3)
 
 
+ROUTE_MARGIN = float(os.environ.get("XDDP_ROUTE_MARGIN", "0.1"))
+
+
 def choose_routes(sizes: Sequence[int], times: Dict[int, Sequence[Optional[float]]]) -> Tuple[List[int], List[int], Dict[int, int]]:
     """Fastest route per probe size -> (bounds, routes, winner_by_size).
 
-    ``times[route][i]`` = seconds at ``sizes[i]`` (None = route unavailable at that size). Ties go
-    to the base route (then the lower route id). Messages up to ``bounds[k]`` bytes take
+    ``times[route][i]`` = seconds at ``sizes[i]`` (None = route unavailable at that size). A peer
+    route wins only below (1 - ROUTE_MARGIN) x the base route's time (ties and near-ties go to the
+    base route; among peer routes, the faster, then the lower route id). Messages up to ``bounds[k]`` bytes take
     ``routes[k]``; the last bound is open-ended."""
     order = sorted(range(len(sizes)), key=lambda i: sizes[i])
     winner: Dict[int, int] = {}
+    # a hand-written peer lane replaces the library path only where it is clearly faster: it must
+    # beat the base route's time by ROUTE_MARGIN (measurement noise must not route gradients onto the
+    # less-exercised path for a gain of a few percent)
     for i in order:
-        best_r, best_t = ROUTE_BASE, times.get(ROUTE_BASE, [None] * len(sizes))[i]
+        base_t = times.get(ROUTE_BASE, [None] * len(sizes))[i]
+        best_r, best_t = ROUTE_BASE, (None if base_t is None else base_t * (1.0 - ROUTE_MARGIN))
         for r in sorted(times):
             t = times[r][i]
-            if t is None:
+            if t is None or r == ROUTE_BASE:
                 continue
             if best_t is None or t < best_t:
                 best_r, best_t = r, t
@@ -170,6 +178,25 @@ def self_check(pg, iters: int = 8) -> Tuple[bool, str]:
                     return False, f"a peer kernel timed out (call {k}, {ROUTE_NAMES[route]})"
                 if not torch.equal(x, want):
                     bad.append(f"call {k} {ROUTE_NAMES[route]} {str(dt).replace('torch.', '')} n={n}")
+        # a burst without host syncs, the way DDP issues its buckets: both lanes and the base route
+        # interleaved, every call on its own tensor and pattern (consecutive uses of a lane's
+        # double-buffered slot carry different values), checked only after the whole burst
+        burst = []
+        for k in range(iters):
+            for route, n in ((ROUTE_TWO_SHOT, (2 * MiB) // 4 + 8 * k), (ROUTE_ONE_SHOT, min(one_cap, 65536) // 4 - 4 * k),
+                             (ROUTE_BASE, 4096 + 8 * k)):
+                if (route != ROUTE_BASE and route not in routes) or n <= 0 or (route == ROUTE_ONE_SHOT and one_cap <= 0):
+                    continue
+                x = _pattern(n, rank, 100 + k, torch.float32, dev)
+                burst.append((route, k, x, n, comm.allreduce_via(x, SUM, route)))
+        for b in burst:
+            b[4].wait()  # (stream order only: no host sync inside the burst)
+        torch.cuda.synchronize(dev)
+        if comm.peer_status() != 0:
+            return False, "a peer kernel timed out (burst)"
+        for route, k, x, n, _ in burst:
+            if not torch.equal(x, _expected(n, world, 100 + k, torch.float32, dev)):
+                bad.append(f"burst call {k} {ROUTE_NAMES[route]} n={n}")
     except RuntimeError as e:
         return False, f"peer route raised: {e}"
     if bad:

@@ -52,6 +52,15 @@ def test_choose_routes_segments_and_ties():
     assert r2 == [1] and len(b2) == 1
 
 
+def test_choose_routes_margin_keeps_near_ties_on_base():
+    """A peer route must beat the base route by ROUTE_MARGIN (10 %): a 5 % gain stays on RCCL."""
+    sizes = [MiB, 25 * MiB]
+    times = {1: [100e-6, 1000e-6], 3: [95e-6, 850e-6]}
+    _, _, winner = cal.choose_routes(sizes, times)
+    assert cal.ROUTE_MARGIN == 0.1
+    assert winner == {MiB: 1, 25 * MiB: 3}
+
+
 def test_probe_sizes_cover_plan():
     plan = bp.xgmi_plan(51 * MiB, 8, alpha_us=30, busbw_gbps=350)
     s = cal.probe_sizes(plan.first_bytes, plan.cap_bytes, plan.tail_bytes, 51 * MiB)
