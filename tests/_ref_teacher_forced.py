@@ -26,6 +26,8 @@ from distributeddataparallel_amd.utils.precision import accurate_fp32_convs  # n
 def main(steps):
     if os.environ.get("XDDP_TEST_ACCURATE_CONVS") == "1":
         accurate_fp32_convs()
+    if os.environ.get("XDDP_TEST_NO_MIOPEN") == "1":  # (diagnosis: PyTorch's native convolutions)
+        torch.backends.cudnn.enabled = False
     dist.init_process_group("rccl", device_id=0)
     torch.manual_seed(0)
     ds = SyntheticImages(length=4096, shape=(3, 32, 32))
