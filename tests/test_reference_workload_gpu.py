@@ -63,10 +63,10 @@ def test_reference_workload_fp32_teacher_forced_50_steps():
     gradients checked against fp64 on the same parameters and batch (tests/_ref_teacher_forced.py):
     the loss of every step within 1e-5, and every gradient — xddp's own kernels' (every BatchNorm
     weight / bias, through the fused BN backward; the fc layer) and the library convs' — within 1e-4
-    in at least 30 of the 50 steps (median step within 1e-4); the worst step is printed. The other steps carry 1e-3 - 2e-1
-    relative errors in a few layers whichever conv implementation runs (MIOpen, MIOpen without its
-    implicit-GEMM solvers, or PyTorch's native convolutions: XDDP_TEST_NO_MIOPEN=1) and with r5's BN
-    kernels alike, and which steps they hit changes from run to run: a ReLU or max-pool decision
+    in at least 30 of the 50 steps (median step within 1e-4); the worst step is printed. The other
+    steps carry 1e-3 - 3e-1 relative errors in a few layers whichever conv implementation runs
+    (MIOpen, MIOpen without its implicit-GEMM solvers, or PyTorch's native convolutions:
+    XDDP_TEST_NO_MIOPEN=1) and with r5's BN kernels alike, and which steps they hit changes from run to run: a ReLU or max-pool decision
     that fp32 and fp64 resolve differently (a near-tie) reroutes a whole gradient path, and the
     library's run-to-run rounding moves which near-ties flip (r6 diagnosis, commit log)."""
     from distributeddataparallel_amd.utils.spawn import free_port
