@@ -1,3 +1,5 @@
 bash scripts/gpu_steps.sh \
- "commtests|600|python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_calibrate_gpu.py tests/test_peer_allreduce_gpu.py tests/test_replicas_gpu.py" \
- "bench_peer2|300|python -u bench.py --gpus 2 --backend peer --model resnet50 --batch-size 64 --steps 10 --warmup 3 --diag-steps 0 --json-out gpurun_out/bench_peer2.json"
+ "gputests|1000|python -u -m pytest -q --timeout 240 --timeout-method thread -m gpu tests" \
+ "smoke|300|python -u -c \"import __graft_entry__ as g; g.smoke()\"" \
+ "r50|240|python -u bench.py --gpus 1 --steps 20 --warmup 5 --json-out gpurun_out/r50.json" \
+ "r50b|240|python -u bench.py --gpus 1 --steps 30 --warmup 10 --json-out gpurun_out/r50b.json"
