@@ -103,8 +103,8 @@ def choose_routes(sizes: Sequence[int], times: Dict[int, Sequence[Optional[float
 
     ``times[route][i]`` = seconds at ``sizes[i]`` (None = route unavailable at that size). A peer
     route wins only below (1 - ROUTE_MARGIN) x the base route's time (ties and near-ties go to the
-    base route; among peer routes, the faster, then the lower route id). Messages up to ``bounds[k]`` bytes take
-    ``routes[k]``; the last bound is open-ended."""
+    base route; among peer routes, the faster, then the lower route id). Messages up to
+    ``bounds[k]`` bytes take ``routes[k]``; the last bound is open-ended."""
     order = sorted(range(len(sizes)), key=lambda i: sizes[i])
     winner: Dict[int, int] = {}
     # a hand-written peer lane replaces the library path only where it is clearly faster: it must
@@ -183,9 +183,9 @@ def self_check(pg, iters: int = 8) -> Tuple[bool, str]:
         # double-buffered slot carry different values), checked only after the whole burst
         burst = []
         for k in range(iters):
-            for route, n in ((ROUTE_TWO_SHOT, (2 * MiB) // 4 + 8 * k), (ROUTE_ONE_SHOT, min(one_cap, 65536) // 4 - 4 * k),
-                             (ROUTE_BASE, 4096 + 8 * k)):
-                if (route != ROUTE_BASE and route not in routes) or n <= 0 or (route == ROUTE_ONE_SHOT and one_cap <= 0):
+            for route, n in ((ROUTE_TWO_SHOT, (2 * MiB) // 4 + 8 * k),
+                             (ROUTE_ONE_SHOT, min(one_cap, 65536) // 4 - 4 * k), (ROUTE_BASE, 4096 + 8 * k)):
+                if (route != ROUTE_BASE and route not in routes) or n <= 0:
                     continue
                 x = _pattern(n, rank, 100 + k, torch.float32, dev)
                 burst.append((route, k, x, n, comm.allreduce_via(x, SUM, route)))
