@@ -320,10 +320,12 @@ def train_flops_per_sample(args):
     from distributeddataparallel_amd import models
 
     try:
+        nb = 1
         with torch.device("meta"):
             if is_conv(args):
                 m = models.SimpleCNN() if args.model == "simplecnn" else getattr(models, args.model)()
-                x = torch.empty(1, *sample_shape(args))
+                nb = 2  # (training-mode BatchNorm needs > 1 value per channel at a 1x1 feature map)
+                x = torch.empty(nb, *sample_shape(args))
             elif args.model.startswith("vit"):
                 m = getattr(models, args.model)()
                 x = torch.empty(1, *sample_shape(args))
@@ -338,7 +340,7 @@ def train_flops_per_sample(args):
                 x = torch.empty(1, *sample_shape(args))
         with FlopCounterMode(display=False) as fc:
             m(x).float().sum().backward()
-        return float(fc.get_total_flops())
+        return float(fc.get_total_flops()) / nb
     except Exception as e:  # noqa: BLE001 — MFU is a diagnostic, never fail the bench over it
         print(f"[bench] flop count failed: {e}", file=sys.stderr)
         return None
