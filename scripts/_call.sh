@@ -1,7 +1,4 @@
 bash scripts/gpu_steps.sh \
- "g_new|200|python -u scripts/gemm1x1_time.py" \
- "g_old|200|cd ab_old && PYTHONPATH=. python -u ../scripts/gemm1x1_time.py" \
- "r_new|200|python -u bench.py --steps 30 --warmup 10 --diag-steps 0 --json-out gpurun_out/r_new.json" \
- "r_old|200|cd ab_old && python -u bench.py --steps 30 --warmup 10 --diag-steps 0 --json-out ../gpurun_out/r_old.json" \
- "r_new2|200|python -u bench.py --steps 30 --warmup 10 --diag-steps 0 --json-out gpurun_out/r_new2.json" \
- "r_old2|200|cd ab_old && python -u bench.py --steps 30 --warmup 10 --diag-steps 0 --json-out ../gpurun_out/r_old2.json"
+ "gputests|1000|python -u -m pytest -q --timeout 240 --timeout-method thread -m gpu tests" \
+ "smoke|300|python -u -c \"import __graft_entry__ as g; g.smoke()\"" \
+ "r50|240|python -u bench.py --gpus 1 --steps 20 --warmup 5 --json-out gpurun_out/r50.json"
