@@ -65,3 +65,16 @@ def test_one_rank_reports_no_comm():
     assert c["avg_backward_compute_ms"] is not None and c["timed_iterations"] >= 2
     assert "allreduce_busbw" not in d and "warning" not in d
     assert d["buckets"]["tail"]["exposed_tail_us_model"] == 0.0
+
+
+def test_flop_count_per_sample_matches_survey():
+    """bench.py's MFU denominator: model FLOPs of one forward + backward per sample on the meta device
+    (~0.22 GFLOP for the reference ResNet-18 at 32x32; ResNet-50 at 224: 3 x ~8.1)."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    ref = bench.train_flops_per_sample(bench.parse(["--model", "simplecnn", "--image-size", "32",
+                                                    "--batch-size", "32"]))
+    r50 = bench.train_flops_per_sample(bench.parse(["--model", "resnet50"]))
+    assert ref is not None and 0.20e9 < ref < 0.24e9
+    assert r50 is not None and 23e9 < r50 < 26e9
